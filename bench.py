@@ -1,0 +1,303 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X LBVH build + ray-traversal path.
+
+Metric (BASELINE.json): Mrays/s, primary + 1 reflection bounce; BVH build Mtris/s;
+at 1/2/4/8 GPUs.  Default workload = BASELINE config C5: 10M
+synthetic triangles (splitmix64 seed 0x5EED0005, box x,y +-100, z +-50), a
+3840x2160 frame, primary rays + 1 bounce.  Multi-GPU: every rank holds the same
+scene and builds the same BVH (replicas, deterministic); the frame is split in
+8-row bands dealt round-robin to the ranks, and the bands are gathered to rank 0
+over RCCL (torch.distributed "nccl") and assembled into the frame.
+
+One step = trace of this rank's bands (primary kernel + bounce kernel) + the
+RCCL gather + assembly on rank 0.  The BVH is built once before the timed loop
+(the scene is static; replicated build throughput is measured separately and
+reported under "build").  value = all rays of the frame (W*H primary + every
+live bounce ray, summed over ranks) / max-over-ranks time per step.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c3]
+       (N > 1 under `torch.distributed.run --nproc-per-node N`).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_HBM_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# algorithmic bytes of OUR layout (DESIGN.md "Byte model"), per unit
+B_INTERNAL_VISIT = 64            # one 64-B child-pair record
+B_LEAF_VISIT = 48                # one 48-B clip-space triangle record
+B_HIT_SHADE = 48 + 12 + 96 + 4 + 68   # leaf re-read, 3 indices, 3 vertices, matIndex, material
+B_PRIMARY_OUT = 16               # color
+B_QUEUE = 32                     # one bounce-queue entry (write by primary, read by bounce)
+B_BOUNCE_RMW = 32                # color read + write
+B_BUILD_PER_TRI = 392            # DESIGN.md "Byte model": build kernels' algorithmic bytes per triangle
+
+WORKLOADS = {
+    "c5": dict(name="C5: synthetic 10M tris (seed 0x5EED0005, box 100x100x50), 3840x2160, primary+1 bounce",
+               ntris=10_000_000, seed=0x5EED0005, half=(100.0, 100.0, 50.0), W=3840, H=2160, bounces=1),
+    "c3": dict(name="C3: Obj/Test.obj (1952 tris), 1920x1080, primary+1 bounce", obj="Test", W=1920, H=1080,
+               bounces=1),
+}
+
+
+def log(msg):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def make_scene(rt, wl):
+    if "obj" in wl:
+        return rt.load_npz(os.path.join(REPO, "tests", "golden", "scenes", wl["obj"] + ".npz"))
+    return rt.synthetic(wl["ntris"], seed=wl["seed"], half_extent=wl["half"])
+
+
+def trace_bytes(st, pass_idx, rays_in, rays_live_out):
+    v_int, v_leaf, hits = st["internal_visits"][pass_idx], st["leaf_visits"][pass_idx], st["hits"][pass_idx]
+    b = B_INTERNAL_VISIT * v_int + B_LEAF_VISIT * v_leaf + B_HIT_SHADE * hits
+    if pass_idx == 0:
+        b += B_PRIMARY_OUT * rays_in + B_QUEUE * rays_live_out
+    else:
+        b += (B_QUEUE + B_BOUNCE_RMW) * rays_in
+    return b
+
+
+def load_pmc(workload, kernel):
+    path = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def cpu_baseline(rt, scene, ctx, wl, W, H):
+    """Oracle (single-thread C++ restatement of the reference path) on a bounded sample."""
+    from oracle import lib as orc
+    wvp, wv = rt.camera_reference(W, H)
+    nodes = ctx.read_bvh()
+    osc = orc.Scene(scene.vertices, scene.indices, scene.mat_indices, scene.material_blob)
+    step = 8 if W * H > 4_000_000 else 4
+    t0 = time.perf_counter()
+    _, _, st = orc.trace(osc, nodes, wvp, wv, W, H, wl["bounces"], 0, H, step)
+    dt = time.perf_counter() - t0
+    rays = st["primary"] + st["bounce"]
+    res = {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+           "sample": f"oracle/liboracle.so orc_trace of every {step}th row of the same frame and BVH "
+                     f"({st['primary']} primary + {st['bounce']} bounce rays, {dt:.1f} s, 1 thread)"}
+    # build baseline: reference-faithful 32 x 1-bit split sort + Karras + refit on a 1M-triangle sample
+    n_s = 1_000_000
+    sub = rt.Scene(scene.vertices[: 3 * n_s], scene.indices[: 3 * n_s], scene.mat_indices[:n_s], scene.materials)
+    if "obj" in wl:
+        sub = scene
+    osub = orc.Scene(sub.vertices, sub.indices, sub.mat_indices, sub.material_blob)
+    t0 = time.perf_counter()
+    orc.build(osub, wvp, sort_mode=0)
+    dt = time.perf_counter() - t0
+    res["build_mtris_s"] = sub.num_tris / dt / 1e6
+    res["build_sample"] = f"orc_build (32 split passes + Karras + refit) on {sub.num_tris} triangles, {dt:.2f} s, 1 thread"
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
+    ap.add_argument("--build-iters", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C4 build / C3 side measurements")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    import raytracebvh_amd as rt
+
+    wl = WORKLOADS[args.workload]
+    W, H, bounces = wl["W"], wl["H"], wl["bounces"]
+    t_setup = time.perf_counter()
+    scene = make_scene(rt, wl)
+    stream = torch.cuda.current_stream(dev)
+    ctx = rt.Context(device=local, flags=rt.FLAG_TIMING, stream=stream.cuda_stream)
+    ctx.set_scene(scene)
+    wvp, wv = rt.camera_reference(W, H)
+    ctx.set_camera(wvp, wv)
+    log(f"scene {scene.num_tris} tris ready in {time.perf_counter() - t_setup:.1f}s (rank {rank}/{world})")
+
+    # ---- BVH build (replicated on every rank), hipEvent-timed
+    ctx.build()
+    ctx.build()
+    ctx.reset_stats()
+    for _ in range(args.build_iters):
+        ctx.build(sync=False)
+    ctx.synchronize()
+    bst = ctx.stats()
+    build = {"workload": f"{scene.num_tris} tris (bench scene)", "ms": bst["ms_build"],
+             "mtris_s": scene.num_tris / (bst["ms_build"] * 1e-3) / 1e6,
+             "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
+                                   [round(x, 4) for x in bst["ms_stage"][:5]]))}
+
+    # ---- band buffers + gather plumbing
+    L = rt.lib()
+    rows = [L.rtbvh_band_rows(H, r, world) for r in range(world)]
+    max_rows = max(rows)
+    band = torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev)
+    frame = band if world == 1 else None
+    gather_list, row_idx = None, None
+    if world > 1 and rank == 0:
+        frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+        gather_list = [torch.empty_like(band) for _ in range(world)]
+        row_idx = []
+        for r in range(world):
+            ys = [y for b in range(r, (H + 7) // 8, world) for y in range(8 * b, min(8 * b + 8, H))]
+            row_idx.append(torch.tensor(ys, dtype=torch.long, device=dev))
+
+    def step():
+        ctx.trace_band_async(W, H, bounces, rank, world, band.data_ptr())
+        if world > 1:
+            dist.gather(band, gather_list if rank == 0 else None, dst=0)
+            if rank == 0:
+                for r in range(world):
+                    frame.index_copy_(0, row_idx[r], gather_list[r][: rows[r]])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    st = ctx.stats()
+    rays_local = st["primary_rays"] + st["bounce_rays"]
+    live_local = st["bounce_rays"]
+    tot = torch.tensor([rays_local, live_local], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    rays_per_step = float(tot[0].item())
+
+    # ---- timed region
+    ctx.reset_stats()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    tst = ctx.stats()   # hipEvent averages of the primary / bounce kernels over the timed steps
+    ms_step = elapsed / args.steps * 1e3
+    value = rays_per_step / (ms_step * 1e-3) / 1e6
+
+    # ---- visit counts for the byte model (one extra, untimed trace of this rank's bands)
+    ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_COUNT_VISITS)
+    ctx.reset_stats()
+    ctx.trace_band_async(W, H, bounces, rank, world, band.data_ptr())
+    cst = ctx.stats()
+    ctx.set_flags(rt.FLAG_TIMING)
+    kern = {}
+    prim_rays = cst["primary_rays"]
+    live = cst["bounce_rays"]
+    kern["k_primary"] = dict(ms=tst["ms_stage"][5], bytes=trace_bytes(cst, 0, prim_rays, live))
+    if bounces:
+        kern["k_bounce"] = dict(ms=tst["ms_stage"][6], bytes=trace_bytes(cst, 1, live, 0))
+    dom = max(kern, key=lambda k: kern[k]["ms"])
+    for k, v in kern.items():
+        v["achieved_gbs"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
+    traffic = load_pmc(args.workload, dom)
+    roofline = {"bound": "hbm", "achieved": round(kern[dom]["achieved_gbs"], 1), "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": round(kern[dom]["achieved_gbs"] / PEAK_HBM_GBS, 4),
+                "traffic": traffic, "kernel": dom, "kernel_ms": round(kern[dom]["ms"], 4),
+                "algorithmic_bytes": int(kern[dom]["bytes"])}
+
+    result = None
+    if rank == 0:
+        extras = {}
+        if world == 1 and not args.no_extras and args.workload == "c5":
+            # C4: 10M synthetic (seed 0x5EED0004, +-50) build only; C3: Test.obj 1080p primary+1 bounce
+            c4 = rt.synthetic(10_000_000, seed=0x5EED0004, half_extent=(50.0, 50.0, 50.0))
+            with rt.Context(device=local, flags=rt.FLAG_TIMING) as c:
+                c.set_scene(c4)
+                c.set_camera(*rt.camera_reference(1920, 1080))
+                c.build()
+                c.reset_stats()
+                for _ in range(args.build_iters):
+                    c.build(sync=False)
+                c.synchronize()
+                s4 = c.stats()
+            extras["c4_build"] = {"mtris_s": round(10_000_000 / (s4["ms_build"] * 1e-3) / 1e6, 1),
+                                  "ms": round(s4["ms_build"], 4),
+                                  "achieved_gbs": round(B_BUILD_PER_TRI * 1e7 / (s4["ms_build"] * 1e-3) / 1e9, 1),
+                                  "stages_ms": [round(x, 4) for x in s4["ms_stage"][:5]]}
+            del c4
+            s3 = make_scene(rt, WORKLOADS["c3"])
+            with rt.Context(device=local, flags=rt.FLAG_TIMING) as c:
+                c.set_scene(s3)
+                c.set_camera(*rt.camera_reference(1920, 1080))
+                c.compute_bvh(1920, 1080, 1)
+                q = c.stats()
+                c.reset_stats()
+                t0 = time.perf_counter()
+                for _ in range(50):
+                    c.compute_bvh(1920, 1080, 1)
+                dt = (time.perf_counter() - t0) / 50
+                q2 = c.stats()
+            r3 = q["primary_rays"] + q["bounce_rays"]
+            extras["c3_frame"] = {"mrays_s_trace": round(r3 / (q2["ms_trace"] * 1e-3) / 1e6, 1),
+                                  "mrays_s_build_plus_trace_wall": round(r3 / dt / 1e6, 1),
+                                  "ms_build": round(q2["ms_build"], 4), "ms_trace": round(q2["ms_trace"], 4)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline (oracle, bounded sample) ...")
+            cpu = cpu_baseline(rt, scene, ctx, wl, W, H)
+        result = {
+            "metric": "Mrays/s primary+1-bounce (C5 frame); BVH build Mtris/s under build",
+            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (splitmix64 generator, SURVEY §8(d))" if "obj" not in wl else "Obj/Test.obj fixture",
+            "config": {"workload": wl["name"], "width": W, "height": H, "bounces": bounces,
+                       "triangles": scene.num_tris, "rays_per_step": int(rays_per_step),
+                       "parallelism": f"image bands x{world} + RCCL gather" if world > 1 else "single GPU"},
+            "roofline": roofline,
+            "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                        for k, v in kern.items()},
+            "visits": {"internal": cst["internal_visits"], "leaf": cst["leaf_visits"], "hits": cst["hits"]},
+            "build": build,
+            "cpu_baseline": cpu,
+        }
+        result.update(extras)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

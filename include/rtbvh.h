@@ -1,0 +1,234 @@
+/*
+ * rtbvh.h -- C ABI of librtbvh.so, the MI355X (gfx950) LBVH build + ray traversal path.
+ *
+ * Drop-in boundary for the reference's GPU hot path (Fierykev/RayTraceBVH).  The
+ * reference has no plugin API: the whole path is the private member
+ * Graphics::computeBVH() (Graphics.cpp:667-831), fed through a D3D12 binding
+ * contract (RayTraceGlobal.hlsl:87-120, Graphics.h:50-83, Graphics.cpp:293-303)
+ * by Graphics::onUpdate() (Graphics.cpp:40-61) with inputs produced by
+ * ObjLoader (ObjectFileLoader.h:120-240).  Each entry point below names the
+ * reference interface it replaces.  See INTEGRATION.md for the binding a
+ * maintainer adds on the reference side.
+ *
+ * Conventions: plain pointers and sizes only, no C++ or torch types.  A context
+ * is single-thread affine and owns one HIP stream (or uses the caller's) and
+ * every device buffer it allocates.  Input arrays are owned by the caller and
+ * copied on the call.  Calls never throw; they return rtbvh_status and leave a
+ * message for rtbvh_last_error().  All calls are synchronous unless the name
+ * says `_async` (those only enqueue on the context stream).
+ */
+#ifndef RTBVH_H
+#define RTBVH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTBVH_ABI_VERSION 1
+
+typedef enum {
+    RTBVH_OK = 0,
+    RTBVH_ERR_INVALID_ARG = 1,
+    RTBVH_ERR_HIP = 2,            /* a HIP runtime call failed (message has the HIP error) */
+    RTBVH_ERR_OOM = 3,
+    RTBVH_ERR_NOT_READY = 4,      /* e.g. trace before build, build before set_scene */
+    RTBVH_ERR_STACK_OVERFLOW = 5, /* a traversal stack overflowed (never for a clz64 tree) */
+    RTBVH_ERR_IO = 6,             /* scene file could not be read / parsed */
+    RTBVH_ERR_NO_DEVICE = 7
+} rtbvh_status;
+
+/* ---- data layouts (byte-identical to the reference's HLSL structs) -------- */
+
+/* Vertex, RayTraceGlobal.hlsl:53-58 / ObjectFileLoader.h:98-103 (32 B) */
+typedef struct {
+    float position[3];
+    float normal[3];
+    float texcoord[2];
+} rtbvh_vertex;
+
+/* Material as uploaded, RayTraceGlobal.hlsl:60-72 / MaterialUpload ObjectFileLoader.h:79-96 (68 B) */
+typedef struct {
+    float ambient[4];
+    float diffuse[4];
+    float specular[4];
+    float shininess;
+    float optical_density;
+    float alpha;
+    uint32_t specularb; /* HLSL bool = 4 bytes */
+    int32_t tex_num;    /* -1 = untextured */
+} rtbvh_material;
+
+/* Node, RayTraceGlobal.hlsl:39-51 / Graphics.h:157-169 (44 B).  Export layout
+ * of rtbvh_read_bvh: leaves [0,n), internal node k at n+k, root at n.
+ * parent of the root and child_l/child_r of leaves = 0xFFFFFFFF; internal
+ * nodes have code = 0 and index = 0 (the reference leaves sort scratch there). */
+typedef struct {
+    uint32_t parent, child_l, child_r, code;
+    float bb_min[3], bb_max[3];
+    uint32_t index; /* 3 * triangle id, for leaves */
+} rtbvh_node;
+
+/* RayPresent, RayTraceGlobal.hlsl:30-35 (56 B) */
+typedef struct {
+    float intensity;
+    float origin[3], direction[3], inv_direction[3];
+    float color[4];
+} rtbvh_ray_present;
+
+/* An RGBA8 texture (sRGB encoded, as the reference's R8G8B8A8_UNORM_SRGB, Image.cpp:9) */
+typedef struct {
+    uint32_t width, height;
+    const uint8_t* rgba8; /* width*height*4 bytes, row 0 = first row of the image */
+} rtbvh_texture;
+
+enum {
+    RTBVH_MORTON_CPUTESTS = 0, /* ShaderSim/main.cpp:292-301: object-space centroid, mesh AABB, x<<2|y<<1|z (default) */
+    RTBVH_MORTON_HLSL = 1      /* MortonCodes.hlsl:70-106: clip-space, avg=bbMin/3, config scene box, x|y<<1|z<<2 */
+};
+enum {
+    RTBVH_DELTA_CLZ64 = 0,   /* BVHConstructP1.hlsl:61-72: clz, ties 32 + clz(i^j) (default, always valid) */
+    RTBVH_DELTA_CPUTESTS = 1 /* RadixBVHCombo/main.cpp:136-151: ties clz(i^j), De Bruijn quirks */
+};
+enum {
+    RTBVH_FLAG_TIMING = 1u << 0,         /* record per-stage hipEvent times (rtbvh_get_stats) */
+    RTBVH_FLAG_COUNT_VISITS = 1u << 1,   /* count traversal visits (slower; for the byte model) */
+    RTBVH_FLAG_REFRACT_RECORDS = 1u << 2 /* also build refractRay records (RayTraceLaunch.hlsl:70-80) */
+};
+
+typedef struct {
+    int32_t device;          /* HIP device ordinal */
+    uint32_t morton_mode;    /* RTBVH_MORTON_* */
+    uint32_t delta_mode;     /* RTBVH_DELTA_* */
+    uint32_t flags;          /* RTBVH_FLAG_* */
+    float scene_bb_min[3];   /* MORTON_HLSL only: cbuffer sceneBBMin (Graphics.cpp:529 uses -700) */
+    float scene_bb_max[3];   /* MORTON_HLSL only: cbuffer sceneBBMax (Graphics.cpp:528 uses +700) */
+    void* stream;            /* hipStream_t to use, or NULL: the context creates its own */
+} rtbvh_config;
+
+typedef struct {
+    uint32_t num_tris, num_nodes, width, height;
+    uint64_t primary_rays, bounce_rays;        /* rays traced by the last trace */
+    /* RTBVH_FLAG_COUNT_VISITS only, last trace; [0] = primary pass, [1] = bounce passes */
+    uint64_t internal_visits[2], leaf_visits[2], hits[2];
+    uint64_t textured_hits, stack_overflows;
+    /* RTBVH_FLAG_TIMING only: hipEvent averages over the builds / traces enqueued on
+     * the context stream since rtbvh_reset_stats (the most recent 32 of each) */
+    uint32_t timed_builds, timed_traces;
+    float ms_build, ms_trace;
+    float ms_stage[8];   /* bounds, morton, sort, leaf+karras, refit, primary, bounce, - */
+} rtbvh_stats;
+typedef struct rtbvh_ctx rtbvh_ctx;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+/* Fills cfg with defaults (device 0, CPUTests Morton, clz64 delta, +-700 box). */
+void rtbvh_config_default(rtbvh_config* cfg);
+/* Replaces Graphics::onInit/loadPipeline device + queue creation (Graphics.cpp:34-38,110-235). */
+rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out);
+/* Replaces Graphics::onDestroy (Graphics.cpp:94-103). NULL is a no-op. */
+void rtbvh_destroy(rtbvh_ctx* ctx);
+/* Last error message of this context (or of the last failed rtbvh_create when ctx == NULL). */
+const char* rtbvh_last_error(const rtbvh_ctx* ctx);
+int rtbvh_abi_version(void);
+
+/* ---- inputs (the binding contract, RayTraceGlobal.hlsl:87-120) ------------ */
+/* SRV t0 verts, t1 indices, t2 matIndices, t3 materials, t4.. textures:
+ * replaces ObjLoader::UploadData (ObjectFileLoader.cpp:549-624).  nidx must be
+ * a positive multiple of 3; mat_idx has nidx/3 entries; textures may be NULL. */
+rtbvh_status rtbvh_set_scene(rtbvh_ctx* ctx, const rtbvh_vertex* verts, uint32_t nverts,
+                             const uint32_t* indices, uint32_t nidx, const uint32_t* mat_idx,
+                             const rtbvh_material* mats, uint32_t nmats,
+                             const rtbvh_texture* textures, uint32_t ntex);
+/* cbuffer WORLD_POS (b0) {WVP, WV}: replaces the CB write in Graphics::onUpdate
+ * (Graphics.cpp:50-53).  Row-major 4x4, row-vector convention (p' = [p 1] * M),
+ * i.e. the DirectXMath matrices BEFORE the transpose for HLSL packing. */
+rtbvh_status rtbvh_set_camera(rtbvh_ctx* ctx, const float wvp[16], const float wv[16]);
+
+/* ---- the hot path (Graphics::computeBVH, Graphics.cpp:667-831) ------------ */
+/* MortonCodes -> radix sort -> BVHConstructP1 -> BVHConstructP2 (Graphics.cpp:705-782). */
+rtbvh_status rtbvh_build(rtbvh_ctx* ctx);
+rtbvh_status rtbvh_build_async(rtbvh_ctx* ctx);
+/* RayTraceLaunch + `bounces` x RayTraceReflection (Graphics.cpp:785-810) at W x H. */
+rtbvh_status rtbvh_trace(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces);
+rtbvh_status rtbvh_trace_async(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces);
+/* The whole computeBVH: build + trace (Graphics.cpp:667-831). */
+rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces);
+/* Image-tile shard for multi-GPU (no reference equivalent): trace
+ * only the 8-row bands b with b % nranks == rank of a W x H frame and write them
+ * compacted (band order) as RGBA f32 into dev_out (device memory, at least
+ * rtbvh_band_rows(H, rank, nranks) * W * 4 floats), enqueued on `stream`
+ * (hipStream_t, NULL = the context stream).  The caller gathers the shards. */
+rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces,
+                                    uint32_t rank, uint32_t nranks, float* dev_out, void* stream);
+uint32_t rtbvh_band_rows(uint32_t height, uint32_t rank, uint32_t nranks);
+rtbvh_status rtbvh_synchronize(rtbvh_ctx* ctx);
+
+/* ---- outputs --------------------------------------------------------------- */
+/* reflectRay[].color, the framebuffer of record (RayTraceBVHPS.hlsl:13-16): W*H*4 floats, row y at y*W. */
+rtbvh_status rtbvh_read_framebuffer(rtbvh_ctx* ctx, float* rgba);
+/* Final reflectRay[].intensity per pixel (W*H floats). */
+rtbvh_status rtbvh_read_intensity(rtbvh_ctx* ctx, float* intensity);
+/* Device pointer of the W*H*4-float framebuffer (valid until the next trace/destroy). */
+const float* rtbvh_framebuffer_device(rtbvh_ctx* ctx);
+/* BVHTree UAV u0 in the reference layout (2n-1 nodes, see rtbvh_node). */
+rtbvh_status rtbvh_read_bvh(rtbvh_ctx* ctx, rtbvh_node* out, uint32_t capacity);
+/* Per-triangle Morton codes in triangle order (MortonCodes.hlsl:104-112). */
+rtbvh_status rtbvh_read_morton(rtbvh_ctx* ctx, uint32_t* codes);
+/* Stable radix order: sorted codes and the triangle id of each sorted position. */
+rtbvh_status rtbvh_read_sorted(rtbvh_ctx* ctx, uint32_t* sorted_codes, uint32_t* tri_ids);
+/* refractRay records (RTBVH_FLAG_REFRACT_RECORDS) and reflectRay records of the last trace. */
+rtbvh_status rtbvh_read_rays(rtbvh_ctx* ctx, rtbvh_ray_present* reflect_out, rtbvh_ray_present* refract_out);
+rtbvh_status rtbvh_get_stats(rtbvh_ctx* ctx, rtbvh_stats* out);
+/* Restart the timing averages of rtbvh_get_stats. */
+rtbvh_status rtbvh_reset_stats(rtbvh_ctx* ctx);
+/* Replace the RTBVH_FLAG_* bits of the context (takes effect for the next build/trace). */
+rtbvh_status rtbvh_set_flags(rtbvh_ctx* ctx, uint32_t flags);
+
+/* ---- primitives (exposed for tests and callers with their own buffers) ---- */
+/* Stable LSD radix sort of (key, value) pairs, 8-bit digits over bits [0, key_bits).
+ * Device pointers; keys/vals_in may be overwritten (ping-pong); the sorted
+ * result lands in keys_out/vals_out.  Enqueued on the context stream. */
+rtbvh_status rtbvh_sort_pairs_async(rtbvh_ctx* ctx, uint32_t* keys_in, uint32_t* vals_in,
+                                    uint32_t* keys_out, uint32_t* vals_out, uint32_t n,
+                                    uint32_t key_bits);
+/* Host-memory convenience wrapper of the above (synchronous). */
+rtbvh_status rtbvh_sort_pairs_host(rtbvh_ctx* ctx, const uint32_t* keys, const uint32_t* vals,
+                                   uint32_t* keys_out, uint32_t* vals_out, uint32_t n, uint32_t key_bits);
+/* Karras + refit on caller-given sorted codes and leaf boxes (host arrays; leaf
+ * boxes n x 6 floats {min xyz, max xyz}); writes 2n-1 nodes (reference layout).
+ * Lets the build kernels be checked on the reference's own RadixBVHCombo data. */
+rtbvh_status rtbvh_build_from_codes(rtbvh_ctx* ctx, const uint32_t* sorted_codes,
+                                    const float* leaf_boxes, uint32_t n, rtbvh_node* out);
+
+/* ---- host-side scene helpers (ObjLoader replacement, camera) ---------------- */
+typedef struct rtbvh_scene rtbvh_scene;
+/* ObjLoader::Load (ObjectFileLoader.cpp:212-547) incl. its de-duplication rules. */
+rtbvh_status rtbvh_scene_load_obj(const char* path, rtbvh_scene** out);
+/* Synthetic random triangles: splitmix64(seed), centroids uniform
+ * in [-half,+half], vertex offsets (u-0.5)*1.0, face normals, one material. */
+rtbvh_status rtbvh_scene_synthetic(uint64_t seed, uint32_t ntris, const float half_extent[3],
+                                   rtbvh_scene** out);
+void rtbvh_scene_free(rtbvh_scene* s);
+uint32_t rtbvh_scene_num_vertices(const rtbvh_scene* s);
+uint32_t rtbvh_scene_num_indices(const rtbvh_scene* s);
+uint32_t rtbvh_scene_num_materials(const rtbvh_scene* s);
+uint32_t rtbvh_scene_num_textures(const rtbvh_scene* s);
+const rtbvh_vertex* rtbvh_scene_vertices(const rtbvh_scene* s);
+const uint32_t* rtbvh_scene_indices(const rtbvh_scene* s);
+const uint32_t* rtbvh_scene_mat_indices(const rtbvh_scene* s);
+const rtbvh_material* rtbvh_scene_materials(const rtbvh_scene* s);
+/* texture path of texture k (as named by map_Kd), or NULL */
+const char* rtbvh_scene_texture_path(const rtbvh_scene* s, uint32_t k);
+/* Upload a loaded scene (set_scene with the scene's arrays; textures as given). */
+rtbvh_status rtbvh_set_scene_obj(rtbvh_ctx* ctx, const rtbvh_scene* s, const rtbvh_texture* textures,
+                                 uint32_t ntex);
+/* Graphics::onUpdate's camera (Graphics.cpp:44-53, Graphics.h:200-204):
+ * LookAtLH(eye (0,5,-100), at 0, up +y) * PerspectiveFovLH(pi/4, H/W, 0.1, 1000). */
+void rtbvh_camera_reference(uint32_t width, uint32_t height, float wvp[16], float wv[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTBVH_H */

@@ -1,0 +1,155 @@
+"""ctypes binding of librtbvh.so (the C ABI in include/rtbvh.h).
+
+The product path is the HIP library; there is no CPU fallback.  If the shared
+library has not been built this module raises at import time.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtbvh.so")
+
+OK, ERR_INVALID_ARG, ERR_HIP, ERR_OOM, ERR_NOT_READY, ERR_STACK_OVERFLOW, ERR_IO, ERR_NO_DEVICE = range(8)
+MORTON_CPUTESTS, MORTON_HLSL = 0, 1
+DELTA_CLZ64, DELTA_CPUTESTS = 0, 1
+FLAG_TIMING, FLAG_COUNT_VISITS, FLAG_REFRACT_RECORDS = 1, 2, 4
+
+# every symbol include/rtbvh.h declares (tests check the library exports them all)
+EXPORTS = [
+    "rtbvh_config_default", "rtbvh_create", "rtbvh_destroy", "rtbvh_last_error", "rtbvh_abi_version",
+    "rtbvh_set_scene", "rtbvh_set_camera", "rtbvh_build", "rtbvh_build_async", "rtbvh_trace",
+    "rtbvh_trace_async", "rtbvh_compute_bvh", "rtbvh_trace_band_async", "rtbvh_band_rows",
+    "rtbvh_synchronize", "rtbvh_read_framebuffer", "rtbvh_read_intensity", "rtbvh_framebuffer_device",
+    "rtbvh_read_bvh", "rtbvh_read_morton", "rtbvh_read_sorted", "rtbvh_read_rays", "rtbvh_get_stats",
+    "rtbvh_reset_stats", "rtbvh_set_flags",
+    "rtbvh_sort_pairs_async", "rtbvh_sort_pairs_host", "rtbvh_build_from_codes", "rtbvh_scene_load_obj",
+    "rtbvh_scene_synthetic", "rtbvh_scene_free", "rtbvh_scene_num_vertices", "rtbvh_scene_num_indices",
+    "rtbvh_scene_num_materials", "rtbvh_scene_num_textures", "rtbvh_scene_vertices", "rtbvh_scene_indices",
+    "rtbvh_scene_mat_indices", "rtbvh_scene_materials", "rtbvh_scene_texture_path", "rtbvh_set_scene_obj",
+    "rtbvh_camera_reference",
+]
+
+NODE_DTYPE = np.dtype([("parent", "<u4"), ("child_l", "<u4"), ("child_r", "<u4"), ("code", "<u4"),
+                       ("bb_min", "<f4", (3,)), ("bb_max", "<f4", (3,)), ("index", "<u4")])
+MATERIAL_DTYPE = np.dtype([("ambient", "<f4", (4,)), ("diffuse", "<f4", (4,)), ("specular", "<f4", (4,)),
+                           ("shininess", "<f4"), ("optical_density", "<f4"), ("alpha", "<f4"),
+                           ("specularb", "<u4"), ("tex_num", "<i4")])
+assert NODE_DTYPE.itemsize == 44 and MATERIAL_DTYPE.itemsize == 68
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("morton_mode", ctypes.c_uint32), ("delta_mode", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("scene_bb_min", ctypes.c_float * 3),
+                ("scene_bb_max", ctypes.c_float * 3), ("stream", ctypes.c_void_p)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("num_tris", ctypes.c_uint32), ("num_nodes", ctypes.c_uint32), ("width", ctypes.c_uint32),
+                ("height", ctypes.c_uint32), ("primary_rays", ctypes.c_uint64), ("bounce_rays", ctypes.c_uint64),
+                ("internal_visits", ctypes.c_uint64 * 2), ("leaf_visits", ctypes.c_uint64 * 2),
+                ("hits", ctypes.c_uint64 * 2), ("textured_hits", ctypes.c_uint64),
+                ("stack_overflows", ctypes.c_uint64), ("timed_builds", ctypes.c_uint32),
+                ("timed_traces", ctypes.c_uint32), ("ms_build", ctypes.c_float), ("ms_trace", ctypes.c_float),
+                ("ms_stage", ctypes.c_float * 8)]
+
+    def as_dict(self) -> dict:
+        d = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            d[k] = list(v) if hasattr(v, "__len__") else v
+        return d
+
+
+class RtbvhError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"rtbvh status {status}: {msg}")
+        self.status = status
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(there is no CPU fallback for the HIP path)")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7, NEEDED by torch as "libamdhip64.so").  Loading torch first
+    # makes librtbvh.so's NEEDED libamdhip64.so.7 bind to that same runtime; the
+    # other order maps two runtimes and torch then sees no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    sig = {
+        "rtbvh_config_default": (None, [ctypes.POINTER(Config)]),
+        "rtbvh_create": (i32, [ctypes.POINTER(Config), ctypes.POINTER(vp)]),
+        "rtbvh_destroy": (None, [vp]),
+        "rtbvh_last_error": (ctypes.c_char_p, [vp]),
+        "rtbvh_abi_version": (i32, []),
+        "rtbvh_set_scene": (i32, [vp, vp, u32, vp, u32, vp, vp, u32, vp, u32]),
+        "rtbvh_set_camera": (i32, [vp, vp, vp]),
+        "rtbvh_build": (i32, [vp]),
+        "rtbvh_build_async": (i32, [vp]),
+        "rtbvh_trace": (i32, [vp, u32, u32, u32]),
+        "rtbvh_trace_async": (i32, [vp, u32, u32, u32]),
+        "rtbvh_compute_bvh": (i32, [vp, u32, u32, u32]),
+        "rtbvh_trace_band_async": (i32, [vp, u32, u32, u32, u32, u32, vp, vp]),
+        "rtbvh_band_rows": (u32, [u32, u32, u32]),
+        "rtbvh_synchronize": (i32, [vp]),
+        "rtbvh_read_framebuffer": (i32, [vp, vp]),
+        "rtbvh_read_intensity": (i32, [vp, vp]),
+        "rtbvh_framebuffer_device": (vp, [vp]),
+        "rtbvh_read_bvh": (i32, [vp, vp, u32]),
+        "rtbvh_read_morton": (i32, [vp, vp]),
+        "rtbvh_read_sorted": (i32, [vp, vp, vp]),
+        "rtbvh_read_rays": (i32, [vp, vp, vp]),
+        "rtbvh_get_stats": (i32, [vp, ctypes.POINTER(Stats)]),
+        "rtbvh_reset_stats": (i32, [vp]),
+        "rtbvh_set_flags": (i32, [vp, u32]),
+        "rtbvh_sort_pairs_async": (i32, [vp, vp, vp, vp, vp, u32, u32]),
+        "rtbvh_sort_pairs_host": (i32, [vp, vp, vp, vp, vp, u32, u32]),
+        "rtbvh_build_from_codes": (i32, [vp, vp, vp, u32, vp]),
+        "rtbvh_scene_load_obj": (i32, [ctypes.c_char_p, ctypes.POINTER(vp)]),
+        "rtbvh_scene_synthetic": (i32, [u64, u32, vp, ctypes.POINTER(vp)]),
+        "rtbvh_scene_free": (None, [vp]),
+        "rtbvh_scene_num_vertices": (u32, [vp]),
+        "rtbvh_scene_num_indices": (u32, [vp]),
+        "rtbvh_scene_num_materials": (u32, [vp]),
+        "rtbvh_scene_num_textures": (u32, [vp]),
+        "rtbvh_scene_vertices": (vp, [vp]),
+        "rtbvh_scene_indices": (vp, [vp]),
+        "rtbvh_scene_mat_indices": (vp, [vp]),
+        "rtbvh_scene_materials": (vp, [vp]),
+        "rtbvh_scene_texture_path": (ctypes.c_char_p, [vp, u32]),
+        "rtbvh_set_scene_obj": (i32, [vp, vp, vp, u32]),
+        "rtbvh_camera_reference": (None, [u32, u32, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def ptr(a: np.ndarray):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to librtbvh must be C-contiguous"
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def check(status: int, ctx=None) -> None:
+    if status != OK:
+        msg = lib().rtbvh_last_error(ctx)
+        raise RtbvhError(status, msg.decode() if msg else "")

@@ -1,0 +1,638 @@
+// api.hip -- the C ABI of librtbvh.so (include/rtbvh.h): context, device
+// buffers, stream ordering and the host sequence of Graphics::computeBVH
+// (Graphics.cpp:667-831), re-done as one HIP stream of kernels with no per-frame
+// queue/allocator/fence creation and no host round trip inside build or trace.
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rtbvh.h"
+#include "rtbvh_internal.h"
+
+using namespace rtbvh;
+
+struct rtbvh_ctx {
+    rtbvh_config cfg{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+
+    // scene (set_scene)
+    uint32_t V = 0, T = 0, nmat = 0;
+    float4* d_opos = nullptr;
+    float* d_verts = nullptr;
+    uint32_t* d_idx = nullptr;
+    uint32_t* d_matidx = nullptr;
+    Mat* d_mats = nullptr;
+    float wvp[16], wv[16];
+    bool have_scene = false, have_camera = false, built = false;
+
+    // build buffers (capacity cap_T)
+    uint32_t cap_T = 0;
+    uint32_t *d_codes = nullptr, *d_ids = nullptr, *d_ka = nullptr, *d_va = nullptr, *d_kb = nullptr, *d_vb = nullptr;
+    uint32_t* d_sort_scratch = nullptr;
+    float4 *d_tclip = nullptr, *d_leaf = nullptr;
+    Inner* d_inner = nullptr;
+    uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr, *d_bounds = nullptr;
+    float* d_rootbox = nullptr;
+    SortResult sorted{nullptr, nullptr};
+
+    // trace buffers (capacity cap_P pixels)
+    size_t cap_P = 0;
+    uint32_t W = 0, H = 0, bounces = 0, rank = 0, nranks = 1;
+    float4* d_color = nullptr;
+    float* d_intensity = nullptr;
+    RayQ* d_q[2] = {nullptr, nullptr};
+    uint32_t* d_qcount = nullptr;             // [16]
+    unsigned long long* d_counters = nullptr; // [8]
+    bool traced = false;
+
+    // hipEvent rings: per build 6 events (before bounds, after bounds/morton/sort/karras/refit),
+    // per trace 3 (before primary, after primary, after bounces)
+    static constexpr int RING = 32;
+    hipEvent_t evb[RING][6] = {};
+    hipEvent_t evt[RING][3] = {};
+    uint32_t n_builds = 0, n_traces = 0;   // timed samples since reset
+    hipEvent_t ev_ready = nullptr;
+};
+
+namespace {
+
+std::string g_create_error;
+
+rtbvh_status fail(rtbvh_ctx* c, rtbvh_status st, const std::string& msg) {
+    if (c) c->err = msg;
+    else g_create_error = msg;
+    return st;
+}
+
+#define HIPC(ctx, expr)                                                                          \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return fail(ctx, _e == hipErrorOutOfMemory ? RTBVH_ERR_OOM : RTBVH_ERR_HIP,          \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                      \
+    } while (0)
+
+template <typename T>
+void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+template <typename T>
+hipError_t dalloc(T*& p, size_t count) {
+    dfree(p);
+    if (count == 0) count = 1;
+    return hipMalloc((void**)&p, count * sizeof(T));
+}
+
+rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
+    if (T <= c->cap_T && c->d_codes) return RTBVH_OK;
+    const size_t n = T, ni = T > 1 ? T - 1 : 1;
+    HIPC(c, dalloc(c->d_codes, n));
+    HIPC(c, dalloc(c->d_ids, n));
+    HIPC(c, dalloc(c->d_ka, n));
+    HIPC(c, dalloc(c->d_va, n));
+    HIPC(c, dalloc(c->d_kb, n));
+    HIPC(c, dalloc(c->d_vb, n));
+    HIPC(c, dalloc(c->d_sort_scratch, sort_scratch_words(T)));
+    HIPC(c, dalloc(c->d_tclip, 3 * n));
+    HIPC(c, dalloc(c->d_leaf, 3 * n));
+    HIPC(c, dalloc(c->d_inner, ni));
+    HIPC(c, dalloc(c->d_pleaf, n));
+    HIPC(c, dalloc(c->d_pint, ni));
+    HIPC(c, dalloc(c->d_cnt, ni));
+    HIPC(c, dalloc(c->d_bounds, 8));
+    HIPC(c, dalloc(c->d_rootbox, 8));
+    c->cap_T = T;
+    return RTBVH_OK;
+}
+
+rtbvh_status ensure_trace_capacity(rtbvh_ctx* c, size_t P) {
+    if (P <= c->cap_P && c->d_color) return RTBVH_OK;
+    HIPC(c, dalloc(c->d_color, P));
+    HIPC(c, dalloc(c->d_intensity, P));
+    HIPC(c, dalloc(c->d_q[0], P));
+    HIPC(c, dalloc(c->d_q[1], P));
+    if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 16));
+    if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 16));
+    c->cap_P = P;
+    return RTBVH_OK;
+}
+
+BuildArgs build_args(rtbvh_ctx* c) {
+    BuildArgs a{};
+    a.opos = c->d_opos;
+    a.idx = c->d_idx;
+    a.V = c->V;
+    a.T = c->T;
+    a.morton_mode = (int)c->cfg.morton_mode;
+    a.delta_mode = (int)c->cfg.delta_mode;
+    memcpy(a.wvp.m, c->wvp, sizeof(c->wvp));
+    memcpy(a.smin, c->cfg.scene_bb_min, 12);
+    memcpy(a.smax, c->cfg.scene_bb_max, 12);
+    a.bounds = c->d_bounds;
+    a.keys = c->d_codes;
+    a.vals = c->d_ids;
+    a.tclip = c->d_tclip;
+    a.sorted_keys = c->sorted.keys;
+    a.sorted_vals = c->sorted.vals;
+    a.leaf = c->d_leaf;
+    a.inner = c->d_inner;
+    a.pleaf = c->d_pleaf;
+    a.pint = c->d_pint;
+    a.refit_cnt = c->d_cnt;
+    a.rootbox = c->d_rootbox;
+    return a;
+}
+
+TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks, float4* color, float* inten) {
+    TraceArgs a{};
+    a.inner = c->d_inner;
+    a.leaf = c->d_leaf;
+    a.verts = c->d_verts;
+    a.idx = c->d_idx;
+    a.matidx = c->d_matidx;
+    a.mats = c->d_mats;
+    a.T = c->T;
+    a.W = W;
+    a.H = H;
+    a.rank = rank;
+    a.nranks = nranks;
+    memcpy(a.wv.m, c->wv, sizeof(c->wv));
+    a.color = color;
+    a.intensity = inten;
+    a.counters = c->d_counters;
+    return a;
+}
+
+rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(c, RTBVH_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return RTBVH_OK;
+}
+
+rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
+                           float4* color, float* inten, hipStream_t s) {
+    if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
+    if (W == 0 || H == 0 || nranks == 0 || rank >= nranks || bounces > 14)
+        return fail(c, RTBVH_ERR_INVALID_ARG, "bad trace dimensions");
+    rtbvh_status st = ensure_trace_capacity(c, (size_t)W * H);
+    if (st) return st;
+    if (!color) color = c->d_color;
+    const bool count = (c->cfg.flags & RTBVH_FLAG_COUNT_VISITS) != 0;
+    const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream;
+    TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
+    HIPC(c, hipMemsetAsync(c->d_qcount, 0, 16 * sizeof(uint32_t), s));
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), s));
+    hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
+    if (timing) HIPC(c, hipEventRecord(ev[0], s));
+    launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, s);
+    if (timing) HIPC(c, hipEventRecord(ev[1], s));
+    for (uint32_t b = 0; b < bounces; b++)
+        launch_bounce(a, c->d_q[b & 1], &c->d_qcount[b], c->d_q[(b + 1) & 1], &c->d_qcount[b + 1], count,
+                      b + 1 < bounces, s);
+    if (timing) {
+        HIPC(c, hipEventRecord(ev[2], s));
+        c->n_traces++;
+    }
+    c->W = W;
+    c->H = H;
+    c->bounces = bounces;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->traced = true;
+    return check_launch(c, "trace kernels");
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtbvh_abi_version(void) { return RTBVH_ABI_VERSION; }
+
+void rtbvh_config_default(rtbvh_config* cfg) {
+    if (!cfg) return;
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->device = 0;
+    cfg->morton_mode = RTBVH_MORTON_CPUTESTS;
+    cfg->delta_mode = RTBVH_DELTA_CLZ64;
+    for (int k = 0; k < 3; k++) {   // Graphics.cpp:528-529
+        cfg->scene_bb_min[k] = -700.f;
+        cfg->scene_bb_max[k] = 700.f;
+    }
+}
+
+rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
+    if (!out) return fail(nullptr, RTBVH_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    rtbvh_ctx* c = new (std::nothrow) rtbvh_ctx();
+    if (!c) return fail(nullptr, RTBVH_ERR_OOM, "host allocation failed");
+    if (cfg) c->cfg = *cfg;
+    else rtbvh_config_default(&c->cfg);
+    if (c->cfg.morton_mode > 1 || c->cfg.delta_mode > 1) {
+        delete c;
+        return fail(nullptr, RTBVH_ERR_INVALID_ARG, "bad morton/delta mode");
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        delete c;
+        return fail(nullptr, RTBVH_ERR_NO_DEVICE, "no HIP device");
+    }
+    if (c->cfg.device < 0 || c->cfg.device >= ndev || hipSetDevice(c->cfg.device) != hipSuccess) {
+        delete c;
+        return fail(nullptr, RTBVH_ERR_NO_DEVICE, "bad device ordinal");
+    }
+    if (c->cfg.stream) {
+        c->stream = (hipStream_t)c->cfg.stream;
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            return fail(nullptr, RTBVH_ERR_HIP, "hipStreamCreate failed");
+        }
+        c->own_stream = true;
+    }
+    bool ev_ok = true;
+    for (auto& row : c->evb)
+        for (auto& e : row) ev_ok = ev_ok && hipEventCreate(&e) == hipSuccess;
+    for (auto& row : c->evt)
+        for (auto& e : row) ev_ok = ev_ok && hipEventCreate(&e) == hipSuccess;
+    if (!ev_ok) {
+        rtbvh_destroy(c);
+        return fail(nullptr, RTBVH_ERR_HIP, "hipEventCreate failed");
+    }
+    if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess) {
+        rtbvh_destroy(c);
+        return fail(nullptr, RTBVH_ERR_HIP, "hipEventCreate failed");
+    }
+    *out = c;
+    return RTBVH_OK;
+}
+
+void rtbvh_destroy(rtbvh_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->cfg.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
+    dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner);
+    dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
+    dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount);
+    dfree(c->d_counters);
+    for (auto& row : c->evb)
+        for (auto& e : row)
+            if (e) (void)hipEventDestroy(e);
+    for (auto& row : c->evt)
+        for (auto& e : row)
+            if (e) (void)hipEventDestroy(e);
+    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rtbvh_last_error(const rtbvh_ctx* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t nverts, const uint32_t* indices,
+                             uint32_t nidx, const uint32_t* mat_idx, const rtbvh_material* mats, uint32_t nmats,
+                             const rtbvh_texture* textures, uint32_t ntex) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    (void)textures;
+    (void)ntex;
+    if (!verts || !indices || !mat_idx || !mats || nverts == 0 || nidx == 0 || nidx % 3 != 0 || nmats == 0)
+        return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: empty or ragged input");
+    const uint32_t T = nidx / 3;
+    if (T >= (1u << 30)) return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: too many triangles");
+    for (uint32_t i = 0; i < nidx; i++)
+        if (indices[i] >= nverts) return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: index out of range");
+    for (uint32_t t = 0; t < T; t++)
+        if (mat_idx[t] >= nmats) return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: material index out of range");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    try {
+        std::vector<float4> opos(nverts);
+        for (uint32_t i = 0; i < nverts; i++)
+            opos[i] = make_float4(verts[i].position[0], verts[i].position[1], verts[i].position[2], 0.f);
+        HIPC(c, dalloc(c->d_opos, nverts));
+        HIPC(c, dalloc(c->d_verts, (size_t)nverts * 8));
+        HIPC(c, dalloc(c->d_idx, nidx));
+        HIPC(c, dalloc(c->d_matidx, T));
+        HIPC(c, dalloc(c->d_mats, nmats));
+        HIPC(c, hipMemcpy(c->d_opos, opos.data(), sizeof(float4) * nverts, hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_verts, verts, sizeof(rtbvh_vertex) * nverts, hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_idx, indices, sizeof(uint32_t) * nidx, hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_matidx, mat_idx, sizeof(uint32_t) * T, hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_mats, mats, sizeof(rtbvh_material) * nmats, hipMemcpyHostToDevice));
+    } catch (const std::bad_alloc&) {
+        return fail(c, RTBVH_ERR_OOM, "set_scene: host allocation failed");
+    }
+    static_assert(sizeof(rtbvh_material) == sizeof(Mat), "material layout");
+    c->V = nverts;
+    c->T = T;
+    c->nmat = nmats;
+    rtbvh_status st = ensure_build_capacity(c, T);
+    if (st) return st;
+    c->have_scene = true;
+    c->built = false;
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_set_camera(rtbvh_ctx* c, const float wvp[16], const float wv[16]) {
+    if (!c || !wvp || !wv) return RTBVH_ERR_INVALID_ARG;
+    memcpy(c->wvp, wvp, sizeof(c->wvp));
+    memcpy(c->wv, wv, sizeof(c->wv));
+    c->have_camera = true;
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    if (!c->have_scene || !c->have_camera) return fail(c, RTBVH_ERR_NOT_READY, "build before set_scene/set_camera");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    hipStream_t s = c->stream;
+    const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0;
+    BuildArgs a = build_args(c);
+    hipEvent_t* ev = c->evb[c->n_builds % rtbvh_ctx::RING];
+    if (timing) HIPC(c, hipEventRecord(ev[0], s));
+    if (c->cfg.morton_mode == RTBVH_MORTON_CPUTESTS) {
+        HIPC(c, hipMemsetAsync(c->d_bounds, 0xFF, 3 * sizeof(uint32_t), s));
+        HIPC(c, hipMemsetAsync(c->d_bounds + 3, 0x00, 3 * sizeof(uint32_t), s));
+        launch_bounds(a, s);
+    }
+    if (timing) HIPC(c, hipEventRecord(ev[1], s));
+    launch_morton(a, s);
+    if (timing) HIPC(c, hipEventRecord(ev[2], s));
+    c->sorted = radix_sort_pairs(c->d_codes, c->d_ids, c->d_ka, c->d_va, c->d_kb, c->d_vb, c->T, 30,
+                                 c->d_sort_scratch, s);
+    if (timing) HIPC(c, hipEventRecord(ev[3], s));
+    a.sorted_keys = c->sorted.keys;
+    a.sorted_vals = c->sorted.vals;
+    launch_leaf_karras(a, s);
+    if (timing) HIPC(c, hipEventRecord(ev[4], s));
+    if (c->T > 1) HIPC(c, hipMemsetAsync(c->d_cnt, 0, sizeof(uint32_t) * (c->T - 1), s));
+    launch_refit(a, s);
+    if (timing) HIPC(c, hipEventRecord(ev[5], s));
+    if (timing) c->n_builds++;
+    c->built = true;
+    return check_launch(c, "build kernels");
+}
+
+rtbvh_status rtbvh_build(rtbvh_ctx* c) {
+    rtbvh_status st = rtbvh_build_async(c);
+    if (st) return st;
+    return rtbvh_synchronize(c);
+}
+
+rtbvh_status rtbvh_trace_async(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    rtbvh_status st = ensure_trace_capacity(c, (size_t)W * H);
+    if (st) return st;
+    return enqueue_trace(c, W, H, bounces, 0, 1, c->d_color, c->d_intensity, c->stream);
+}
+
+rtbvh_status rtbvh_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
+    rtbvh_status st = rtbvh_trace_async(c, W, H, bounces);
+    if (st) return st;
+    return rtbvh_synchronize(c);
+}
+
+rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
+    rtbvh_status st = rtbvh_build_async(c);
+    if (st) return st;
+    st = rtbvh_trace_async(c, W, H, bounces);
+    if (st) return st;
+    return rtbvh_synchronize(c);
+}
+
+uint32_t rtbvh_band_rows(uint32_t H, uint32_t rank, uint32_t nranks) {
+    if (nranks == 0 || rank >= nranks) return 0;
+    uint32_t rows = 0;
+    for (uint32_t b = rank; b * 8 < H; b += nranks) rows += (H - b * 8) < 8 ? (H - b * 8) : 8;
+    return rows;
+}
+
+rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank,
+                                    uint32_t nranks, float* dev_out, void* stream) {
+    if (!c || !dev_out) return RTBVH_ERR_INVALID_ARG;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (s != c->stream) {   // order after the build / previous work on the context stream
+        HIPC(c, hipEventRecord(c->ev_ready, c->stream));
+        HIPC(c, hipStreamWaitEvent(s, c->ev_ready, 0));
+    }
+    rtbvh_status st = enqueue_trace(c, W, H, bounces, rank, nranks, (float4*)dev_out, nullptr, s);
+    if (st) return st;
+    if (s != c->stream) {   // and make later context work wait for this trace
+        HIPC(c, hipEventRecord(c->ev_ready, s));
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_ready, 0));
+    }
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_read_framebuffer(rtbvh_ctx* c, float* rgba) {
+    if (!c || !rgba) return RTBVH_ERR_INVALID_ARG;
+    if (!c->traced) return fail(c, RTBVH_ERR_NOT_READY, "no trace yet");
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(rgba, c->d_color, sizeof(float4) * (size_t)c->W * c->H, hipMemcpyDeviceToHost));
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_read_intensity(rtbvh_ctx* c, float* inten) {
+    if (!c || !inten) return RTBVH_ERR_INVALID_ARG;
+    if (!c->traced) return fail(c, RTBVH_ERR_NOT_READY, "no trace yet");
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(inten, c->d_intensity, sizeof(float) * (size_t)c->W * c->H, hipMemcpyDeviceToHost));
+    return RTBVH_OK;
+}
+
+const float* rtbvh_framebuffer_device(rtbvh_ctx* c) { return c ? (const float*)c->d_color : nullptr; }
+
+rtbvh_status rtbvh_read_bvh(rtbvh_ctx* c, rtbvh_node* out, uint32_t capacity) {
+    if (!c || !out) return RTBVH_ERR_INVALID_ARG;
+    if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "no build yet");
+    const size_t total = 2 * (size_t)c->T - 1;
+    if (capacity < total) return fail(c, RTBVH_ERR_INVALID_ARG, "read_bvh: capacity < 2n-1");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    void* tmp = nullptr;
+    HIPC(c, hipMalloc(&tmp, total * sizeof(rtbvh_node)));
+    BuildArgs a = build_args(c);
+    launch_export(a, tmp, c->stream);
+    hipError_t e1 = hipGetLastError();
+    hipError_t e2 = hipStreamSynchronize(c->stream);
+    hipError_t e3 = hipMemcpy(out, tmp, total * sizeof(rtbvh_node), hipMemcpyDeviceToHost);
+    (void)hipFree(tmp);
+    HIPC(c, e1);
+    HIPC(c, e2);
+    HIPC(c, e3);
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_read_morton(rtbvh_ctx* c, uint32_t* codes) {
+    if (!c || !codes) return RTBVH_ERR_INVALID_ARG;
+    if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "no build yet");
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(codes, c->d_codes, sizeof(uint32_t) * c->T, hipMemcpyDeviceToHost));
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_read_sorted(rtbvh_ctx* c, uint32_t* keys, uint32_t* ids) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "no build yet");
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (keys) HIPC(c, hipMemcpy(keys, c->sorted.keys, sizeof(uint32_t) * c->T, hipMemcpyDeviceToHost));
+    if (ids) HIPC(c, hipMemcpy(ids, c->sorted.vals, sizeof(uint32_t) * c->T, hipMemcpyDeviceToHost));
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_read_rays(rtbvh_ctx* c, rtbvh_ray_present*, rtbvh_ray_present*) {
+    return fail(c, RTBVH_ERR_INVALID_ARG, "read_rays: ray records are not kept in this version");
+}
+
+rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
+    if (!c || !out) return RTBVH_ERR_INVALID_ARG;
+    memset(out, 0, sizeof(*out));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    out->num_tris = c->T;
+    out->num_nodes = c->T ? 2 * c->T - 1 : 0;
+    out->width = c->W;
+    out->height = c->H;
+    const uint32_t nb = c->n_builds < (uint32_t)rtbvh_ctx::RING ? c->n_builds : rtbvh_ctx::RING;
+    for (uint32_t k = 0; k < nb; k++) {
+        float ms;
+        HIPC(c, hipEventElapsedTime(&ms, c->evb[k][0], c->evb[k][5]));
+        out->ms_build += ms / nb;
+        for (int st = 0; st < 5; st++) {
+            HIPC(c, hipEventElapsedTime(&ms, c->evb[k][st], c->evb[k][st + 1]));
+            out->ms_stage[st] += ms / nb;
+        }
+    }
+    out->timed_builds = nb;
+    const uint32_t nt = c->n_traces < (uint32_t)rtbvh_ctx::RING ? c->n_traces : rtbvh_ctx::RING;
+    for (uint32_t k = 0; k < nt; k++) {
+        float ms;
+        HIPC(c, hipEventElapsedTime(&ms, c->evt[k][0], c->evt[k][2]));
+        out->ms_trace += ms / nt;
+        HIPC(c, hipEventElapsedTime(&ms, c->evt[k][0], c->evt[k][1]));
+        out->ms_stage[5] += ms / nt;
+        HIPC(c, hipEventElapsedTime(&ms, c->evt[k][1], c->evt[k][2]));
+        out->ms_stage[6] += ms / nt;
+    }
+    out->timed_traces = nt;
+    if (c->traced && c->d_counters) {
+        unsigned long long cnt[16];
+        uint32_t q[16];
+        HIPC(c, hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(q, c->d_qcount, sizeof(q), hipMemcpyDeviceToHost));
+        out->primary_rays = (uint64_t)c->W * rtbvh_band_rows(c->H, c->rank, c->nranks);
+        uint64_t b = 0;
+        for (uint32_t k = 0; k < c->bounces; k++) b += q[k];
+        out->bounce_rays = b;
+        for (int p = 0; p < 2; p++) {
+            out->internal_visits[p] = cnt[2 + 3 * p];
+            out->leaf_visits[p] = cnt[3 + 3 * p];
+            out->hits[p] = cnt[4 + 3 * p];
+        }
+        out->stack_overflows = cnt[8];
+        out->textured_hits = cnt[9];
+    }
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_set_flags(rtbvh_ctx* c, uint32_t flags) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    c->cfg.flags = flags;
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_reset_stats(rtbvh_ctx* c) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->n_builds = 0;
+    c->n_traces = 0;
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_sort_pairs_async(rtbvh_ctx* c, uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vout,
+                                    uint32_t n, uint32_t key_bits) {
+    if (!c || (n && (!kin || !vin || !kout || !vout)) || key_bits == 0 || key_bits > 32)
+        return RTBVH_ERR_INVALID_ARG;
+    if (n == 0) return RTBVH_OK;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const uint32_t passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
+    uint32_t *tk = nullptr, *tv = nullptr, *scratch = nullptr;
+    HIPC(c, hipMallocAsync((void**)&scratch, sort_scratch_words(n) * 4, c->stream));
+    if (passes > 1) {
+        HIPC(c, hipMallocAsync((void**)&tk, (size_t)n * 4, c->stream));
+        HIPC(c, hipMallocAsync((void**)&tv, (size_t)n * 4, c->stream));
+    }
+    // odd pass count ends in A, even in B: arrange for the result to land in (kout, vout)
+    if (passes & 1) radix_sort_pairs(kin, vin, kout, vout, tk, tv, n, key_bits, scratch, c->stream);
+    else radix_sort_pairs(kin, vin, tk, tv, kout, vout, n, key_bits, scratch, c->stream);
+    rtbvh_status st = check_launch(c, "sort kernels");
+    (void)hipFreeAsync(scratch, c->stream);
+    if (tk) (void)hipFreeAsync(tk, c->stream);
+    if (tv) (void)hipFreeAsync(tv, c->stream);
+    return st;
+}
+
+rtbvh_status rtbvh_sort_pairs_host(rtbvh_ctx* c, const uint32_t* keys, const uint32_t* vals, uint32_t* kout,
+                                   uint32_t* vout, uint32_t n, uint32_t key_bits) {
+    if (!c || (n && (!keys || !vals || !kout || !vout))) return RTBVH_ERR_INVALID_ARG;
+    if (n == 0) return RTBVH_OK;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    uint32_t* d = nullptr;
+    HIPC(c, hipMalloc((void**)&d, (size_t)n * 16));
+    uint32_t *dk = d, *dv = d + n, *ok = d + 2 * (size_t)n, *ov = d + 3 * (size_t)n;
+    rtbvh_status st = RTBVH_OK;
+    if (hipMemcpy(dk, keys, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dv, vals, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess)
+        st = fail(c, RTBVH_ERR_HIP, "sort_pairs_host: upload failed");
+    if (!st) st = rtbvh_sort_pairs_async(c, dk, dv, ok, ov, n, key_bits);
+    if (!st && hipStreamSynchronize(c->stream) != hipSuccess) st = fail(c, RTBVH_ERR_HIP, "sort_pairs_host: sync");
+    if (!st && (hipMemcpy(kout, ok, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(vout, ov, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess))
+        st = fail(c, RTBVH_ERR_HIP, "sort_pairs_host: download failed");
+    (void)hipFree(d);
+    return st;
+}
+
+rtbvh_status rtbvh_build_from_codes(rtbvh_ctx* c, const uint32_t* sorted_codes, const float* leaf_boxes, uint32_t n,
+                                    rtbvh_node* out) {
+    if (!c || !sorted_codes || !leaf_boxes || !out || n == 0 || n >= (1u << 30)) return RTBVH_ERR_INVALID_ARG;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    rtbvh_status st = ensure_build_capacity(c, n);
+    if (st) return st;
+    float* d_boxes = nullptr;
+    void* d_out = nullptr;
+    HIPC(c, hipMalloc((void**)&d_boxes, (size_t)n * 24));
+    HIPC(c, hipMalloc(&d_out, (2 * (size_t)n - 1) * sizeof(rtbvh_node)));
+    HIPC(c, hipMemcpy(c->d_ka, sorted_codes, (size_t)n * 4, hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(d_boxes, leaf_boxes, (size_t)n * 24, hipMemcpyHostToDevice));
+    BuildArgs a = build_args(c);
+    a.T = n;
+    a.sorted_keys = c->d_ka;
+    a.sorted_vals = nullptr;
+    a.leaf = nullptr;
+    launch_from_codes(a, d_boxes, c->stream);
+    launch_export(a, d_out, c->stream);
+    st = check_launch(c, "build_from_codes kernels");
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (!st && e == hipSuccess) e = hipMemcpy(out, d_out, (2 * (size_t)n - 1) * sizeof(rtbvh_node), hipMemcpyDeviceToHost);
+    (void)hipFree(d_boxes);
+    (void)hipFree(d_out);
+    if (st) return st;
+    HIPC(c, e);
+    c->built = false;   // the scene's BVH buffers were reused
+    return RTBVH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,306 @@
+// build.hip -- LBVH build kernels for gfx950: scene bounds, Morton codes,
+// leaf records + Karras internal nodes, bottom-up refit, reference-layout export.
+//
+// Reference: MortonCodes.hlsl (2 triangles per thread, writes whole 44-B nodes),
+// BVHConstructP1.hlsl (Karras 2012, one thread per internal node), and
+// BVHConstructP2.hlsl (atomic 2nd-arriver refit).  Differences by design (see
+// DESIGN.md): codes and triangle ids are sorted as 8-B pairs instead of moving
+// 44-B nodes; the clip-space triangle is written once in triangle order and
+// gathered once into SORTED leaf records; each internal node is one 64-B record
+// holding both children's boxes, so traversal reads one line per node.
+#include "rtbvh_internal.h"
+
+namespace rtbvh {
+namespace {
+
+constexpr uint32_t BLOCK = 256;
+
+__device__ __forceinline__ uint32_t expand_bits(uint32_t var) {   // MortonCodes.hlsl:13-31
+    var &= 0x000003ffu; var |= var << 16;
+    var &= 0x030000ffu; var |= var << 8;
+    var &= 0x0300f00fu; var |= var << 4;
+    var &= 0x030c30c3u; var |= var << 2;
+    return var & 0x09249249u;
+}
+// Morton Code/main.cpp:84-92 (CPUTests) -- NaN quantises to 0
+__device__ __forceinline__ uint32_t quantise_cputests(float p) {
+    p *= 1024.f;
+    if (p < 0) p = 0;
+    else if (p >= 1024) p = 1023;
+    if (p != p) return 0u;
+    return (uint32_t)p;
+}
+// MortonCodes.hlsl:42-47: clamp(p, 0, 1023) = min(max(p, 0), 1023)
+__device__ __forceinline__ uint32_t quantise_hlsl(float p) {
+    p *= 1024.f;
+    p = fminf(fmaxf(p, 0.0f), 1023.0f);
+    return (uint32_t)p;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_bounds(const float4* __restrict__ opos, uint32_t V, uint32_t* __restrict__ bounds) {
+    f3 mn = mk(INFINITY, INFINITY, INFINITY), mx = mk(-INFINITY, -INFINITY, -INFINITY);
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < V; i += (size_t)gridDim.x * BLOCK) {
+        float4 p = opos[i];
+        mn = vmin(mn, mk(p.x, p.y, p.z));
+        mx = vmax(mx, mk(p.x, p.y, p.z));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        mn.x = fminf(mn.x, __shfl_xor(mn.x, off, 64));
+        mn.y = fminf(mn.y, __shfl_xor(mn.y, off, 64));
+        mn.z = fminf(mn.z, __shfl_xor(mn.z, off, 64));
+        mx.x = fmaxf(mx.x, __shfl_xor(mx.x, off, 64));
+        mx.y = fmaxf(mx.y, __shfl_xor(mx.y, off, 64));
+        mx.z = fmaxf(mx.z, __shfl_xor(mx.z, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&bounds[0], f2ord(mn.x));
+        atomicMin(&bounds[1], f2ord(mn.y));
+        atomicMin(&bounds[2], f2ord(mn.z));
+        atomicMax(&bounds[3], f2ord(mx.x));
+        atomicMax(&bounds[4], f2ord(mx.y));
+        atomicMax(&bounds[5], f2ord(mx.z));
+    }
+}
+
+// MortonCodes.hlsl:54-125 (HLSL mode) / ShaderSim/main.cpp:292-301 (CPUTests mode)
+__global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= a.T) return;
+    const uint32_t i0 = a.idx[3 * (size_t)t], i1 = a.idx[3 * (size_t)t + 1], i2 = a.idx[3 * (size_t)t + 2];
+    const float4 q0 = a.opos[i0], q1 = a.opos[i1], q2 = a.opos[i2];
+    const f3 p0 = mk(q0.x, q0.y, q0.z), p1 = mk(q1.x, q1.y, q1.z), p2 = mk(q2.x, q2.y, q2.z);
+    const f3 c0 = xform_point(a.wvp.m, p0), c1 = xform_point(a.wvp.m, p1), c2 = xform_point(a.wvp.m, p2);
+    uint32_t code;
+    if (a.morton_mode == 0) {
+        const f3 mn = mk(ord2f(a.bounds[0]), ord2f(a.bounds[1]), ord2f(a.bounds[2]));
+        const f3 mx = mk(ord2f(a.bounds[3]), ord2f(a.bounds[4]), ord2f(a.bounds[5]));
+        const float xv = p0.x + p1.x + p2.x, yv = p0.y + p1.y + p2.y, zv = p0.z + p1.z + p2.z;
+        const uint32_t qx = quantise_cputests((xv / 3.f - mn.x) / (mx.x - mn.x));
+        const uint32_t qy = quantise_cputests((yv / 3.f - mn.y) / (mx.y - mn.y));
+        const uint32_t qz = quantise_cputests((zv / 3.f - mn.z) / (mx.z - mn.z));
+        code = expand_bits(qz) | expand_bits(qy) << 1 | expand_bits(qx) << 2;
+    } else {
+        f3 bmin = vmin(c0, c1);
+        bmin = vmin(bmin, c2);   // avg == bbMin after the loop (MortonCodes.hlsl:98 bug)
+        const f3 avg = mk(bmin.x / 3.f, bmin.y / 3.f, bmin.z / 3.f);
+        const uint32_t qx = quantise_hlsl((avg.x - a.smin[0]) / (a.smax[0] - a.smin[0]));
+        const uint32_t qy = quantise_hlsl((avg.y - a.smin[1]) / (a.smax[1] - a.smin[1]));
+        const uint32_t qz = quantise_hlsl((avg.z - a.smin[2]) / (a.smax[2] - a.smin[2]));
+        code = expand_bits(qx) | expand_bits(qy) << 1 | expand_bits(qz) << 2;
+    }
+    a.keys[t] = code;
+    a.vals[t] = t;
+    float4* o = a.tclip + 3 * (size_t)t;
+    o[0] = make_float4(c0.x, c0.y, c0.z, __uint_as_float(t));
+    o[1] = make_float4(c1.x, c1.y, c1.z, 0.f);
+    o[2] = make_float4(c2.x, c2.y, c2.z, 0.f);
+}
+
+// ---- Karras 2012 (BVHConstructP1.hlsl:61-165) --------------------------------
+__device__ __forceinline__ int delta_clz64(const uint32_t* __restrict__ c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
+    if (j < 0 || j >= n) return -1;   // leadingPrefixBounds :78-84
+    const uint32_t cj = c[j];
+    return ci != cj ? __clz((int)(ci ^ cj)) : 32 + __clz((int)(i ^ (uint32_t)j));
+}
+__device__ __forceinline__ int debruijn_lz(uint32_t data) {   // RadixBVHCombo/main.cpp:136-151
+    const int tbl[32] = {0, 31, 9, 30, 3, 8, 13, 29, 2, 5, 7, 21, 12, 24, 28, 19,
+                         1, 10, 4, 14, 6, 22, 25, 20, 11, 15, 23, 26, 16, 27, 17, 18};
+    data |= data >> 1; data |= data >> 2; data |= data >> 4; data |= data >> 8; data |= data >> 16;
+    data++;
+    return data ? tbl[(uint32_t)(data * 0x076be629u) >> 27] : 32;
+}
+__device__ __forceinline__ int delta_cputests(const uint32_t* __restrict__ c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
+    if (j < 0 || j >= n) return -1;
+    const uint32_t cj = c[j];
+    return debruijn_lz(ci == cj ? (i ^ (uint32_t)j) : (ci ^ cj));
+}
+
+template <int MODE>
+__device__ __forceinline__ int delta(const uint32_t* c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
+    return MODE == 0 ? delta_clz64(c, n, i, ci, j) : delta_cputests(c, n, i, ci, j);
+}
+
+template <int MODE>
+__device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t i, Inner* __restrict__ inner,
+                            uint32_t* __restrict__ pleaf, uint32_t* __restrict__ pint) {
+    const int64_t N = n, I = i;
+    const uint32_t ci = c[i];
+    const int64_t d = delta<MODE>(c, N, i, ci, I + 1) < delta<MODE>(c, N, i, ci, I - 1) ? -1 : 1;
+    const int min_lz = delta<MODE>(c, N, i, ci, I - d);
+    int64_t bound_len = 2;
+    while (min_lz < delta<MODE>(c, N, i, ci, I + bound_len * d)) bound_len <<= 1;
+    int64_t dl = bound_len, dsum = 0;
+    do {
+        dl = (dl + 1) >> 1;
+        if (min_lz < delta<MODE>(c, N, i, ci, I + (dsum + dl) * d)) dsum += dl;
+    } while (1 < dl);
+    const int64_t bound_start = I + dsum * d;
+    const int lz = delta<MODE>(c, N, i, ci, bound_start);
+    dl = dsum;
+    int64_t tmp = 0;
+    do {
+        dl = (dl + 1) >> 1;
+        if (lz < delta<MODE>(c, N, i, ci, I + (tmp + dl) * d)) tmp += dl;
+    } while (1 < dl);
+    const int64_t loc = I + tmp * d + (d < 0 ? d : 0);
+    const bool left_leaf = (I < bound_start ? I : bound_start) == loc;
+    const bool right_leaf = (I > bound_start ? I : bound_start) == loc + 1;
+    const uint32_t l = (uint32_t)loc, r = (uint32_t)(loc + 1);
+    inner[i].child_l = left_leaf ? (LEAF_BIT | l) : l;
+    inner[i].child_r = right_leaf ? (LEAF_BIT | r) : r;
+    if (left_leaf) pleaf[l] = i << 1; else pint[l] = i << 1;
+    if (right_leaf) pleaf[r] = (i << 1) | 1u; else pint[r] = (i << 1) | 1u;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= a.T) return;
+    // leaf record: gather the clip-space triangle of sorted position i
+    const uint32_t t = a.sorted_vals[i];
+    const float4* src = a.tclip + 3 * (size_t)t;
+    float4* dst = a.leaf + 3 * (size_t)i;
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
+    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.inner, a.pleaf, a.pint);
+    if (i == 0 && a.T > 1) a.pint[0] = INVALID;   // root (BVHConstructP1.hlsl:186-187)
+}
+
+// Karras only (for rtbvh_build_from_codes): leaf boxes come from the caller
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_karras_only(BuildArgs a) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.inner, a.pleaf, a.pint);
+    if (i == 0 && a.T > 1) a.pint[0] = INVALID;
+}
+
+// ---- refit (BVHConstructP2.hlsl:8-37) -----------------------------------------
+// One thread per leaf climbs; a per-node ticket makes the second arriver union
+// both child boxes.  Each box is stored into its parent's 64-B record (side
+// 0/1) BEFORE the ticket; the ticket is an agent-scope acq_rel RMW, so the
+// second arriver's loads of the sibling box see the first arriver's stores
+// whichever CU / XCD either ran on (cdna_hip_programming.md §6 G16).
+__device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __restrict__ inner,
+                                            const uint32_t* __restrict__ pint, uint32_t* __restrict__ cnt,
+                                            float* __restrict__ rootbox) {
+    // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
+    // tree with a parent cycle from spinning forever
+    for (int level = 0; level < 2 * STACK_SIZE; level++) {
+        const uint32_t p = e >> 1, side = e & 1u;
+        float* dst = side ? inner[p].rmin : inner[p].lmin;   // min[3], max[3] contiguous
+        dst[0] = lo.x; dst[1] = lo.y; dst[2] = lo.z;
+        dst[3] = hi.x; dst[4] = hi.y; dst[5] = hi.z;
+        const uint32_t old = __hip_atomic_fetch_add(&cnt[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == 0) return;
+        const float* sib = side ? inner[p].lmin : inner[p].rmin;
+        const f3 smin = mk(sib[0], sib[1], sib[2]), smax = mk(sib[3], sib[4], sib[5]);
+        // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
+        if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
+        else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
+        e = pint[p];
+        if (e == INVALID) {
+            rootbox[0] = lo.x; rootbox[1] = lo.y; rootbox[2] = lo.z;
+            rootbox[3] = hi.x; rootbox[4] = hi.y; rootbox[5] = hi.z;
+            return;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= a.T) return;
+    const float4* r = a.leaf + 3 * (size_t)i;
+    const float4 v0 = r[0], v1 = r[1], v2 = r[2];
+    f3 lo = mk(v0.x, v0.y, v0.z), hi = lo;   // MortonCodes.hlsl:87-96
+    lo = vmin(lo, mk(v1.x, v1.y, v1.z)); hi = vmax(hi, mk(v1.x, v1.y, v1.z));
+    lo = vmin(lo, mk(v2.x, v2.y, v2.z)); hi = vmax(hi, mk(v2.x, v2.y, v2.z));
+    if (a.T == 1) {
+        a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
+        a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+        return;
+    }
+    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= a.T) return;
+    const float* b = boxes + 6 * (size_t)i;
+    const f3 lo = mk(b[0], b[1], b[2]), hi = mk(b[3], b[4], b[5]);
+    if (a.T == 1) {
+        for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
+        return;
+    }
+    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox);
+}
+
+// reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k
+struct RefNode { uint32_t parent, child_l, child_r, code; float bb_min[3], bb_max[3]; uint32_t index; };
+static_assert(sizeof(RefNode) == 44, "44-B Node");
+
+__global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restrict__ out) {
+    const uint32_t T = a.T;
+    const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
+    if (r >= 2 * T - 1) return;
+    RefNode o;
+    const float* box;
+    uint32_t e;
+    if (r < T) {
+        e = T == 1 ? INVALID : a.pleaf[r];
+        o.child_l = INVALID;
+        o.child_r = INVALID;
+        o.code = a.sorted_keys[r];
+        o.index = a.leaf ? 3u * __float_as_uint(a.leaf[3 * (size_t)r].w) : 0u;
+    } else {
+        const uint32_t k = r - T;
+        e = a.pint[k];
+        const uint32_t cl = a.inner[k].child_l, cr = a.inner[k].child_r;
+        o.child_l = (cl & LEAF_BIT) ? (cl & ~LEAF_BIT) : T + cl;
+        o.child_r = (cr & LEAF_BIT) ? (cr & ~LEAF_BIT) : T + cr;
+        o.code = 0;
+        o.index = 0;
+    }
+    if (e == INVALID) {
+        o.parent = INVALID;
+        box = a.rootbox;
+    } else {
+        o.parent = (e >> 1) + T;
+        box = (e & 1u) ? a.inner[e >> 1].rmin : a.inner[e >> 1].lmin;
+    }
+    for (int k = 0; k < 3; k++) { o.bb_min[k] = box[k]; o.bb_max[k] = box[3 + k]; }
+    out[r] = o;
+}
+
+inline uint32_t blocks_for(size_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
+
+}  // namespace
+
+void launch_bounds(const BuildArgs& a, hipStream_t s) {
+    uint32_t blocks = blocks_for(a.V);
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_bounds, dim3(blocks), dim3(BLOCK), 0, s, a.opos, a.V, a.bounds);
+}
+void launch_morton(const BuildArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_morton, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+}
+void launch_leaf_karras(const BuildArgs& a, hipStream_t s) {
+    if (a.delta_mode == 0) hipLaunchKernelGGL(k_leaf_karras<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL(k_leaf_karras<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+}
+void launch_refit(const BuildArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+}
+void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_export, dim3(blocks_for(2 * (size_t)a.T - 1)), dim3(BLOCK), 0, s, a, (RefNode*)out);
+}
+void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t s) {
+    if (a.delta_mode == 0) hipLaunchKernelGGL(k_karras_only<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL(k_karras_only<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    if (a.T > 1) (void)hipMemsetAsync(a.refit_cnt, 0, sizeof(uint32_t) * (a.T - 1), s);
+    hipLaunchKernelGGL(k_refit_boxes, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a, leaf_boxes);
+}
+
+}  // namespace rtbvh

@@ -1,0 +1,91 @@
+// rtbvh_device.h -- device-side data layouts and the exact-arithmetic helpers
+// shared by the build and trace kernels (gfx950, wave64).
+//
+// HBM layout (see DESIGN.md "Data layout"):
+//   opos   float4[V]     object-space vertex positions (w unused), set_scene
+//   tclip  float4[3*T]   per-triangle clip-space vertices, TRIANGLE order (Morton kernel)
+//   keys/vals u32[T] x2  radix ping-pong (Morton code, triangle id)
+//   leaf   float4[3*T]   leaf records in SORTED order: {v0.xyz, tri}, {v1.xyz, 0}, {v2.xyz, 0}
+//   inner  Inner[T-1]    64-B child-pair records; internal node k, root = 0
+//   pleaf  u32[T], pint u32[T-1]   parent<<1 | side (side 0 = left child)
+// Node ids inside kernels: internal k -> k, leaf j -> LEAF_BIT | j.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtbvh {
+
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+constexpr uint32_t INVALID = 0xFFFFFFFFu;
+constexpr int STACK_SIZE = 66;   // >= 64 levels of a clz64 Karras tree + sentinel
+
+// 64-byte child-pair record of internal node k (boxes of both children, then ids)
+struct alignas(64) Inner {
+    float lmin[3], lmax[3];
+    float rmin[3], rmax[3];
+    uint32_t child_l, child_r;
+    uint32_t pad0, pad1;
+};
+static_assert(sizeof(Inner) == 64, "Inner must be one 64-B record");
+
+struct alignas(16) RayQ {   // bounce queue entry (32 B)
+    uint32_t idx;           // output pixel index
+    float intensity;
+    float ox, oy, oz;
+    float dx, dy, dz;
+};
+static_assert(sizeof(RayQ) == 32, "RayQ 32 B");
+
+struct Mat {   // rtbvh_material, 68 B (read with scalar loads)
+    float ambient[4], diffuse[4], specular[4];
+    float shininess, optical_density, alpha;
+    uint32_t specularb;
+    int32_t tex_num;
+};
+
+// ---- exact helpers: same op order as oracle/rtbvh_oracle.cpp (no FMA: the
+// translation unit is compiled with -ffp-contract=off) ----------------------
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 mul(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ f3 vmin(f3 a, f3 b) { return mk(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
+__device__ __forceinline__ f3 vmax(f3 a, f3 b) { return mk(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
+__device__ __forceinline__ f3 normalize(f3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return mul(v, inv); }
+__device__ __forceinline__ f3 reflect(f3 i, f3 n) { float t = 2.0f * dot(i, n); return sub(i, mul(n, t)); }
+__device__ __forceinline__ float magnitude(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+__device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
+__device__ __forceinline__ float lerpf(float a, float b, float s) { return a + s * (b - a); }
+
+// mul(float4(p,1), M), row-major M (row-vector convention)
+__device__ __forceinline__ f3 xform_point(const float* M, f3 p) {
+    f3 r;
+    r.x = ((p.x * M[0] + p.y * M[4]) + p.z * M[8]) + M[12];
+    r.y = ((p.x * M[1] + p.y * M[5]) + p.z * M[9]) + M[13];
+    r.z = ((p.x * M[2] + p.y * M[6]) + p.z * M[10]) + M[14];
+    return r;
+}
+// mul(n, (float3x3)M)
+__device__ __forceinline__ f3 xform_normal(const float* M, f3 n) {
+    f3 r;
+    r.x = (n.x * M[0] + n.y * M[4]) + n.z * M[8];
+    r.y = (n.x * M[1] + n.y * M[5]) + n.z * M[9];
+    r.z = (n.x * M[2] + n.y * M[6]) + n.z * M[10];
+    return r;
+}
+
+// order-preserving float <-> u32 (for atomic min/max of the scene box)
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+}  // namespace rtbvh

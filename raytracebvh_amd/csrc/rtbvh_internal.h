@@ -1,0 +1,82 @@
+// rtbvh_internal.h -- host-side launchers shared by the translation units of
+// librtbvh.so.  Not part of the public ABI (that is include/rtbvh.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rtbvh_device.h"
+
+namespace rtbvh {
+
+struct Mat4 { float m[16]; };
+
+// ---- radix sort (sort.hip) --------------------------------------------------
+constexpr uint32_t SORT_BLOCK = 256;
+constexpr uint32_t SORT_ITEMS = 16;
+constexpr uint32_t SORT_TILE = SORT_BLOCK * SORT_ITEMS;   // 4096 keys per tile
+constexpr uint32_t RADIX_BITS = 8;
+constexpr uint32_t RADIX = 1u << RADIX_BITS;
+
+inline uint32_t sort_tiles(uint32_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
+// scratch words needed: RADIX * tiles (per-tile digit counts) + RADIX (digit totals)
+inline size_t sort_scratch_words(uint32_t n) { return (size_t)RADIX * sort_tiles(n) + RADIX; }
+
+// Stable LSD sort of (key, val) over bits [0, key_bits), 8-bit digits.  Pass 0
+// reads (kin, vin) and writes (ka, va); later passes ping-pong A <-> B, so the
+// input is preserved.  Returns where the sorted pairs are (A, or B, or the
+// input itself when n == 0).  Result is in A for an odd pass count, else B.
+struct SortResult { uint32_t* keys; uint32_t* vals; };
+SortResult radix_sort_pairs(const uint32_t* kin, const uint32_t* vin, uint32_t* ka, uint32_t* va, uint32_t* kb,
+                            uint32_t* vb, uint32_t n, uint32_t key_bits, uint32_t* scratch, hipStream_t s);
+
+// ---- build (build.hip) ------------------------------------------------------
+struct BuildArgs {
+    const float4* opos;       // [V]
+    const uint32_t* idx;      // [3T]
+    uint32_t V, T;
+    int morton_mode, delta_mode;
+    Mat4 wvp;
+    float smin[3], smax[3];   // HLSL-mode scene box
+    uint32_t* bounds;         // 6 ordered-u32 (min xyz, max xyz) for CPUTests mode
+    uint32_t* keys;           // [T] Morton codes (triangle order) -> sort input
+    uint32_t* vals;           // [T] triangle ids
+    float4* tclip;            // [3T]
+    const uint32_t* sorted_keys;  // [T]
+    const uint32_t* sorted_vals;  // [T]
+    float4* leaf;             // [3T]
+    Inner* inner;             // [T-1]
+    uint32_t* pleaf;          // [T]
+    uint32_t* pint;           // [T-1]
+    uint32_t* refit_cnt;      // [T-1]
+    float* rootbox;           // [6]
+};
+void launch_bounds(const BuildArgs& a, hipStream_t s);
+void launch_morton(const BuildArgs& a, hipStream_t s);
+void launch_leaf_karras(const BuildArgs& a, hipStream_t s);
+void launch_refit(const BuildArgs& a, hipStream_t s);
+// reference-layout export (44-B Node), 2T-1 entries
+void launch_export(const BuildArgs& a, void* out_nodes, hipStream_t s);
+// Karras + refit from given sorted codes and leaf boxes (n x 6 floats, device)
+void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t s);
+
+// ---- trace (trace.hip) ------------------------------------------------------
+struct TraceArgs {
+    const Inner* inner;
+    const float4* leaf;
+    const float* verts;       // rtbvh_vertex AoS, 8 floats each
+    const uint32_t* idx;
+    const uint32_t* matidx;
+    const Mat* mats;
+    uint32_t T, W, H, rank, nranks;
+    Mat4 wv;
+    float4* color;            // output pixels (compacted band rows when nranks > 1)
+    float* intensity;         // optional, same indexing as color
+    unsigned long long* counters;   // 8 x u64: primary, bounce, int visits, leaf visits, hits, tex hits, overflow, -
+    float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
+    float* refr_rec;          // optional refractRay records
+};
+void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, hipStream_t s);
+void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, RayQ* qout, uint32_t* qout_count,
+                   bool count, bool emit, hipStream_t s);
+
+}  // namespace rtbvh

@@ -1,0 +1,292 @@
+// trace.hip -- closest-hit traversal + shading kernels for gfx950.
+//
+// RayTraceLaunch.hlsl (primary rays, 15x15 thread groups) and
+// RayTraceReflection.hlsl (bounce, every pixel re-dispatched, idle lanes for
+// rays with intensity 0) on top of findCollision (RayTraceTraversal.hlsl:106-193).
+// Here: a wave64 traces one 8x8 pixel tile (a 256-thread workgroup = 4 tiles
+// side by side in one 8-row band, which is also the multi-GPU sharding unit);
+// every child-pair test reads ONE 64-B node record; leaves read a 48-B
+// pre-transformed triangle (getUpdateVerts hoisted to the build); the bounce
+// pass runs only over a wave-compacted queue of live rays (ballot + one atomic
+// per wave).  Traversal order, pruning and tie rules are the reference's
+// exactly, so results match the CPU oracle bit for bit.
+#include "rtbvh_internal.h"
+
+namespace rtbvh {
+namespace {
+
+constexpr uint32_t BLOCK = 256;
+constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
+
+struct Counts { uint32_t internal, leaf, overflow; };
+
+// rayTriangleCollision, RayTraceTraversal.hlsl:41-86
+__device__ __forceinline__ float ray_triangle(f3 o, f3 d, f3 p0, f3 p1, f3 p2) {
+    const f3 e1 = sub(p1, p0), e2 = sub(p2, p0);
+    f3 tmp = cross(d, e2);
+    const float dx = dot(e1, tmp);
+    if (fabsf(dx) < EPSILON) return -1.f;
+    const float idx = 1.f / dx;
+    const f3 rt = sub(o, p0);
+    const float u = dot(rt, tmp) * idx;
+    if (u < .0f || 1.f < u) return -1.f;
+    tmp = cross(rt, e1);
+    const float v = dot(d, tmp) * idx;
+    if (v < .0f || 1.f < u + v) return -1.f;
+    const float t = dot(e2, tmp) * idx;
+    if (EPSILON < t) return t;
+    return -1.f;
+}
+
+// rayBoxCollision, RayTraceTraversal.hlsl:92-104 (fminf/fmaxf drop NaN like HLSL min/max)
+__device__ __forceinline__ bool ray_box(f3 o, f3 inv, float bx0, float by0, float bz0, float bx1, float by1, float bz1,
+                                        bool hit, float best) {
+    const float tx0 = (bx0 - o.x) * inv.x, ty0 = (by0 - o.y) * inv.y, tz0 = (bz0 - o.z) * inv.z;
+    const float tx1 = (bx1 - o.x) * inv.x, ty1 = (by1 - o.y) * inv.y, tz1 = (bz1 - o.z) * inv.z;
+    const float mn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+    const float mx = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return 0 <= mx && mn <= mx && (!hit || mn <= best);
+}
+
+// findCollision, RayTraceTraversal.hlsl:106-193.  Returns hit; best_leaf = sorted leaf index.
+template <bool COUNT>
+__device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const float4* __restrict__ leaf, uint32_t T,
+                                         f3 o, f3 d, f3 inv, float& best, uint32_t& best_leaf, Counts& c) {
+    bool hit = false;
+    best = 0.f;
+    best_leaf = 0;
+    uint32_t stack[STACK_SIZE];
+    int sp = 0;
+    stack[0] = INVALID;
+    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    uint32_t guard = 2 * T + 2;   // a valid tree is walked in <= 2T-1 steps
+    do {
+        if (--guard == 0) { c.overflow++; break; }
+        if (node & LEAF_BIT) {
+            const uint32_t j = node & ~LEAF_BIT;
+            const float4* r = leaf + 3 * (size_t)j;
+            const float4 a = r[0], b = r[1], q = r[2];
+            if (COUNT) c.leaf++;
+            const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(q.x, q.y, q.z));
+            if (t != -1.f && (!hit || t < best)) {
+                best = t;
+                best_leaf = j;
+                hit = true;
+            }
+            node = stack[sp--];
+            continue;
+        }
+        if (COUNT) c.internal++;
+        const float4* r = reinterpret_cast<const float4*>(inner + node);
+        const float4 q0 = r[0], q1 = r[1], q2 = r[2];
+        const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
+        const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best);
+        const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best);
+        if (!lh && !rh) {
+            node = stack[sp--];
+        } else {
+            if (lh && rh) {
+                if (sp + 1 >= STACK_SIZE) { c.overflow++; node = stack[sp--]; continue; }
+                stack[++sp] = q3.y;
+            }
+            node = lh ? q3.x : q3.y;
+        }
+    } while (sp != -1);
+    return hit;
+}
+
+struct HitInfo {
+    float4 color;   // renderPixel(...) * specular
+    f3 hitp, nrm;
+    float shininess;
+    bool textured;
+};
+
+// getHitLoc (:15-19) + getNromalTexCoord (RayTraceHelper.hlsl:12-35) + renderPixel*specular
+// (RayTraceRender.hlsl:16-29, RayTraceLaunch.hlsl:57-59).  Texture sampling: white.
+__device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_leaf, f3 o, f3 d, float t) {
+    HitInfo h;
+    const float4* r = a.leaf + 3 * (size_t)best_leaf;
+    const float4 a0 = r[0], a1 = r[1], a2 = r[2];
+    const uint32_t tri = __float_as_uint(a0.w);
+    const f3 P0 = mk(a0.x, a0.y, a0.z), P1 = mk(a1.x, a1.y, a1.z), P2 = mk(a2.x, a2.y, a2.z);
+    f3 n[3];
+    float uv[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float* v = a.verts + 8 * (size_t)a.idx[3 * (size_t)tri + k];
+        n[k] = xform_normal(a.wv.m, mk(v[3], v[4], v[5]));
+        uv[k][0] = v[6];
+        uv[k][1] = v[7];
+    }
+    h.hitp = add(o, mul(d, t));
+    const f3 v0 = sub(P0, h.hitp), v1 = sub(P1, h.hitp), v2 = sub(P2, h.hitp);
+    const float a_0 = magnitude(cross(sub(P0, P1), sub(P0, P2)));
+    const float w1 = magnitude(cross(v1, v2)) / a_0;
+    const float w2 = magnitude(cross(v2, v0)) / a_0;
+    const float w3 = magnitude(cross(v0, v1)) / a_0;
+    const float tu = (uv[0][0] * w1 + uv[1][0] * w2) + uv[2][0] * w3;
+    const float tv = (uv[0][1] * w1 + uv[1][1] * w2) + uv[2][1] * w3;
+    (void)tu;
+    (void)tv;
+    h.nrm = add(add(mul(n[0], w1), mul(n[1], w2)), mul(n[2], w3));
+    const Mat& m = a.mats[a.matidx[tri]];
+    h.textured = m.tex_num != -1;
+    const float tx = 1.f, ty = 1.f, tz = 1.f, tw = 1.f;
+    h.color = make_float4(sat(m.ambient[0] + m.diffuse[0] * tx) * m.specular[0],
+                          sat(m.ambient[1] + m.diffuse[1] * ty) * m.specular[1],
+                          sat(m.ambient[2] + m.diffuse[2] * tz) * m.specular[2],
+                          sat(m.ambient[3] + m.diffuse[3] * tw) * m.specular[3]);
+    h.shininess = m.shininess;
+    return h;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// wave-aggregated append: one atomic per wave, lanes keep their order
+__device__ __forceinline__ uint32_t wave_append(bool active, uint32_t* counter) {
+    const uint64_t mask = __ballot(active);
+    if (mask == 0) return 0;
+    const uint32_t lane = lane_id();
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader, 64);
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    return base + (uint32_t)__popcll(mask & lt);
+}
+
+// counters: [base] internal visits, [base+1] leaf visits, [base+2] hits (base 2 primary,
+// 5 bounce), [8] stack overflows / guard trips, [9] textured hits
+template <bool COUNT>
+__device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c, uint32_t hits, uint32_t tex,
+                                             int base) {
+    unsigned long long v[5] = {c.internal, c.leaf, hits, c.overflow, tex};
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+    if (lane_id() == 0) {
+        if (COUNT) {
+            atomicAdd(&a.counters[base], v[0]);
+            atomicAdd(&a.counters[base + 1], v[1]);
+            atomicAdd(&a.counters[base + 2], v[2]);
+            atomicAdd(&a.counters[9], v[4]);
+        }
+        if (v[3]) atomicAdd(&a.counters[8], v[3]);
+    }
+}
+
+// RayTraceLaunch.hlsl:6-93
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_primary(TraceArgs a, RayQ* __restrict__ q, uint32_t* __restrict__ qcount, int emit) {
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
+    const uint32_t band = blockIdx.y * a.nranks + a.rank;
+    const uint32_t y = band * 8 + (lane >> 3);
+    const bool valid = x < a.W && y < a.H;
+    const size_t out = ((size_t)blockIdx.y * 8 + (lane >> 3)) * a.W + x;
+    Counts c = {0, 0, 0};
+    uint32_t hits = 0, tex = 0;
+    bool live = false;
+    RayQ e;
+    if (valid) {
+        const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
+        const f3 o = mk(((float)x - hw) / 4.f, ((float)y - hh) / 4.f, 0.f);   // :23-24
+        const f3 d = mk(0.f, 0.f, 1.f);
+        const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+        float best;
+        uint32_t bl;
+        float4 color;
+        float intensity = 0.f;
+        if (traverse<COUNT>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
+            hits = 1;
+            const HitInfo h = shade_hit(a, bl, o, d, best);
+            tex = h.textured;
+            intensity = h.shininess / 1000.f * 1;   // :48 (REFLECTION_DECAY 1)
+            color = h.color;
+            if (0 < intensity) {   // traced by RayTraceReflection.hlsl:17-18 only when > INTENSITY_MIN
+                const f3 ro = add(h.hitp, mul(h.nrm, .001f));   // RAY_OFFSET .001
+                const f3 rd = normalize(reflect(d, h.nrm));
+                e.idx = (uint32_t)out;
+                e.intensity = intensity;
+                e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
+                e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
+                live = true;
+            }
+        } else {
+            color = make_float4(.5f, .5f, .5f, 1.f);   // getBackground, :85-86
+        }
+        a.color[out] = color;
+        if (a.intensity) a.intensity[out] = intensity;
+    }
+    const uint32_t slot = wave_append(emit && live, qcount);
+    if (emit && live) q[slot] = e;
+    flush_counts<COUNT>(a, c, hits, tex, 2);
+}
+
+// RayTraceReflection.hlsl:6-62 over the compacted queue of live rays
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_bounce(TraceArgs a, const RayQ* __restrict__ qin, const uint32_t* __restrict__ qin_count,
+                                                  RayQ* __restrict__ qout, uint32_t* __restrict__ qout_count, int emit) {
+    const uint32_t n = *qin_count;
+    Counts c = {0, 0, 0};
+    uint32_t hits = 0, tex = 0;
+    for (uint32_t base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        bool live = false;
+        RayQ e;
+        if (i < n) {
+            e = qin[i];
+            const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
+            const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+            float best;
+            uint32_t bl;
+            float4 col = a.color[e.idx];
+            float intensity = e.intensity;
+            if (traverse<COUNT>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
+                hits++;
+                const HitInfo h = shade_hit(a, bl, o, d, best);
+                tex += h.textured;
+                col = make_float4(lerpf(col.x, h.color.x, intensity), lerpf(col.y, h.color.y, intensity),
+                                  lerpf(col.z, h.color.z, intensity), lerpf(col.w, h.color.w, intensity));
+                intensity *= h.shininess / 1000.f * 1;
+                const f3 ro = add(h.hitp, mul(h.nrm, .0001f));   // RAY_OFFSET .0001
+                const f3 rd = normalize(reflect(d, h.nrm));
+                e.intensity = intensity;
+                e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
+                e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
+                live = 0 < intensity;
+            } else {
+                col = make_float4(lerpf(col.x, .5f, intensity), lerpf(col.y, .5f, intensity),
+                                  lerpf(col.z, .5f, intensity), lerpf(col.w, 1.f, intensity));
+                intensity = 0.f;
+            }
+            a.color[e.idx] = col;
+            if (a.intensity) a.intensity[e.idx] = intensity;
+        }
+        const uint32_t slot = wave_append(emit && live, qout_count);
+        if (emit && live) qout[slot] = e;
+    }
+    flush_counts<COUNT>(a, c, hits, tex, 5);
+}
+
+}  // namespace
+
+void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, hipStream_t s) {
+    const uint32_t nbands = (a.H + 7) / 8;
+    const uint32_t my_bands = a.rank < nbands ? (nbands - a.rank + a.nranks - 1) / a.nranks : 0;
+    if (my_bands == 0 || a.W == 0) return;
+    dim3 grid((a.W + 31) / 32, my_bands);
+    if (count) hipLaunchKernelGGL(k_primary<true>, grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
+    else hipLaunchKernelGGL(k_primary<false>, grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
+}
+
+void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, RayQ* qout, uint32_t* qout_count,
+                   bool count, bool emit, hipStream_t s) {
+    const uint32_t blocks = 2048;   // grid-stride over the device-side queue length
+    if (count) hipLaunchKernelGGL(k_bounce<true>, dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, qout, qout_count, (int)emit);
+    else hipLaunchKernelGGL(k_bounce<false>, dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, qout, qout_count, (int)emit);
+}
+
+}  // namespace rtbvh

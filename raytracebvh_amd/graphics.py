@@ -1,0 +1,194 @@
+"""Host-side mirror of the reference's Manager/Graphics dispatch surface.
+
+The reference drives the path from `class Graphics : public Manager`
+(Graphics.h:16-27): onInit -> loadAssets uploads the ObjLoader arrays
+(Graphics.cpp:237-665), onUpdate writes the camera cbuffer and calls the private
+computeBVH() (Graphics.cpp:40-61, 667-831).  `Graphics` below keeps those names
+and meanings over librtbvh.so; `Context` is the thin 1:1 wrapper of the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as _L
+from .scene import Scene, camera_reference
+
+
+class Context:
+    """One rtbvh_ctx: one HIP device, one stream, the scene/BVH/frame buffers."""
+
+    def __init__(self, device: int = 0, morton_mode: int = _L.MORTON_CPUTESTS, delta_mode: int = _L.DELTA_CLZ64,
+                 flags: int = 0, scene_bb_min=(-700.0,) * 3, scene_bb_max=(700.0,) * 3, stream: int | None = None):
+        L = _L.lib()
+        cfg = _L.Config()
+        L.rtbvh_config_default(ctypes.byref(cfg))
+        cfg.device = device
+        cfg.morton_mode = morton_mode
+        cfg.delta_mode = delta_mode
+        cfg.flags = flags
+        cfg.scene_bb_min[:] = list(scene_bb_min)
+        cfg.scene_bb_max[:] = list(scene_bb_max)
+        cfg.stream = stream
+        h = ctypes.c_void_p()
+        _L.check(L.rtbvh_create(ctypes.byref(cfg), ctypes.byref(h)), None)
+        self._h = h
+        self.num_tris = 0
+        self.width = self.height = 0
+
+    # -- lifecycle --
+    def close(self):
+        if getattr(self, "_h", None):
+            _L.lib().rtbvh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st):
+        _L.check(st, self._h)
+
+    # -- inputs --
+    def set_scene(self, scene: Scene):
+        self._scene = scene   # keep arrays alive for the duration of the call (copied by the library)
+        self._check(_L.lib().rtbvh_set_scene(self._h, _L.ptr(scene.vertices), len(scene.vertices),
+                                             _L.ptr(scene.indices), len(scene.indices), _L.ptr(scene.mat_indices),
+                                             _L.ptr(scene.materials), len(scene.materials), None, 0))
+        self.num_tris = scene.num_tris
+
+    def set_camera(self, wvp, wv):
+        wvp = np.ascontiguousarray(wvp, dtype=np.float32).reshape(16)
+        wv = np.ascontiguousarray(wv, dtype=np.float32).reshape(16)
+        self._check(_L.lib().rtbvh_set_camera(self._h, _L.ptr(wvp), _L.ptr(wv)))
+
+    # -- hot path --
+    def build(self, sync: bool = True):
+        L = _L.lib()
+        self._check(L.rtbvh_build(self._h) if sync else L.rtbvh_build_async(self._h))
+
+    def trace(self, width: int, height: int, bounces: int = 1, sync: bool = True):
+        L = _L.lib()
+        f = L.rtbvh_trace if sync else L.rtbvh_trace_async
+        self._check(f(self._h, width, height, bounces))
+        self.width, self.height = width, height
+
+    def compute_bvh(self, width: int, height: int, bounces: int = 1):
+        self._check(_L.lib().rtbvh_compute_bvh(self._h, width, height, bounces))
+        self.width, self.height = width, height
+
+    def trace_band_async(self, width: int, height: int, bounces: int, rank: int, nranks: int, dev_out_ptr: int,
+                         stream_ptr: int | None = None):
+        self._check(_L.lib().rtbvh_trace_band_async(self._h, width, height, bounces, rank, nranks,
+                                                    ctypes.c_void_p(dev_out_ptr),
+                                                    ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def synchronize(self):
+        self._check(_L.lib().rtbvh_synchronize(self._h))
+
+    # -- outputs --
+    def read_framebuffer(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.float32)
+        self._check(_L.lib().rtbvh_read_framebuffer(self._h, _L.ptr(out)))
+        return out
+
+    def read_intensity(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width), np.float32)
+        self._check(_L.lib().rtbvh_read_intensity(self._h, _L.ptr(out)))
+        return out
+
+    def framebuffer_device_ptr(self) -> int:
+        return _L.lib().rtbvh_framebuffer_device(self._h) or 0
+
+    def read_bvh(self) -> np.ndarray:
+        out = np.zeros(2 * self.num_tris - 1, dtype=_L.NODE_DTYPE)
+        self._check(_L.lib().rtbvh_read_bvh(self._h, ctypes.c_void_p(out.ctypes.data), len(out)))
+        return out
+
+    def read_morton(self) -> np.ndarray:
+        out = np.zeros(self.num_tris, np.uint32)
+        self._check(_L.lib().rtbvh_read_morton(self._h, _L.ptr(out)))
+        return out
+
+    def read_sorted(self):
+        keys = np.zeros(self.num_tris, np.uint32)
+        ids = np.zeros(self.num_tris, np.uint32)
+        self._check(_L.lib().rtbvh_read_sorted(self._h, _L.ptr(keys), _L.ptr(ids)))
+        return keys, ids
+
+    def stats(self) -> dict:
+        """rtbvh_get_stats: counts of the last trace; hipEvent averages since reset_stats()."""
+        s = _L.Stats()
+        self._check(_L.lib().rtbvh_get_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        self._check(_L.lib().rtbvh_reset_stats(self._h))
+
+    def set_flags(self, flags: int):
+        self._check(_L.lib().rtbvh_set_flags(self._h, flags))
+
+    # -- primitives --
+    def sort_pairs(self, keys: np.ndarray, vals: np.ndarray, key_bits: int = 32):
+        keys = np.ascontiguousarray(keys, np.uint32)
+        vals = np.ascontiguousarray(vals, np.uint32)
+        ko = np.zeros_like(keys)
+        vo = np.zeros_like(vals)
+        self._check(_L.lib().rtbvh_sort_pairs_host(self._h, _L.ptr(keys), _L.ptr(vals), _L.ptr(ko), _L.ptr(vo),
+                                                   len(keys), key_bits))
+        return ko, vo
+
+    def sort_pairs_device(self, keys_ptr: int, vals_ptr: int, keys_out_ptr: int, vals_out_ptr: int, n: int,
+                          key_bits: int = 32):
+        self._check(_L.lib().rtbvh_sort_pairs_async(self._h, ctypes.c_void_p(keys_ptr), ctypes.c_void_p(vals_ptr),
+                                                    ctypes.c_void_p(keys_out_ptr), ctypes.c_void_p(vals_out_ptr),
+                                                    n, key_bits))
+
+    def build_from_codes(self, sorted_codes: np.ndarray, leaf_boxes: np.ndarray) -> np.ndarray:
+        codes = np.ascontiguousarray(sorted_codes, np.uint32)
+        boxes = np.ascontiguousarray(leaf_boxes, np.float32).reshape(-1, 6)
+        out = np.zeros(2 * len(codes) - 1, dtype=_L.NODE_DTYPE)
+        self._check(_L.lib().rtbvh_build_from_codes(self._h, _L.ptr(codes), _L.ptr(boxes), len(codes),
+                                                    ctypes.c_void_p(out.ctypes.data)))
+        return out
+
+
+class Graphics:
+    """Graphics : Manager (Graphics.h:16-27) over librtbvh.so.
+
+    onInit(scene)  ~ Graphics::onInit -> loadAssets (Graphics.cpp:34-38, 237-665)
+    onUpdate()     ~ Graphics::onUpdate: camera + computeBVH (Graphics.cpp:40-61)
+    computeBVH()   ~ Graphics::computeBVH (Graphics.cpp:667-831)
+    """
+
+    def __init__(self, width: int = 800, height: int = 800, bounces: int = 3, **ctx_kwargs):
+        # main.cpp:7 opens an 800x800 window; Graphics.cpp:795 runs 3 reflection passes
+        self.width, self.height, self.bounces = width, height, bounces
+        self.ctx = Context(**ctx_kwargs)
+
+    def onInit(self, scene: Scene):  # noqa: N802
+        self.ctx.set_scene(scene)
+
+    def onUpdate(self):  # noqa: N802
+        wvp, wv = camera_reference(self.width, self.height)
+        self.ctx.set_camera(wvp, wv)
+        self.computeBVH()
+
+    def computeBVH(self):  # noqa: N802
+        self.ctx.compute_bvh(self.width, self.height, self.bounces)
+
+    def framebuffer(self) -> np.ndarray:
+        """reflectRay[].color as (H, W, 4) f32 (the framebuffer of record, RayTraceBVHPS.hlsl:13-16)."""
+        return self.ctx.read_framebuffer()
+
+    def onDestroy(self):  # noqa: N802
+        self.ctx.close()

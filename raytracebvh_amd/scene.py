@@ -1,0 +1,109 @@
+"""Scene inputs of the path (vertices, indices, material indices, materials).
+
+Host-side mirror of ObjLoader's getters (ObjectFileLoader.h:120-240); the
+loading itself is native (rtbvh_scene_load_obj in librtbvh.so).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as _L
+
+
+@dataclass
+class Scene:
+    vertices: np.ndarray                 # (V, 8) f32: position xyz, normal xyz, texcoord uv (32-B Vertex)
+    indices: np.ndarray                  # (3T,) u32
+    mat_indices: np.ndarray              # (T,) u32
+    materials: np.ndarray                # (M,) MATERIAL_DTYPE (68-B MaterialUpload)
+    texture_paths: list = field(default_factory=list)
+
+    def __post_init__(self):
+        self.vertices = np.ascontiguousarray(self.vertices, dtype=np.float32).reshape(-1, 8)
+        self.indices = np.ascontiguousarray(self.indices, dtype=np.uint32).ravel()
+        self.mat_indices = np.ascontiguousarray(self.mat_indices, dtype=np.uint32).ravel()
+        m = np.ascontiguousarray(self.materials)
+        if m.dtype != _L.MATERIAL_DTYPE:
+            m = np.frombuffer(np.ascontiguousarray(m, dtype=np.uint8).tobytes(), dtype=_L.MATERIAL_DTYPE).copy()
+        self.materials = m
+
+    @property
+    def num_tris(self) -> int:
+        return len(self.indices) // 3
+
+    @property
+    def material_blob(self) -> np.ndarray:
+        return self.materials.view(np.uint8).reshape(-1, 68)
+
+    # ObjLoader getter names (ObjectFileLoader.h:139-212)
+    def getNumVertices(self) -> int:  # noqa: N802
+        return len(self.vertices)
+
+    def getNumIndices(self) -> int:  # noqa: N802
+        return len(self.indices)
+
+    def getNumMaterialIndices(self) -> int:  # noqa: N802
+        return len(self.mat_indices)
+
+    def getNumMaterials(self) -> int:  # noqa: N802
+        return len(self.materials)
+
+
+def _from_native(handle) -> Scene:
+    L = _L.lib()
+    nv = L.rtbvh_scene_num_vertices(handle)
+    ni = L.rtbvh_scene_num_indices(handle)
+    nm = L.rtbvh_scene_num_materials(handle)
+    nt = L.rtbvh_scene_num_textures(handle)
+    verts = np.ctypeslib.as_array(ctypes.cast(L.rtbvh_scene_vertices(handle), ctypes.POINTER(ctypes.c_float)),
+                                  shape=(nv * 8,)).copy() if nv else np.zeros(0, np.float32)
+    idx = np.ctypeslib.as_array(ctypes.cast(L.rtbvh_scene_indices(handle), ctypes.POINTER(ctypes.c_uint32)),
+                                shape=(ni,)).copy() if ni else np.zeros(0, np.uint32)
+    midx = np.ctypeslib.as_array(ctypes.cast(L.rtbvh_scene_mat_indices(handle), ctypes.POINTER(ctypes.c_uint32)),
+                                 shape=(ni // 3,)).copy() if ni else np.zeros(0, np.uint32)
+    mats = np.ctypeslib.as_array(ctypes.cast(L.rtbvh_scene_materials(handle), ctypes.POINTER(ctypes.c_uint8)),
+                                 shape=(nm * 68,)).copy()
+    paths = [L.rtbvh_scene_texture_path(handle, k).decode() for k in range(nt)]
+    return Scene(verts.reshape(-1, 8), idx, midx, mats.view(_L.MATERIAL_DTYPE), paths)
+
+
+def load_obj(path: str) -> Scene:
+    """ObjLoader::Load (ObjectFileLoader.cpp:470-547) via the native loader."""
+    L = _L.lib()
+    h = ctypes.c_void_p()
+    _L.check(L.rtbvh_scene_load_obj(os.fsencode(path), ctypes.byref(h)))
+    try:
+        return _from_native(h)
+    finally:
+        L.rtbvh_scene_free(h)
+
+
+def synthetic(ntris: int, seed: int = 0x5EED0004, half_extent=(50.0, 50.0, 50.0)) -> Scene:
+    """SURVEY §8(d) synthetic scene (C4: seed 0x5EED0004, +-50; C5: 0x5EED0005, (100,100,50))."""
+    L = _L.lib()
+    h = ctypes.c_void_p()
+    half = np.asarray(half_extent, dtype=np.float32)
+    _L.check(L.rtbvh_scene_synthetic(seed, ntris, _L.ptr(half), ctypes.byref(h)))
+    try:
+        return _from_native(h)
+    finally:
+        L.rtbvh_scene_free(h)
+
+
+def load_npz(path: str) -> Scene:
+    """Scene fixture written by tests/golden/make_golden.py (parsed reference Obj/ meshes)."""
+    z = np.load(path)
+    names = [str(x) for x in z["texture_names"]] if "texture_names" in z else []
+    return Scene(z["vertices"], z["indices"], z["mat_indices"], z["material_blob"], names)
+
+
+def camera_reference(width: int, height: int):
+    """Graphics::onUpdate camera (Graphics.cpp:44-53): returns (WVP, WV) as (4,4) f32, row-vector convention."""
+    wvp = np.zeros(16, np.float32)
+    wv = np.zeros(16, np.float32)
+    _L.lib().rtbvh_camera_reference(width, height, _L.ptr(wvp), _L.ptr(wv))
+    return wvp.reshape(4, 4), wv.reshape(4, 4)

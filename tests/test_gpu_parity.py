@@ -1,0 +1,273 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference's own golden outputs.  Integer/index work must be bit-exact; pixel RGB
+is compared with a 1e-4 tolerance (north_star) and is in fact expected to be
+bit-identical because both sides use the same IEEE op sequence without FMA."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import raytracebvh_amd as rt
+from oracle import lib as orc
+from tests.conftest import GOLDEN, load_scene_fixture
+
+pytestmark = pytest.mark.gpu
+RGB_TOL = 1e-4
+
+
+def fnv_u32_values(vals):
+    h = 1469598103934665603
+    for v in vals:
+        h ^= int(v) & 0xFFFFFFFF
+        h = (h * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = rt.Context(device=0, flags=rt.FLAG_TIMING)
+    yield c
+    c.close()
+
+
+def _oscene(s):
+    return orc.Scene(s.vertices, s.indices, s.mat_indices, s.material_blob)
+
+
+def _assert_nodes_equal(got, want, n):
+    for f in ("parent", "child_l", "child_r"):
+        np.testing.assert_array_equal(got[f], want[f], err_msg=f)
+    np.testing.assert_array_equal(got["code"][:n], want["code"][:n])
+    np.testing.assert_array_equal(got["index"][:n], want["index"][:n])
+    np.testing.assert_array_equal(got["bb_min"], want["bb_min"])
+    np.testing.assert_array_equal(got["bb_max"], want["bb_max"])
+
+
+# ---------------------------------------------------------------- sort
+@pytest.mark.parametrize("n", [1, 2, 3, 255, 4095, 4096, 4097, 12289, 100_003])
+@pytest.mark.parametrize("key_bits", [32, 30])
+def test_sort_pairs_stable(ctx, n, key_bits):
+    rng = np.random.default_rng(n + key_bits)
+    keys = rng.integers(0, 1 << key_bits, size=n, dtype=np.uint64).astype(np.uint32)
+    keys[::7] = keys[0]   # duplicates
+    vals = np.arange(n, dtype=np.uint32)
+    ko, vo = ctx.sort_pairs(keys, vals, key_bits)
+    perm = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(ko, keys[perm])
+    np.testing.assert_array_equal(vo, perm.astype(np.uint32))
+
+
+def test_sort_matches_reference_combo(ctx):
+    z = np.load(os.path.join(GOLDEN, "combo.npz"))
+    keys = z["input_codes"]
+    ko, vo = ctx.sort_pairs(keys, np.arange(len(keys), dtype=np.uint32), 30)
+    np.testing.assert_array_equal(ko, z["sorted_codes"])
+    np.testing.assert_array_equal(vo, orc.split_sort(keys))
+
+
+def test_sort_large_property(ctx):
+    """10M keys (BASELINE C4 size): sortedness + permutation + stability."""
+    n = 10_000_000
+    rng = np.random.default_rng(4)
+    keys = rng.integers(0, 1 << 30, size=n, dtype=np.uint32)
+    keys[: n // 4] &= np.uint32(0x3FF00000)   # heavy duplicates
+    ko, vo = ctx.sort_pairs(keys, np.arange(n, dtype=np.uint32), 30)
+    assert (np.diff(ko.astype(np.int64)) >= 0).all()
+    np.testing.assert_array_equal(keys[vo], ko)
+    np.testing.assert_array_equal(np.sort(vo), np.arange(n, dtype=np.uint32))
+    eq = ko[1:] == ko[:-1]
+    assert (vo[1:][eq] > vo[:-1][eq]).all()   # stable
+
+
+# ---------------------------------------------------------------- Karras + refit
+@pytest.mark.parametrize("mode", [rt.DELTA_CPUTESTS, rt.DELTA_CLZ64])
+def test_karras_refit_matches_reference_combo(mode):
+    """RadixBVHCombo: every parent/child link and refit box of the reference's 11,775 nodes."""
+    z = np.load(os.path.join(GOLDEN, "combo.npz"))
+    n = len(z["sorted_codes"])
+    boxes = np.concatenate([z["bb_min"][:n], z["bb_max"][:n]], axis=1)
+    with rt.Context(device=0, delta_mode=mode) as c:
+        nodes = c.build_from_codes(z["sorted_codes"], boxes)
+    np.testing.assert_array_equal(nodes["parent"], z["parent"].astype(np.uint32))
+    np.testing.assert_array_equal(nodes["child_l"], z["child_l"].astype(np.uint32))
+    np.testing.assert_array_equal(nodes["child_r"], z["child_r"].astype(np.uint32))
+    np.testing.assert_array_equal(nodes["bb_min"], z["bb_min"])
+    np.testing.assert_array_equal(nodes["bb_max"], z["bb_max"])
+    kat = json.load(open(os.path.join(GOLDEN, "shadersim_kats.json")))["combo_topology_fnv"]["value"]
+    links = np.stack([nodes["parent"], nodes["child_l"], nodes["child_r"]], 1).ravel()
+    assert "%016x" % fnv_u32_values(links) == kat
+
+
+def test_karras_paper_example():
+    z = np.load(os.path.join(GOLDEN, "bvhct.npz"))
+    codes = z["code"][:8].astype(np.uint32)
+    boxes = np.zeros((8, 6), np.float32)
+    with rt.Context(device=0) as c:
+        nodes = c.build_from_codes(codes, boxes)
+    np.testing.assert_array_equal(nodes["child_l"][8:], z["child_l"][8:].astype(np.uint32))
+    np.testing.assert_array_equal(nodes["child_r"][8:], z["child_r"][8:].astype(np.uint32))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 65_537])
+def test_from_codes_random_duplicates_vs_oracle(n):
+    rng = np.random.default_rng(n)
+    codes = np.sort(rng.integers(0, 1 << 12, size=n, dtype=np.uint32) << np.uint32(18))
+    lo = rng.standard_normal((n, 3)).astype(np.float32)
+    hi = lo + rng.random((n, 3), dtype=np.float32)
+    with rt.Context(device=0) as c:
+        nodes = c.build_from_codes(codes, np.concatenate([lo, hi], 1))
+    if n == 1:
+        assert nodes["parent"][0] == 0xFFFFFFFF
+        return
+    parent, cl, cr = orc.karras(codes, orc.DELTA_CLZ64)
+    bmin = np.zeros((2 * n - 1, 3), np.float32)
+    bmax = np.zeros((2 * n - 1, 3), np.float32)
+    bmin[:n], bmax[:n] = lo, hi
+    bmin, bmax, _ = orc.refit(n, parent, cl, cr, bmin, bmax)
+    np.testing.assert_array_equal(nodes["parent"], parent)
+    np.testing.assert_array_equal(nodes["child_l"], cl)
+    np.testing.assert_array_equal(nodes["child_r"], cr)
+    np.testing.assert_array_equal(nodes["bb_min"], bmin)
+    np.testing.assert_array_equal(nodes["bb_max"], bmax)
+
+
+# ---------------------------------------------------------------- full build on the reference scenes
+@pytest.mark.parametrize("name", ["Rect", "Image_Test", "Test"])
+@pytest.mark.parametrize("morton_mode", [rt.MORTON_CPUTESTS, rt.MORTON_HLSL])
+def test_build_matches_oracle_on_obj(name, morton_mode):
+    d = load_scene_fixture(name)
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    wvp, wv = rt.camera_reference(1920, 1080)
+    with rt.Context(device=0, morton_mode=morton_mode) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.build()
+        codes = c.read_morton()
+        keys, ids = c.read_sorted()
+        nodes = c.read_bvh()
+    os_ = _oscene(s)
+    ocodes = orc.morton_tris(os_, morton_mode, wvp, (-700,) * 3, (700,) * 3)
+    np.testing.assert_array_equal(codes, ocodes)
+    if morton_mode == rt.MORTON_CPUTESTS:
+        kat = json.load(open(os.path.join(GOLDEN, "shadersim_kats.json")))[name]
+        assert "%016x" % fnv_u32_values(codes) == kat["fnv"]
+    perm = orc.split_sort(ocodes)
+    np.testing.assert_array_equal(ids, perm)
+    np.testing.assert_array_equal(keys, ocodes[perm])
+    onodes = orc.build(os_, wvp, morton_mode=morton_mode, sort_mode=0)
+    _assert_nodes_equal(nodes, onodes, s.num_tris)
+
+
+@pytest.mark.parametrize("ntris", [1, 2, 5, 1000, 200_000])
+def test_build_matches_oracle_synthetic(ntris):
+    s = rt.synthetic(ntris, seed=0x5EED0004, half_extent=(50, 50, 50))
+    wvp, wv = rt.camera_reference(1920, 1080)
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.build()
+        nodes = c.read_bvh()
+    onodes = orc.build(_oscene(s), wvp)
+    _assert_nodes_equal(nodes, onodes, ntris)
+
+
+def test_build_10m_tree_properties():
+    """C4 size: 10M triangles.  Valid tree (one parent per node), boxes nest, codes sorted."""
+    n = 10_000_000
+    s = rt.synthetic(n, seed=0x5EED0004, half_extent=(50, 50, 50))
+    wvp, wv = rt.camera_reference(1920, 1080)
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.build()
+        nodes = c.read_bvh()
+        keys, ids = c.read_sorted()
+    assert (np.diff(keys.astype(np.int64)) >= 0).all()
+    np.testing.assert_array_equal(np.sort(ids), np.arange(n, dtype=np.uint32))
+    cl = nodes["child_l"][n:].astype(np.int64)
+    cr = nodes["child_r"][n:].astype(np.int64)
+    counts = np.bincount(np.concatenate([cl, cr]), minlength=2 * n - 1)
+    assert counts[n] == 0 and (np.delete(counts, n) == 1).all()
+    np.testing.assert_array_equal(nodes["parent"][cl], np.arange(n, 2 * n - 1))
+    np.testing.assert_array_equal(nodes["parent"][cr], np.arange(n, 2 * n - 1))
+    for side in (cl, cr):
+        assert (nodes["bb_min"][side] >= nodes["bb_min"][n:]).all()
+        assert (nodes["bb_max"][side] <= nodes["bb_max"][n:]).all()
+
+
+# ---------------------------------------------------------------- trace
+def _trace_both(s, W, H, bounces, rows=None, flags=0):
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=flags | rt.FLAG_COUNT_VISITS) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, bounces)
+        fb = c.read_framebuffer()
+        inten = c.read_intensity()
+        nodes = c.read_bvh()
+        st = c.stats()
+    r0, r1, step = rows if rows else (0, H, 1)
+    ofb, oint, ost = orc.trace(_oscene(s), nodes, wvp, wv, W, H, bounces, r0, r1, step, want_intensity=True)
+    return fb[r0:r1:step], inten[r0:r1:step], st, ofb, oint, ost
+
+
+@pytest.mark.parametrize("name,W,H,bounces", [("Rect", 320, 240, 1), ("Image_Test", 1920, 1080, 0),
+                                               ("Test", 1920, 1080, 1), ("Test", 800, 800, 3)])
+def test_trace_matches_oracle_on_obj(name, W, H, bounces):
+    d = load_scene_fixture(name)
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    fb, inten, st, ofb, oint, ost = _trace_both(s, W, H, bounces)
+    np.testing.assert_allclose(fb, ofb, atol=RGB_TOL, rtol=0)
+    assert np.array_equal(fb, ofb), "expected bit-identical pixels"
+    np.testing.assert_array_equal(inten, oint)
+    assert sum(st["internal_visits"]) == ost["internal_visits"] and sum(st["leaf_visits"]) == ost["leaf_visits"]
+    assert sum(st["hits"]) == ost["hits"] and st["textured_hits"] == ost["textured_hits"]
+    assert st["bounce_rays"] == ost["bounce"] and st["stack_overflows"] == 0
+    assert ost["hits"] > 0
+
+
+def test_trace_synthetic_sampled_rows():
+    """C5 scene at reduced size: 500k triangles, 1920x1080, every 37th row vs oracle."""
+    s = rt.synthetic(500_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    fb, inten, st, ofb, oint, ost = _trace_both(s, 1920, 1080, 1, rows=(3, 1080, 37))
+    np.testing.assert_allclose(fb, ofb, atol=RGB_TOL, rtol=0)
+    assert np.array_equal(fb, ofb)
+    np.testing.assert_array_equal(inten, oint)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_band_split_reassembles_full_frame(nranks):
+    import torch
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    W, H = 640, 357
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        full = c.read_framebuffer()
+        frame = np.zeros_like(full)
+        for r in range(nranks):
+            rows = rt.lib().rtbvh_band_rows(H, r, nranks)
+            buf = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda:0")
+            c.trace_band_async(W, H, 1, r, nranks, buf.data_ptr())
+            c.synchronize()
+            got = buf.cpu().numpy()
+            ys = [y for b in range(r, (H + 7) // 8, nranks) for y in range(8 * b, min(8 * b + 8, H))]
+            frame[ys] = got
+    np.testing.assert_array_equal(frame, full)
+
+
+def test_errors_are_reported():
+    with rt.Context(device=0) as c:
+        with pytest.raises(rt.RtbvhError) as e:
+            c.build()
+        assert e.value.status == 4   # NOT_READY
+        d = load_scene_fixture("Rect")
+        bad = d["indices"].copy()
+        bad[0] = 10_000
+        with pytest.raises(rt.RtbvhError) as e:
+            c.set_scene(rt.Scene(d["vertices"], bad, d["mat_indices"], d["material_blob"]))
+        assert e.value.status == 1

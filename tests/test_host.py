@@ -1,0 +1,120 @@
+"""CPU-only checks of librtbvh.so: it loads, exports every symbol include/rtbvh.h
+declares, and its host-side pieces (OBJ loader, synthetic generator, camera,
+band split) agree with independent restatements.  No compute call needs a GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import raytracebvh_amd as rt
+from raytracebvh_amd import _lib
+from tests.conftest import REPO, load_scene_fixture
+
+
+def test_library_exports_every_header_symbol():
+    header = open(os.path.join(REPO, "include", "rtbvh.h")).read()
+    declared = set(re.findall(r"\b(rtbvh_[a-z_0-9]+)\s*\(", header))
+    declared -= {"rtbvh_status"}
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    L = rt.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.rtbvh_abi_version() == 1
+
+
+def test_layout_sizes():
+    assert rt.NODE_DTYPE.itemsize == 44 and rt.MATERIAL_DTYPE.itemsize == 68
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/Obj"), reason="reference not mounted")
+@pytest.mark.parametrize("name", ["Rect", "Image_Test", "Test"])
+def test_native_obj_loader_matches_oracle_loader(name):
+    s = rt.load_obj(f"/root/reference/Obj/{name}.obj")
+    f = load_scene_fixture(name)
+    np.testing.assert_array_equal(s.vertices, f["vertices"])
+    np.testing.assert_array_equal(s.indices, f["indices"])
+    np.testing.assert_array_equal(s.mat_indices, f["mat_indices"])
+    np.testing.assert_array_equal(s.material_blob, f["material_blob"])
+    assert [os.path.basename(p) for p in s.texture_paths] == [str(x) for x in f["texture_names"]]
+
+
+def test_obj_loader_quirks(tmp_path):
+    """Dedup by position, normal z ignored (Helper.h:11-14), d sets alpha, Tr ignored."""
+    (tmp_path / "q.mtl").write_text("newmtl A\nKd 0.5 0.25 0.125\nd 0.5\nTr 0.9\nNs 42\nmap_Kd t.bmp\nnewmtl B\n")
+    (tmp_path / "q.obj").write_text(
+        "mtllib q.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\nvn 0 0 -1\nvt 0 0\n"
+        "usemtl B\nf 1/1/1 2/1/1 3/1/1\nusemtl A\nf 1/1/2 2/1/2 3/1/1\n")
+    s = rt.load_obj(str(tmp_path / "q.obj"))
+    assert len(s.vertices) == 3                      # normals differing only in z merged
+    np.testing.assert_array_equal(s.indices, [0, 1, 2, 0, 1, 2])
+    np.testing.assert_array_equal(s.mat_indices, [1, 0])
+    a, b = s.materials
+    assert a["alpha"] == np.float32(0.5) and a["shininess"] == 42 and a["tex_num"] == 0
+    np.testing.assert_array_equal(a["diffuse"], np.float32([0.5, 0.25, 0.125, 1]))
+    np.testing.assert_array_equal(b["ambient"], np.float32([0.2, 0.2, 0.2, 1]))   # Base_Mat
+    assert b["tex_num"] == -1
+
+
+def test_obj_loader_missing_file_is_io_error():
+    with pytest.raises(rt.RtbvhError) as e:
+        rt.load_obj("/nonexistent/x.obj")
+    assert e.value.status == _lib.ERR_IO
+
+
+def _synthetic_numpy(seed, ntris, half):
+    """Independent numpy restatement of the SURVEY §8(d) generator."""
+    M = (1 << 64) - 1
+    k = np.arange(1, ntris * 12 + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)) & np.uint64(M)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    u = u.reshape(ntris, 12)
+    half = np.asarray(half, np.float32)
+    c = (u[:, :3] * np.float32(2.0) - np.float32(1.0)) * half
+    v = c[:, None, :] + (u[:, 3:].reshape(ntris, 3, 3) - np.float32(0.5)) * np.float32(1.0)
+    return v.astype(np.float32)
+
+
+def test_synthetic_generator_matches_numpy_restatement():
+    s = rt.synthetic(1000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    v = _synthetic_numpy(0x5EED0005, 1000, (100, 100, 50))
+    np.testing.assert_array_equal(s.vertices[:, :3].reshape(1000, 3, 3), v)
+    np.testing.assert_array_equal(s.indices, np.arange(3000))
+    n = s.vertices[:, 3:6]
+    assert np.allclose(np.linalg.norm(n, axis=1), 1, atol=1e-6)
+    assert s.materials[0]["shininess"] == 300 and s.materials[0]["tex_num"] == -1
+
+
+def test_camera_matches_oracle():
+    from oracle import lib as orc
+    for W, H in ((1920, 1080), (3840, 2160), (800, 800)):
+        a = rt.camera_reference(W, H)
+        b = orc.camera_reference(W, H)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+    wvp, _ = rt.camera_reference(1920, 1080)
+    # SURVEY §8(d) quotes these WVP rows at 1920x1080
+    np.testing.assert_allclose(wvp[0], [4.291935, 0, 0, 0], atol=1e-5)
+    np.testing.assert_allclose(wvp[3], [0, 0, 100.03492, 100.12492], atol=1e-3)
+
+
+@pytest.mark.parametrize("H,n", [(1080, 1), (1080, 2), (1080, 8), (2160, 8), (7, 3), (17, 4)])
+def test_band_rows_partition_the_frame(H, n):
+    L = rt.lib()
+    rows = [L.rtbvh_band_rows(H, r, n) for r in range(n)]
+    assert sum(rows) == H
+    want = [sum(min(8, H - 8 * b) for b in range(r, (H + 7) // 8, n)) for r in range(n)]
+    assert rows == want
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(rt.RtbvhError) as e:
+        rt.Context()
+    assert e.value.status == _lib.ERR_NO_DEVICE
