@@ -35,7 +35,8 @@ struct rtbvh_ctx {
     uint32_t* d_sort_scratch = nullptr;
     float4 *d_tclip = nullptr, *d_leaf = nullptr;
     Inner* d_inner = nullptr;
-    uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr, *d_bounds = nullptr;
+    uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr;
+    float* d_bounds = nullptr;
     float* d_rootbox = nullptr;
     SortResult sorted{nullptr, nullptr};
 
@@ -105,7 +106,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
     HIPC(c, dalloc(c->d_cnt, ni));
-    HIPC(c, dalloc(c->d_bounds, 8));
+    HIPC(c, dalloc(c->d_bounds, BOUNDS_WORDS));
     HIPC(c, dalloc(c->d_rootbox, 8));
     c->cap_T = T;
     return RTBVH_OK;
@@ -357,8 +358,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     hipEvent_t* ev = c->evb[c->n_builds % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (c->cfg.morton_mode == RTBVH_MORTON_CPUTESTS) {
-        HIPC(c, hipMemsetAsync(c->d_bounds, 0xFF, 3 * sizeof(uint32_t), s));
-        HIPC(c, hipMemsetAsync(c->d_bounds + 3, 0x00, 3 * sizeof(uint32_t), s));
         launch_bounds(a, s);
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));

@@ -37,13 +37,12 @@ __device__ __forceinline__ uint32_t quantise_hlsl(float p) {
     return (uint32_t)p;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_bounds(const float4* __restrict__ opos, uint32_t V, uint32_t* __restrict__ bounds) {
-    f3 mn = mk(INFINITY, INFINITY, INFINITY), mx = mk(-INFINITY, -INFINITY, -INFINITY);
-    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < V; i += (size_t)gridDim.x * BLOCK) {
-        float4 p = opos[i];
-        mn = vmin(mn, mk(p.x, p.y, p.z));
-        mx = vmax(mx, mk(p.x, p.y, p.z));
-    }
+// Scene AABB of the object-space vertices (ShaderSim/main.cpp:277-285), two launches
+// without global atomics: per-block partials (wave shuffles + LDS), then one block
+// reduces the partials.  bounds layout: [0..5] = min xyz, max xyz; [8..] partials.
+constexpr uint32_t BOUNDS_BLOCKS = 1024;
+
+__device__ __forceinline__ void reduce_box_block(f3& mn, f3& mx, float* s_red /*4*6*/) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         mn.x = fminf(mn.x, __shfl_xor(mn.x, off, 64));
@@ -53,13 +52,47 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(const float4* __restrict__ opo
         mx.y = fmaxf(mx.y, __shfl_xor(mx.y, off, 64));
         mx.z = fmaxf(mx.z, __shfl_xor(mx.z, off, 64));
     }
+    const uint32_t w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&bounds[0], f2ord(mn.x));
-        atomicMin(&bounds[1], f2ord(mn.y));
-        atomicMin(&bounds[2], f2ord(mn.z));
-        atomicMax(&bounds[3], f2ord(mx.x));
-        atomicMax(&bounds[4], f2ord(mx.y));
-        atomicMax(&bounds[5], f2ord(mx.z));
+        s_red[6 * w + 0] = mn.x; s_red[6 * w + 1] = mn.y; s_red[6 * w + 2] = mn.z;
+        s_red[6 * w + 3] = mx.x; s_red[6 * w + 4] = mx.y; s_red[6 * w + 5] = mx.z;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; k++) {
+            mn = vmin(mn, mk(s_red[6 * k + 0], s_red[6 * k + 1], s_red[6 * k + 2]));
+            mx = vmax(mx, mk(s_red[6 * k + 3], s_red[6 * k + 4], s_red[6 * k + 5]));
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_bounds(const float4* __restrict__ opos, uint32_t V, float* __restrict__ bounds) {
+    __shared__ float s_red[24];
+    f3 mn = mk(INFINITY, INFINITY, INFINITY), mx = mk(-INFINITY, -INFINITY, -INFINITY);
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < V; i += (size_t)gridDim.x * BLOCK) {
+        const float4 p = opos[i];
+        mn = vmin(mn, mk(p.x, p.y, p.z));
+        mx = vmax(mx, mk(p.x, p.y, p.z));
+    }
+    reduce_box_block(mn, mx, s_red);
+    if (threadIdx.x == 0) {
+        float* o = bounds + 8 + 6 * (size_t)blockIdx.x;
+        o[0] = mn.x; o[1] = mn.y; o[2] = mn.z; o[3] = mx.x; o[4] = mx.y; o[5] = mx.z;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_bounds_final(float* __restrict__ bounds, uint32_t nparts) {
+    __shared__ float s_red[24];
+    f3 mn = mk(INFINITY, INFINITY, INFINITY), mx = mk(-INFINITY, -INFINITY, -INFINITY);
+    for (uint32_t i = threadIdx.x; i < nparts; i += BLOCK) {
+        const float* p = bounds + 8 + 6 * (size_t)i;
+        mn = vmin(mn, mk(p[0], p[1], p[2]));
+        mx = vmax(mx, mk(p[3], p[4], p[5]));
+    }
+    reduce_box_block(mn, mx, s_red);
+    if (threadIdx.x == 0) {
+        bounds[0] = mn.x; bounds[1] = mn.y; bounds[2] = mn.z;
+        bounds[3] = mx.x; bounds[4] = mx.y; bounds[5] = mx.z;
     }
 }
 
@@ -73,8 +106,8 @@ __global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
     const f3 c0 = xform_point(a.wvp.m, p0), c1 = xform_point(a.wvp.m, p1), c2 = xform_point(a.wvp.m, p2);
     uint32_t code;
     if (a.morton_mode == 0) {
-        const f3 mn = mk(ord2f(a.bounds[0]), ord2f(a.bounds[1]), ord2f(a.bounds[2]));
-        const f3 mx = mk(ord2f(a.bounds[3]), ord2f(a.bounds[4]), ord2f(a.bounds[5]));
+        const f3 mn = mk(a.bounds[0], a.bounds[1], a.bounds[2]);
+        const f3 mx = mk(a.bounds[3], a.bounds[4], a.bounds[5]);
         const float xv = p0.x + p1.x + p2.x, yv = p0.y + p1.y + p2.y, zv = p0.z + p1.z + p2.z;
         const uint32_t qx = quantise_cputests((xv / 3.f - mn.x) / (mx.x - mn.x));
         const uint32_t qy = quantise_cputests((yv / 3.f - mn.y) / (mx.y - mn.y));
@@ -178,10 +211,32 @@ __global__ __launch_bounds__(BLOCK) void k_karras_only(BuildArgs a) {
 
 // ---- refit (BVHConstructP2.hlsl:8-37) -----------------------------------------
 // One thread per leaf climbs; a per-node ticket makes the second arriver union
-// both child boxes.  Each box is stored into its parent's 64-B record (side
-// 0/1) BEFORE the ticket; the ticket is an agent-scope acq_rel RMW, so the
-// second arriver's loads of the sibling box see the first arriver's stores
-// whichever CU / XCD either ran on (cdna_hip_programming.md §6 G16).
+// both child boxes.  Each box is stored into its parent's 64-B record (side 0/1)
+// BEFORE the ticket.  Cross-CU / cross-XCD visibility without a release fence per
+// step (an acq_rel RMW writes back the XCD's whole L2 each time: 43 ms at 10M):
+// the box bytes are written with agent-scope (sc1, write-through) 8-B stores, the
+// storing lane drains them (s_waitcnt vmcnt(0)) before its relaxed agent-scope
+// ticket add, and the second arriver -- told by the value its add returned --
+// reads the sibling box only with agent-scope (sc1) loads.  This is row 1 of the
+// valid hand-off forms of MI355X_MICROARCH.md §"Workgroup dispatch ... visibility".
+__device__ __forceinline__ void st_box_sc1(float* dst, f3 lo, f3 hi) {
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst);   // 8-B aligned: record offset 0 or 24
+    __hip_atomic_store(d + 0, ((uint64_t)__float_as_uint(lo.y) << 32) | __float_as_uint(lo.x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 1, ((uint64_t)__float_as_uint(hi.x) << 32) | __float_as_uint(lo.z), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 2, ((uint64_t)__float_as_uint(hi.z) << 32) | __float_as_uint(hi.y), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(src);
+    const uint64_t a = __hip_atomic_load(s + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t c = __hip_atomic_load(s + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lo = mk(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)), __uint_as_float((uint32_t)b));
+    hi = mk(__uint_as_float((uint32_t)(b >> 32)), __uint_as_float((uint32_t)c), __uint_as_float((uint32_t)(c >> 32)));
+}
+
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __restrict__ inner,
                                             const uint32_t* __restrict__ pint, uint32_t* __restrict__ cnt,
                                             float* __restrict__ rootbox) {
@@ -189,13 +244,13 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
     // tree with a parent cycle from spinning forever
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
-        float* dst = side ? inner[p].rmin : inner[p].lmin;   // min[3], max[3] contiguous
-        dst[0] = lo.x; dst[1] = lo.y; dst[2] = lo.z;
-        dst[3] = hi.x; dst[4] = hi.y; dst[5] = hi.z;
-        const uint32_t old = __hip_atomic_fetch_add(&cnt[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        st_box_sc1(side ? inner[p].rmin : inner[p].lmin, lo, hi);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the box stores before the ticket
+        const uint32_t old = __hip_atomic_fetch_add(&cnt[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == 0) return;
-        const float* sib = side ? inner[p].lmin : inner[p].rmin;
-        const f3 smin = mk(sib[0], sib[1], sib[2]), smax = mk(sib[3], sib[4], sib[5]);
+        asm volatile("" ::: "memory");
+        f3 smin, smax;
+        ld_box_sc1(side ? inner[p].lmin : inner[p].rmin, smin, smax);
         // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
         if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
         else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
@@ -279,9 +334,10 @@ inline uint32_t blocks_for(size_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK
 
 void launch_bounds(const BuildArgs& a, hipStream_t s) {
     uint32_t blocks = blocks_for(a.V);
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > BOUNDS_BLOCKS) blocks = BOUNDS_BLOCKS;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(k_bounds, dim3(blocks), dim3(BLOCK), 0, s, a.opos, a.V, a.bounds);
+    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(BLOCK), 0, s, a.bounds, blocks);
 }
 void launch_morton(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_morton, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);

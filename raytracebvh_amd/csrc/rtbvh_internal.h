@@ -16,6 +16,7 @@ constexpr uint32_t SORT_ITEMS = 16;
 constexpr uint32_t SORT_TILE = SORT_BLOCK * SORT_ITEMS;   // 4096 keys per tile
 constexpr uint32_t RADIX_BITS = 8;
 constexpr uint32_t RADIX = 1u << RADIX_BITS;
+constexpr size_t BOUNDS_WORDS = 8 + 6 * 1024;
 
 inline uint32_t sort_tiles(uint32_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
 // scratch words needed: RADIX * tiles (per-tile digit counts) + RADIX (digit totals)
@@ -37,7 +38,7 @@ struct BuildArgs {
     int morton_mode, delta_mode;
     Mat4 wvp;
     float smin[3], smax[3];   // HLSL-mode scene box
-    uint32_t* bounds;         // 6 ordered-u32 (min xyz, max xyz) for CPUTests mode
+    float* bounds;            // CPUTests mode: [0..5] scene box (min xyz, max xyz), [8..] 1024 x 6 partials
     uint32_t* keys;           // [T] Morton codes (triangle order) -> sort input
     uint32_t* vals;           // [T] triangle ids
     float4* tclip;            // [3T]
