@@ -95,7 +95,15 @@ enum {
 enum {
     RTBVH_FLAG_TIMING = 1u << 0,         /* record per-stage hipEvent times (rtbvh_get_stats) */
     RTBVH_FLAG_COUNT_VISITS = 1u << 1,   /* count traversal visits (slower; for the byte model) */
-    RTBVH_FLAG_REFRACT_RECORDS = 1u << 2 /* also build refractRay records (RayTraceLaunch.hlsl:70-80) */
+    RTBVH_FLAG_REFRACT_RECORDS = 1u << 2, /* also build refractRay records (RayTraceLaunch.hlsl:70-80) */
+    RTBVH_FLAG_SORT_BOUNCE = 1u << 3,     /* sort live bounce rays by (octant, origin Morton) before
+                                             tracing them: same results, better coherence for the
+                                             reference-order traversal */
+    RTBVH_FLAG_NEAREST_FIRST = 1u << 4,   /* visit the nearer child first and keep the lexicographic
+                                             (t, leaf) minimum: the reference DFS's answer unless
+                                             rounding breaks box/triangle containment */
+    /* bits 8..11: kernel variant for A/B measurement (0 = default, 1 = first version) */
+    RTBVH_FLAG_VARIANT_SHIFT = 8
 };
 
 typedef struct {

@@ -46,6 +46,8 @@ struct rtbvh_ctx {
     float4* d_color = nullptr;
     float* d_intensity = nullptr;
     RayQ* d_q[2] = {nullptr, nullptr};
+    uint32_t *d_bkin = nullptr, *d_bvin = nullptr, *d_bka = nullptr, *d_bva = nullptr, *d_bkb = nullptr,
+             *d_bvb = nullptr, *d_bscratch = nullptr;   // bounce coherence sort
     uint32_t* d_qcount = nullptr;             // [16]
     unsigned long long* d_counters = nullptr; // [8]
     bool traced = false;
@@ -101,7 +103,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_vb, n));
     HIPC(c, dalloc(c->d_sort_scratch, sort_scratch_words(T)));
     HIPC(c, dalloc(c->d_tclip, 3 * n));
-    HIPC(c, dalloc(c->d_leaf, 3 * n));
+    HIPC(c, dalloc(c->d_leaf, 4 * n));
     HIPC(c, dalloc(c->d_inner, ni));
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
@@ -118,6 +120,13 @@ rtbvh_status ensure_trace_capacity(rtbvh_ctx* c, size_t P) {
     HIPC(c, dalloc(c->d_intensity, P));
     HIPC(c, dalloc(c->d_q[0], P));
     HIPC(c, dalloc(c->d_q[1], P));
+    HIPC(c, dalloc(c->d_bkin, P));
+    HIPC(c, dalloc(c->d_bvin, P));
+    HIPC(c, dalloc(c->d_bka, P));
+    HIPC(c, dalloc(c->d_bva, P));
+    HIPC(c, dalloc(c->d_bkb, P));
+    HIPC(c, dalloc(c->d_bvb, P));
+    HIPC(c, dalloc(c->d_bscratch, sort_scratch_words((uint32_t)P)));
     if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 16));
     if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 16));
     c->cap_P = P;
@@ -154,6 +163,7 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     TraceArgs a{};
     a.inner = c->d_inner;
     a.leaf = c->d_leaf;
+    a.tclip = c->d_tclip;
     a.verts = c->d_verts;
     a.idx = c->d_idx;
     a.matidx = c->d_matidx;
@@ -191,11 +201,23 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     HIPC(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
-    launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, s);
+    // kernel variant: 0 reference order, 1 nearest-first, 2 first version (A/B)
+    int variant = (c->cfg.flags & RTBVH_FLAG_NEAREST_FIRST) ? 1 : 0;
+    if (((c->cfg.flags >> RTBVH_FLAG_VARIANT_SHIFT) & 15u) == 1) variant = 2;
+    const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
+    const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
+    launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, variant, s);
     if (timing) HIPC(c, hipEventRecord(ev[1], s));
-    for (uint32_t b = 0; b < bounces; b++)
-        launch_bounce(a, c->d_q[b & 1], &c->d_qcount[b], c->d_q[(b + 1) & 1], &c->d_qcount[b + 1], count,
-                      b + 1 < bounces, s);
+    for (uint32_t b = 0; b < bounces; b++) {
+        const uint32_t* perm = nullptr;
+        if (sort) {
+            launch_bounce_keys(c->d_q[b & 1], &c->d_qcount[b], c->d_rootbox, P, c->d_bkin, c->d_bvin, s);
+            perm = radix_sort_pairs(c->d_bkin, c->d_bvin, c->d_bka, c->d_bva, c->d_bkb, c->d_bvb, P, 30,
+                                    c->d_bscratch, s).vals;
+        }
+        launch_bounce(a, c->d_q[b & 1], &c->d_qcount[b], perm, c->d_q[(b + 1) & 1], &c->d_qcount[b + 1], count,
+                      b + 1 < bounces, variant, s);
+    }
     if (timing) {
         HIPC(c, hipEventRecord(ev[2], s));
         c->n_traces++;
@@ -282,6 +304,8 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount);
+    dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
+    dfree(c->d_bscratch);
     dfree(c->d_counters);
     for (auto& row : c->evb)
         for (auto& e : row)

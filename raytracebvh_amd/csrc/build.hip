@@ -190,13 +190,22 @@ template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= a.T) return;
-    // leaf record: gather the clip-space triangle of sorted position i
+    // leaf record of sorted position i: gather the clip-space triangle once, store
+    // (v0, e1, e2) for the triangle test (the reference's edge1/edge2, :43-44) and
+    // the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
     const uint32_t t = a.sorted_vals[i];
     const float4* src = a.tclip + 3 * (size_t)t;
-    float4* dst = a.leaf + 3 * (size_t)i;
-    dst[0] = src[0];
-    dst[1] = src[1];
-    dst[2] = src[2];
+    const float4 s0 = src[0], s1 = src[1], s2 = src[2];
+    const f3 v0 = mk(s0.x, s0.y, s0.z), v1 = mk(s1.x, s1.y, s1.z), v2 = mk(s2.x, s2.y, s2.z);
+    const f3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+    f3 lo = vmin(v0, v1), hi = vmax(v0, v1);
+    lo = vmin(lo, v2);
+    hi = vmax(hi, v2);
+    float4* dst = a.leaf + 4 * (size_t)i;
+    dst[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
+    dst[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+    dst[2] = make_float4(e2.z, __uint_as_float(t), lo.x, lo.y);
+    dst[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
     if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.inner, a.pleaf, a.pint);
     if (i == 0 && a.T > 1) a.pint[0] = INVALID;   // root (BVHConstructP1.hlsl:186-187)
 }
@@ -266,11 +275,9 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
 __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= a.T) return;
-    const float4* r = a.leaf + 3 * (size_t)i;
-    const float4 v0 = r[0], v1 = r[1], v2 = r[2];
-    f3 lo = mk(v0.x, v0.y, v0.z), hi = lo;   // MortonCodes.hlsl:87-96
-    lo = vmin(lo, mk(v1.x, v1.y, v1.z)); hi = vmax(hi, mk(v1.x, v1.y, v1.z));
-    lo = vmin(lo, mk(v2.x, v2.y, v2.z)); hi = vmax(hi, mk(v2.x, v2.y, v2.z));
+    const float4* r = a.leaf + 4 * (size_t)i;
+    const float4 b0 = r[2], b1 = r[3];
+    const f3 lo = mk(b0.z, b0.w, b1.x), hi = mk(b1.y, b1.z, b1.w);
     if (a.T == 1) {
         a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
         a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
@@ -307,7 +314,7 @@ __global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restri
         o.child_l = INVALID;
         o.child_r = INVALID;
         o.code = a.sorted_keys[r];
-        o.index = a.leaf ? 3u * __float_as_uint(a.leaf[3 * (size_t)r].w) : 0u;
+        o.index = a.leaf ? 3u * __float_as_uint(a.leaf[4 * (size_t)r + 2].y) : 0u;
     } else {
         const uint32_t k = r - T;
         e = a.pint[k];

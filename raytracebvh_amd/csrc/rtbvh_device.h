@@ -5,7 +5,8 @@
 //   opos   float4[V]     object-space vertex positions (w unused), set_scene
 //   tclip  float4[3*T]   per-triangle clip-space vertices, TRIANGLE order (Morton kernel)
 //   keys/vals u32[T] x2  radix ping-pong (Morton code, triangle id)
-//   leaf   float4[3*T]   leaf records in SORTED order: {v0.xyz, tri}, {v1.xyz, 0}, {v2.xyz, 0}
+//   leaf   float4[4*T]   64-B leaf records in SORTED order: {v0.xyz, e1.x}, {e1.yz, e2.xy},
+//                        {e2.z, tri, bmin.xy}, {bmin.z, bmax.xyz}; e1 = v1-v0, e2 = v2-v0
 //   inner  Inner[T-1]    64-B child-pair records; internal node k, root = 0
 //   pleaf  u32[T], pint u32[T-1]   parent<<1 | side (side 0 = left child)
 // Node ids inside kernels: internal k -> k, leaf j -> LEAF_BIT | j.
@@ -77,15 +78,6 @@ __device__ __forceinline__ f3 xform_normal(const float* M, f3 n) {
     r.y = (n.x * M[1] + n.y * M[5]) + n.z * M[9];
     r.z = (n.x * M[2] + n.y * M[6]) + n.z * M[10];
     return r;
-}
-
-// order-preserving float <-> u32 (for atomic min/max of the scene box)
-__device__ __forceinline__ uint32_t f2ord(float f) {
-    uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float ord2f(uint32_t u) {
-    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
 
 }  // namespace rtbvh

@@ -44,7 +44,7 @@ struct BuildArgs {
     float4* tclip;            // [3T]
     const uint32_t* sorted_keys;  // [T]
     const uint32_t* sorted_vals;  // [T]
-    float4* leaf;             // [3T]
+    float4* leaf;             // [4T] 64-B sorted leaf records
     Inner* inner;             // [T-1]
     uint32_t* pleaf;          // [T]
     uint32_t* pint;           // [T-1]
@@ -63,7 +63,8 @@ void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t 
 // ---- trace (trace.hip) ------------------------------------------------------
 struct TraceArgs {
     const Inner* inner;
-    const float4* leaf;
+    const float4* leaf;       // [4T] sorted leaf records (see build.hip)
+    const float4* tclip;      // [3T] clip-space triangles in triangle order (hit shading)
     const float* verts;       // rtbvh_vertex AoS, 8 floats each
     const uint32_t* idx;
     const uint32_t* matidx;
@@ -76,8 +77,13 @@ struct TraceArgs {
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
 };
-void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, hipStream_t s);
-void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, RayQ* qout, uint32_t* qout_count,
-                   bool count, bool emit, hipStream_t s);
+// traversal kernel variants (A/B switch; DESIGN.md "Traversal")
+// variant: see RTBVH_FLAG_VARIANT_SHIFT in include/rtbvh.h (0 = default)
+void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, int variant, hipStream_t s);
+void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
+                   uint32_t* qout_count, bool count, bool emit, int variant, hipStream_t s);
+// coherence sort keys of a bounce queue: P entries (past *count: key 0xFFFFFFFF)
+void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, uint32_t P, uint32_t* keys,
+                        uint32_t* vals, hipStream_t s);
 
 }  // namespace rtbvh

@@ -5,11 +5,21 @@
 // rays with intensity 0) on top of findCollision (RayTraceTraversal.hlsl:106-193).
 // Here: a wave64 traces one 8x8 pixel tile (a 256-thread workgroup = 4 tiles
 // side by side in one 8-row band, which is also the multi-GPU sharding unit);
-// every child-pair test reads ONE 64-B node record; leaves read a 48-B
-// pre-transformed triangle (getUpdateVerts hoisted to the build); the bounce
-// pass runs only over a wave-compacted queue of live rays (ballot + one atomic
-// per wave).  Traversal order, pruning and tie rules are the reference's
-// exactly, so results match the CPU oracle bit for bit.
+// every child-pair test reads ONE 64-B node record; leaves read a 64-B record
+// holding the clip-space triangle as (v0, e1 = v1-v0, e2 = v2-v0) -- the same
+// floats the reference computes per test -- so getUpdateVerts and the edge
+// subtractions are hoisted to the build; the bounce pass runs only over a
+// wave-compacted queue of live rays (ballot + one atomic per wave).
+//
+// Traversal orders (DESIGN.md "Traversal"):
+//  * reference order (default): the left-first DFS of findCollision exactly,
+//    same pruning, strict `<` replacement -> bit-identical to the CPU oracle;
+//  * nearest-first (RTBVH_FLAG_NEAREST_FIRST): the nearer child first, with the
+//    lexicographic (t, leaf index) minimum kept, which is what the left-first DFS
+//    returns whenever box/triangle rounding is consistent.
+// A/B-measured alternatives that lost (LDS stacks, while-while loops, leaf
+// batching) are recorded in DESIGN.md; the kept loop is a do-while over a
+// scratch stack whose top lives in a register.
 #include "rtbvh_internal.h"
 
 namespace rtbvh {
@@ -20,9 +30,9 @@ constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
 
 struct Counts { uint32_t internal, leaf, overflow; };
 
-// rayTriangleCollision, RayTraceTraversal.hlsl:41-86
-__device__ __forceinline__ float ray_triangle(f3 o, f3 d, f3 p0, f3 p1, f3 p2) {
-    const f3 e1 = sub(p1, p0), e2 = sub(p2, p0);
+// rayTriangleCollision, RayTraceTraversal.hlsl:41-86, with edge1/edge2 precomputed
+// by the build (identical floats: the same single subtraction)
+__device__ __forceinline__ float ray_triangle(f3 o, f3 d, f3 p0, f3 e1, f3 e2) {
     f3 tmp = cross(d, e2);
     const float dx = dot(e1, tmp);
     if (fabsf(dx) < EPSILON) return -1.f;
@@ -38,20 +48,86 @@ __device__ __forceinline__ float ray_triangle(f3 o, f3 d, f3 p0, f3 p1, f3 p2) {
     return -1.f;
 }
 
-// rayBoxCollision, RayTraceTraversal.hlsl:92-104 (fminf/fmaxf drop NaN like HLSL min/max)
+// rayBoxCollision, RayTraceTraversal.hlsl:92-104 (fminf/fmaxf drop NaN like HLSL
+// min/max).  Also returns the entry distance, used by the nearest-first order.
 __device__ __forceinline__ bool ray_box(f3 o, f3 inv, float bx0, float by0, float bz0, float bx1, float by1, float bz1,
-                                        bool hit, float best) {
+                                        bool hit, float best, float& tmin) {
     const float tx0 = (bx0 - o.x) * inv.x, ty0 = (by0 - o.y) * inv.y, tz0 = (bz0 - o.z) * inv.z;
     const float tx1 = (bx1 - o.x) * inv.x, ty1 = (by1 - o.y) * inv.y, tz1 = (bz1 - o.z) * inv.z;
     const float mn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
     const float mx = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    tmin = mn;
     return 0 <= mx && mn <= mx && (!hit || mn <= best);
 }
 
-// findCollision, RayTraceTraversal.hlsl:106-193.  Returns hit; best_leaf = sorted leaf index.
-template <bool COUNT>
+// findCollision, RayTraceTraversal.hlsl:106-193.  The reference keeps stack[0] = -1
+// and loops `do { ... } while (stackIndex != -1)`; here the entry at the top of
+// the stack is cached in a register (`top`), so a pop hands over the next node at
+// once and refills `top` from scratch in the background.  Returns hit;
+// best_leaf = sorted leaf index.
+template <bool COUNT, bool NEAREST>
 __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const float4* __restrict__ leaf, uint32_t T,
                                          f3 o, f3 d, f3 inv, float& best, uint32_t& best_leaf, Counts& c) {
+    bool hit = false;
+    best = 0.f;
+    best_leaf = 0;
+    uint32_t stack[STACK_SIZE];   // reference entries [0, sp) below the cached top
+    int sp = 0;                   // reference stack index; stack[0] is the sentinel = top at start
+    uint32_t top = INVALID;
+    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    uint32_t guard = 2 * T + 2;   // a valid tree is walked in <= 2T-1 steps
+    do {
+        if (--guard == 0) { c.overflow++; break; }
+        if (node & LEAF_BIT) {
+            const uint32_t j = node & ~LEAF_BIT;
+            const float4* r = leaf + 4 * (size_t)j;
+            const float4 a = r[0], b = r[1];
+            const float e2z = r[2].x;
+            if (COUNT) c.leaf++;
+            const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
+            if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < best_leaf))) {
+                best = t;
+                best_leaf = j;
+                hit = true;
+            }
+            node = top;                                 // pop
+            if (--sp >= 0) top = stack[sp];
+            continue;
+        }
+        if (COUNT) c.internal++;
+        const float4* r = reinterpret_cast<const float4*>(inner + node);
+        const float4 q0 = r[0], q1 = r[1], q2 = r[2];
+        const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
+        float tl, tr;
+        const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
+        const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
+        if (!lh && !rh) {
+            node = top;                                 // pop
+            if (--sp >= 0) top = stack[sp];
+        } else {
+            const bool swap = NEAREST && lh && rh && tr < tl;
+            if (lh && rh) {
+                if (sp + 1 >= STACK_SIZE) {
+                    c.overflow++;
+                    node = top;
+                    if (--sp >= 0) top = stack[sp];
+                    continue;
+                }
+                stack[sp++] = top;                      // push the second child
+                top = swap ? q3.x : q3.y;
+            }
+            node = swap ? q3.y : (lh ? q3.x : q3.y);
+        }
+    } while (sp != -1);
+    return hit;
+}
+
+// The first version of the loop (reference order, whole stack in scratch, no top
+// cache, default occupancy), kept as an A/B variant.
+template <bool COUNT>
+__device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
+                                                       uint32_t T, f3 o, f3 d, f3 inv, float& best, uint32_t& best_leaf,
+                                                       Counts& c) {
     bool hit = false;
     best = 0.f;
     best_leaf = 0;
@@ -59,15 +135,16 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
     int sp = 0;
     stack[0] = INVALID;
     uint32_t node = (T == 1) ? LEAF_BIT : 0u;
-    uint32_t guard = 2 * T + 2;   // a valid tree is walked in <= 2T-1 steps
+    uint32_t guard = 2 * T + 2;
     do {
         if (--guard == 0) { c.overflow++; break; }
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
-            const float4* r = leaf + 3 * (size_t)j;
-            const float4 a = r[0], b = r[1], q = r[2];
+            const float4* r = leaf + 4 * (size_t)j;
+            const float4 a = r[0], b = r[1];
+            const float e2z = r[2].x;
             if (COUNT) c.leaf++;
-            const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(q.x, q.y, q.z));
+            const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
             if (t != -1.f && (!hit || t < best)) {
                 best = t;
                 best_leaf = j;
@@ -80,8 +157,9 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
         const float4* r = reinterpret_cast<const float4*>(inner + node);
         const float4 q0 = r[0], q1 = r[1], q2 = r[2];
         const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
-        const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best);
-        const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best);
+        float tl, tr;
+        const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
+        const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
         if (!lh && !rh) {
             node = stack[sp--];
         } else {
@@ -95,6 +173,20 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
     return hit;
 }
 
+// kernel variants: 0 = reference order (default), 1 = nearest-first,
+// 2 = the first version (reference order) kept for A/B
+template <int V> struct TV {
+    static constexpr bool NEAREST = (V == 1);
+    static constexpr int OCC = (V == 2) ? 1 : 8;   // 8 waves/SIMD => <= 64 VGPRs (A/B: -25% bounce time)
+};
+
+template <bool COUNT, int V>
+__device__ __forceinline__ bool trace_ray(const Inner* __restrict__ inner, const float4* __restrict__ leaf, uint32_t T,
+                                          f3 o, f3 d, f3 inv, float& best, uint32_t& best_leaf, Counts& c) {
+    if (V == 2) return traverse_first_version<COUNT>(inner, leaf, T, o, d, inv, best, best_leaf, c);
+    return traverse<COUNT, TV<V>::NEAREST>(inner, leaf, T, o, d, inv, best, best_leaf, c);
+}
+
 struct HitInfo {
     float4 color;   // renderPixel(...) * specular
     f3 hitp, nrm;
@@ -103,12 +195,14 @@ struct HitInfo {
 };
 
 // getHitLoc (:15-19) + getNromalTexCoord (RayTraceHelper.hlsl:12-35) + renderPixel*specular
-// (RayTraceRender.hlsl:16-29, RayTraceLaunch.hlsl:57-59).  Texture sampling: white.
+// (RayTraceRender.hlsl:16-29, RayTraceLaunch.hlsl:57-59) for the hit triangle only
+// (the reference transforms all three vertices at every leaf it visits).
+// Texture sampling: white.
 __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_leaf, f3 o, f3 d, float t) {
     HitInfo h;
-    const float4* r = a.leaf + 3 * (size_t)best_leaf;
-    const float4 a0 = r[0], a1 = r[1], a2 = r[2];
-    const uint32_t tri = __float_as_uint(a0.w);
+    const uint32_t tri = __float_as_uint(a.leaf[4 * (size_t)best_leaf + 2].y);
+    const float4* P = a.tclip + 3 * (size_t)tri;
+    const float4 a0 = P[0], a1 = P[1], a2 = P[2];
     const f3 P0 = mk(a0.x, a0.y, a0.z), P1 = mk(a1.x, a1.y, a1.z), P2 = mk(a2.x, a2.y, a2.z);
     f3 n[3];
     float uv[3][2];
@@ -178,8 +272,9 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
 }
 
 // RayTraceLaunch.hlsl:6-93
-template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void k_primary(TraceArgs a, RayQ* __restrict__ q, uint32_t* __restrict__ qcount, int emit) {
+template <bool COUNT, int V>
+__global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ* __restrict__ q,
+                                                               uint32_t* __restrict__ qcount, int emit) {
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t band = blockIdx.y * a.nranks + a.rank;
@@ -199,7 +294,7 @@ __global__ __launch_bounds__(BLOCK) void k_primary(TraceArgs a, RayQ* __restrict
         uint32_t bl;
         float4 color;
         float intensity = 0.f;
-        if (traverse<COUNT>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
+        if (trace_ray<COUNT, V>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
             hits = 1;
             const HitInfo h = shade_hit(a, bl, o, d, best);
             tex = h.textured;
@@ -225,10 +320,13 @@ __global__ __launch_bounds__(BLOCK) void k_primary(TraceArgs a, RayQ* __restrict
     flush_counts<COUNT>(a, c, hits, tex, 2);
 }
 
-// RayTraceReflection.hlsl:6-62 over the compacted queue of live rays
-template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void k_bounce(TraceArgs a, const RayQ* __restrict__ qin, const uint32_t* __restrict__ qin_count,
-                                                  RayQ* __restrict__ qout, uint32_t* __restrict__ qout_count, int emit) {
+// RayTraceReflection.hlsl:6-62 over the compacted queue of live rays (in `perm`
+// order when the queue was sorted for coherence)
+template <bool COUNT, int V>
+__global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_bounce(TraceArgs a, const RayQ* __restrict__ qin,
+                                                              const uint32_t* __restrict__ qin_count,
+                                                              const uint32_t* __restrict__ perm, RayQ* __restrict__ qout,
+                                                              uint32_t* __restrict__ qout_count, int emit) {
     const uint32_t n = *qin_count;
     Counts c = {0, 0, 0};
     uint32_t hits = 0, tex = 0;
@@ -237,14 +335,14 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(TraceArgs a, const RayQ* __res
         bool live = false;
         RayQ e;
         if (i < n) {
-            e = qin[i];
+            e = qin[perm ? perm[i] : i];
             const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
             const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
             float best;
             uint32_t bl;
             float4 col = a.color[e.idx];
             float intensity = e.intensity;
-            if (traverse<COUNT>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
+            if (trace_ray<COUNT, V>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
                 hits++;
                 const HitInfo h = shade_hit(a, bl, o, d, best);
                 tex += h.textured;
@@ -271,22 +369,81 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(TraceArgs a, const RayQ* __res
     flush_counts<COUNT>(a, c, hits, tex, 5);
 }
 
+// bounce-ray coherence sort key (results do not depend on the order): direction
+// octant in bits 27..29, 9-bit-per-axis Morton code of the origin inside the scene
+// box in bits 0..26 (A/B vs direction-only / origin-only / mixed keys: DESIGN.md).
+// Entries past the live count get the largest key and sort last.
+__device__ __forceinline__ uint32_t spread9(uint32_t v) {
+    v &= 0x1FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t q9(float x, float lo, float hi) {
+    float t = (x - lo) / (hi - lo) * 512.f;
+    t = fminf(fmaxf(t, 0.f), 511.f);
+    return (uint32_t)t;
+}
+__global__ __launch_bounds__(BLOCK) void k_bounce_keys(const RayQ* __restrict__ q, const uint32_t* __restrict__ count,
+                                                       const float* __restrict__ box, uint32_t P,
+                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= P) return;
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < *count) {
+        const RayQ e = q[i];
+        const uint32_t oct = (e.dx < 0.f) | ((e.dy < 0.f) << 1) | ((e.dz < 0.f) << 2);
+        const uint32_t m = spread9(q9(e.ox, box[0], box[3])) << 2 | spread9(q9(e.oy, box[1], box[4])) << 1 |
+                           spread9(q9(e.oz, box[2], box[5]));
+        key = oct << 27 | m;
+    }
+    keys[i] = key;
+    vals[i] = i;
+}
+
+template <bool COUNT, int V>
+void launch_primary_t(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool emit, dim3 grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_primary<COUNT, V>), grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
+}
+template <bool COUNT, int V>
+void launch_bounce_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
+                     uint32_t* qout_count, bool emit, hipStream_t s) {
+    const uint32_t blocks = 2048;   // 8 waves/SIMD x 1024 SIMDs / 4 waves per block; grid-stride over the queue
+    hipLaunchKernelGGL((k_bounce<COUNT, V>), dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, perm, qout,
+                       qout_count, (int)emit);
+}
+
 }  // namespace
 
-void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, hipStream_t s) {
+#define RTBVH_VARIANTS(M)                                 \
+    switch (variant) {                                    \
+        case 1: count ? M(true, 1) : M(false, 1); break;  \
+        case 2: count ? M(true, 2) : M(false, 2); break;  \
+        default: count ? M(true, 0) : M(false, 0); break; \
+    }
+
+void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, int variant, hipStream_t s) {
     const uint32_t nbands = (a.H + 7) / 8;
     const uint32_t my_bands = a.rank < nbands ? (nbands - a.rank + a.nranks - 1) / a.nranks : 0;
     if (my_bands == 0 || a.W == 0) return;
     dim3 grid((a.W + 31) / 32, my_bands);
-    if (count) hipLaunchKernelGGL(k_primary<true>, grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
-    else hipLaunchKernelGGL(k_primary<false>, grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
+#define RTBVH_PRIM(C, V) launch_primary_t<C, V>(a, q, qcount, emit, grid, s)
+    RTBVH_VARIANTS(RTBVH_PRIM)
+#undef RTBVH_PRIM
 }
 
-void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, RayQ* qout, uint32_t* qout_count,
-                   bool count, bool emit, hipStream_t s) {
-    const uint32_t blocks = 2048;   // grid-stride over the device-side queue length
-    if (count) hipLaunchKernelGGL(k_bounce<true>, dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, qout, qout_count, (int)emit);
-    else hipLaunchKernelGGL(k_bounce<false>, dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, qout, qout_count, (int)emit);
+void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
+                   uint32_t* qout_count, bool count, bool emit, int variant, hipStream_t s) {
+#define RTBVH_BNC(C, V) launch_bounce_t<C, V>(a, qin, qin_count, perm, qout, qout_count, emit, s)
+    RTBVH_VARIANTS(RTBVH_BNC)
+#undef RTBVH_BNC
+}
+
+void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, uint32_t P, uint32_t* keys,
+                        uint32_t* vals, hipStream_t s) {
+    hipLaunchKernelGGL(k_bounce_keys, dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, q, count, box, P, keys, vals);
 }
 
 }  // namespace rtbvh

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""A/B the traversal kernel variants on the C5 frame in ONE process (interleaved
+rounds, cdna_hip_programming.md §5.4 rule 24).  Every variant's framebuffer must
+equal the baseline's bit for bit.  Prints one JSON line per variant."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import raytracebvh_amd as rt  # noqa: E402
+
+
+def main():
+    ntris = int(os.environ.get("AB_TRIS", "10000000"))
+    W, H = int(os.environ.get("AB_W", "3840")), int(os.environ.get("AB_H", "2160"))
+    rounds = int(os.environ.get("AB_ROUNDS", "5"))
+    variants = [("reference", 0), ("reference+sort", rt.FLAG_SORT_BOUNCE), ("nearest", rt.FLAG_NEAREST_FIRST),
+                ("nearest+sort", rt.FLAG_NEAREST_FIRST | rt.FLAG_SORT_BOUNCE), ("first_version", 1 << rt.FLAG_VARIANT_SHIFT)]
+    scene = rt.synthetic(ntris, seed=0x5EED0005, half_extent=(100, 100, 50))
+    ctx = rt.Context(device=0, flags=rt.FLAG_TIMING)
+    ctx.set_scene(scene)
+    ctx.set_camera(*rt.camera_reference(W, H))
+    ctx.build()
+    ref = None
+    res = {v: [] for v in variants}
+    for r in range(rounds):
+        for v, srt in variants:
+            flags = rt.FLAG_TIMING | srt
+            ctx.set_flags(flags)
+            ctx.trace(W, H, 1)   # warm
+            ctx.reset_stats()
+            for _ in range(3):
+                ctx.trace(W, H, 1, sync=False)
+            st = ctx.stats()
+            res[(v, srt)].append((st["ms_stage"][5], st["ms_stage"][6], st["ms_trace"]))
+            if r == 0:
+                fb = ctx.read_framebuffer()
+                if ref is None:
+                    ref = fb
+                ndiff = int((fb != ref).any(axis=-1).sum())
+                print(json.dumps({"variant": v, "pixels_differing_from_first": ndiff}), flush=True)
+    for (v, srt), xs in res.items():
+        a = np.array(xs)
+        print(json.dumps({"variant": v, "primary_ms_med": float(np.median(a[:, 0])),
+                          "bounce_ms_med": float(np.median(a[:, 1])), "trace_ms_med": float(np.median(a[:, 2])),
+                          "trace_ms_min": float(a[:, 2].min())}))
+
+
+if __name__ == "__main__":
+    main()
