@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--build-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C4 build / C3 side measurements")
+    ap.add_argument("--traversal", default="auto", choices=["auto", "reference"],
+                    help="auto: report nearest-first when its frame is identical to the reference order's")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -162,60 +164,60 @@ def main():
              "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
                                    [round(x, 4) for x in bst["ms_stage"][:5]]))}
 
-    # ---- band buffers + gather plumbing
-    L = rt.lib()
-    rows = [L.rtbvh_band_rows(H, r, world) for r in range(world)]
-    max_rows = max(rows)
-    band = torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev)
-    frame = band if world == 1 else None
-    gather_list, row_idx = None, None
-    if world > 1 and rank == 0:
-        frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-        gather_list = [torch.empty_like(band) for _ in range(world)]
-        row_idx = []
-        for r in range(world):
-            ys = [y for b in range(r, (H + 7) // 8, world) for y in range(8 * b, min(8 * b + 8, H))]
-            row_idx.append(torch.tensor(ys, dtype=torch.long, device=dev))
+    # ---- band buffers + RCCL gather plumbing (raytracebvh_amd/tiles.py)
+    from raytracebvh_amd.tiles import BandGather
+    g = BandGather(W, H, rank, world, device=dev)
+    band = g.band
 
     def step():
         ctx.trace_band_async(W, H, bounces, rank, world, band.data_ptr())
+        g.gather()
+
+    def timed(flags):
+        """Warm up, then time exactly args.steps steps between barrier + synchronize."""
+        ctx.set_flags(rt.FLAG_TIMING | flags)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        st = ctx.stats()
+        tot = torch.tensor([st["primary_rays"] + st["bounce_rays"]], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.gather(band, gather_list if rank == 0 else None, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    frame.index_copy_(0, row_idx[r], gather_list[r][: rows[r]])
+            dist.all_reduce(tot)
+        ctx.reset_stats()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        ms = float(el.item()) / args.steps * 1e3
+        rays = float(tot[0].item())
+        return dict(ms_step=ms, rays=rays, value=rays / (ms * 1e-3) / 1e6, stats=ctx.stats(),
+                    band=band.clone())
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    st = ctx.stats()
-    rays_local = st["primary_rays"] + st["bounce_rays"]
-    live_local = st["bounce_rays"]
-    tot = torch.tensor([rays_local, live_local], dtype=torch.float64, device=dev)
+    # reference order (the exact findCollision DFS) and nearest-first; the nearest-first
+    # number is the headline only if its frame is bit-identical to the reference-order
+    # frame of this same run (checked on every rank's bands)
+    ref = timed(rt.FLAG_SORT_BOUNCE)
+    near = timed(rt.FLAG_NEAREST_FIRST)
+    same = torch.tensor([0.0 if torch.equal(ref["band"], near["band"]) else 1.0], device=dev)
     if world > 1:
-        dist.all_reduce(tot)
-    rays_per_step = float(tot[0].item())
-
-    # ---- timed region
-    ctx.reset_stats()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    tst = ctx.stats()   # hipEvent averages of the primary / bounce kernels over the timed steps
-    ms_step = elapsed / args.steps * 1e3
-    value = rays_per_step / (ms_step * 1e-3) / 1e6
+        dist.all_reduce(same)
+    identical = float(same.item()) == 0.0
+    use = near if (identical and args.traversal != "reference") else ref
+    mode_flags = rt.FLAG_NEAREST_FIRST if use is near else rt.FLAG_SORT_BOUNCE
+    rays_per_step, ms_step, value, tst = use["rays"], use["ms_step"], use["value"], use["stats"]
+    traversal = {"mode": "nearest-first" if use is near else "reference-order",
+                 "frames_identical": identical,
+                 "reference_order_mrays_s": round(ref["value"], 2), "reference_order_ms": round(ref["ms_step"], 4),
+                 "nearest_first_mrays_s": round(near["value"], 2), "nearest_first_ms": round(near["ms_step"], 4)}
 
     # ---- visit counts for the byte model (one extra, untimed trace of this rank's bands)
-    ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_COUNT_VISITS)
+    ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_COUNT_VISITS | mode_flags)
     ctx.reset_stats()
     ctx.trace_band_async(W, H, bounces, rank, world, band.data_ptr())
     cst = ctx.stats()
@@ -288,6 +290,7 @@ def main():
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kern.items()},
             "visits": {"internal": cst["internal_visits"], "leaf": cst["leaf_visits"], "hits": cst["hits"]},
+            "traversal": traversal,
             "build": build,
             "cpu_baseline": cpu,
         }

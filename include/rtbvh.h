@@ -102,6 +102,9 @@ enum {
     RTBVH_FLAG_NEAREST_FIRST = 1u << 4,   /* visit the nearer child first and keep the lexicographic
                                              (t, leaf) minimum: the reference DFS's answer unless
                                              rounding breaks box/triangle containment */
+    RTBVH_FLAG_PACKET_PRIMARY = 1u << 5,  /* primary rays: one wave walks its 8x8 tile's rays as a
+                                             masked packet with scalar node fetches (same per-ray
+                                             visit sequence, same results) */
     /* bits 8..11: kernel variant for A/B measurement (0 = default, 1 = first version) */
     RTBVH_FLAG_VARIANT_SHIFT = 8
 };

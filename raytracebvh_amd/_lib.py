@@ -17,6 +17,7 @@ OK, ERR_INVALID_ARG, ERR_HIP, ERR_OOM, ERR_NOT_READY, ERR_STACK_OVERFLOW, ERR_IO
 MORTON_CPUTESTS, MORTON_HLSL = 0, 1
 DELTA_CLZ64, DELTA_CPUTESTS = 0, 1
 FLAG_TIMING, FLAG_COUNT_VISITS, FLAG_REFRACT_RECORDS, FLAG_SORT_BOUNCE, FLAG_NEAREST_FIRST = 1, 2, 4, 8, 16
+FLAG_PACKET_PRIMARY = 1 << 5
 FLAG_VARIANT_SHIFT = 8
 
 # every symbol include/rtbvh.h declares (tests check the library exports them all)

@@ -203,10 +203,13 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     // kernel variant: 0 reference order, 1 nearest-first, 2 first version (A/B)
     int variant = (c->cfg.flags & RTBVH_FLAG_NEAREST_FIRST) ? 1 : 0;
-    if (((c->cfg.flags >> RTBVH_FLAG_VARIANT_SHIFT) & 15u) == 1) variant = 2;
+    const uint32_t vsel = (c->cfg.flags >> RTBVH_FLAG_VARIANT_SHIFT) & 15u;
+    if (vsel == 1) variant = 2;
+    int pvariant = variant;   // primary kernel: 2 = wave packets
+    if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel == 0) pvariant = variant == 1 ? 4 : 3;
     const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
-    launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, variant, s);
+    launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, pvariant, s);
     if (timing) HIPC(c, hipEventRecord(ev[1], s));
     for (uint32_t b = 0; b < bounces; b++) {
         const uint32_t* perm = nullptr;

@@ -173,10 +173,113 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
     return hit;
 }
 
+// ---- wave-packet traversal (primary rays) -------------------------------------
+// The 64 rays of an 8x8 pixel tile are nearly parallel neighbours, so a wave walks
+// ONE node at a time with a per-node lane mask: the node record is fetched by the
+// scalar unit (s_load through the constant address space: no vector-memory/TA
+// work, which PMC showed saturated), each masked lane tests the child boxes with
+// its own (hit, best), and the children are visited with the ballots of the lanes
+// that hit them.  In reference order every lane sees exactly its own findCollision
+// sequence (the nodes it visits are a subsequence of the wave's walk, in the same
+// order, and nothing changes its state in between), so results and per-lane visit
+// counts are identical to the per-lane DFS.  In nearest-first mode the wave takes
+// the child most of its lanes see first.
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef const v4f __attribute__((address_space(4))) cv4f;
+
+__device__ __forceinline__ float4 sload(const float4* p) {
+    const v4f v = *(cv4f*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+template <bool COUNT, bool NEAREST>
+__device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
+                                                uint32_t T, f3 o, f3 d, f3 inv, bool valid, float& best,
+                                                uint32_t& best_leaf, Counts& c, uint32_t* s_st /* per wave [3*STACK_SIZE] */) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lanebit = 1ull << lane;
+    bool hit = false;
+    best = 0.f;
+    best_leaf = 0;
+    uint64_t mask = __ballot(valid);
+    int sp = 0;
+    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    if (mask == 0) return false;
+    uint32_t guard = 2 * T + 2;
+    while (true) {
+        if (--guard == 0) { c.overflow++; break; }
+        bool pop = false;
+        if (node & LEAF_BIT) {
+            const uint32_t j = node & ~LEAF_BIT;
+            const float4 a = sload(leaf + 4 * (size_t)j), b = sload(leaf + 4 * (size_t)j + 1);
+            const float e2z = sload(leaf + 4 * (size_t)j + 2).x;
+            if (mask & lanebit) {
+                if (COUNT) c.leaf++;
+                const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
+                if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < best_leaf))) {
+                    best = t;
+                    best_leaf = j;
+                    hit = true;
+                }
+            }
+            pop = true;
+        } else {
+            const float4* r = reinterpret_cast<const float4*>(inner + node);
+            const float4 q0 = sload(r), q1 = sload(r + 1), q2 = sload(r + 2), q3f = sload(r + 3);
+            const uint32_t cl = __float_as_uint(q3f.x), cr = __float_as_uint(q3f.y);
+            bool lh = false, rh = false;
+            float tl = 0.f, tr = 0.f;
+            if (mask & lanebit) {
+                if (COUNT) c.internal++;
+                lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
+                rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
+            }
+            const uint64_t ml = __ballot(lh), mr = __ballot(rh);
+            if ((ml | mr) == 0) {
+                pop = true;
+            } else if (ml && mr) {
+                bool swap = false;
+                if (NEAREST) {
+                    const uint64_t both = __ballot(lh && rh);
+                    const uint64_t rfirst = __ballot(lh && rh && tr < tl);
+                    swap = 2 * __popcll(rfirst) > __popcll(both);
+                }
+                if (sp + 1 >= STACK_SIZE) { c.overflow++; pop = true; }
+                else {
+                    ++sp;
+                    if (lane == 0) {   // push the second child and its lanes
+                        const uint64_t m2 = swap ? ml : mr;
+                        s_st[3 * sp] = swap ? cl : cr;
+                        s_st[3 * sp + 1] = (uint32_t)m2;
+                        s_st[3 * sp + 2] = (uint32_t)(m2 >> 32);
+                    }
+                    node = swap ? cr : cl;
+                    mask = swap ? mr : ml;
+                }
+            } else {
+                node = ml ? cl : cr;
+                mask = ml ? ml : mr;
+            }
+        }
+        if (pop) {
+            if (sp == 0) break;
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the lane-0 push has landed in LDS
+            node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
+            mask = ((uint64_t)hi << 32) | lo;
+            --sp;
+        }
+    }
+    return hit;
+}
+
 // kernel variants: 0 = reference order (default), 1 = nearest-first,
 // 2 = the first version (reference order) kept for A/B
+// 3 = reference order with wave-packet primary rays, 4 = nearest-first with packets
 template <int V> struct TV {
-    static constexpr bool NEAREST = (V == 1);
+    static constexpr bool NEAREST = (V == 1 || V == 4);
+    static constexpr bool PACKET = (V == 3 || V == 4);
     static constexpr int OCC = (V == 2) ? 1 : 8;   // 8 waves/SIMD => <= 64 VGPRs (A/B: -25% bounce time)
 };
 
@@ -275,6 +378,7 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
 template <bool COUNT, int V>
 __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ* __restrict__ q,
                                                                uint32_t* __restrict__ qcount, int emit) {
+    __shared__ uint32_t s_pst[TV<V>::PACKET ? 4 * 3 * STACK_SIZE : 1];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t band = blockIdx.y * a.nranks + a.rank;
@@ -285,16 +389,20 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
     uint32_t hits = 0, tex = 0;
     bool live = false;
     RayQ e;
+    const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
+    const f3 o = mk(((float)x - hw) / 4.f, ((float)y - hh) / 4.f, 0.f);   // :23-24
+    const f3 d = mk(0.f, 0.f, 1.f);
+    const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    float best = 0.f;
+    uint32_t bl = 0;
+    bool phit = false;
+    if (TV<V>::PACKET)   // whole wave, before any divergence
+        phit = traverse_packet<COUNT, TV<V>::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, best, bl, c,
+                                                      s_pst + w * 3 * STACK_SIZE);
     if (valid) {
-        const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
-        const f3 o = mk(((float)x - hw) / 4.f, ((float)y - hh) / 4.f, 0.f);   // :23-24
-        const f3 d = mk(0.f, 0.f, 1.f);
-        const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
-        float best;
-        uint32_t bl;
         float4 color;
         float intensity = 0.f;
-        if (trace_ray<COUNT, V>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
+        if (TV<V>::PACKET ? phit : trace_ray<COUNT, V>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
             hits = 1;
             const HitInfo h = shade_hit(a, bl, o, d, best);
             tex = h.textured;
@@ -421,6 +529,8 @@ void launch_bounce_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_co
     switch (variant) {                                    \
         case 1: count ? M(true, 1) : M(false, 1); break;  \
         case 2: count ? M(true, 2) : M(false, 2); break;  \
+        case 3: count ? M(true, 3) : M(false, 3); break;  \
+        case 4: count ? M(true, 4) : M(false, 4); break;  \
         default: count ? M(true, 0) : M(false, 0); break; \
     }
 

@@ -20,7 +20,8 @@ def main():
     W, H = int(os.environ.get("AB_W", "3840")), int(os.environ.get("AB_H", "2160"))
     rounds = int(os.environ.get("AB_ROUNDS", "5"))
     variants = [("reference", 0), ("reference+sort", rt.FLAG_SORT_BOUNCE), ("nearest", rt.FLAG_NEAREST_FIRST),
-                ("nearest+sort", rt.FLAG_NEAREST_FIRST | rt.FLAG_SORT_BOUNCE), ("first_version", 1 << rt.FLAG_VARIANT_SHIFT)]
+                ("nearest+sort", rt.FLAG_NEAREST_FIRST | rt.FLAG_SORT_BOUNCE), ("first_version", 1 << rt.FLAG_VARIANT_SHIFT),
+                ("packet", rt.FLAG_PACKET_PRIMARY), ("nearest+packet", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY)]
     scene = rt.synthetic(ntris, seed=0x5EED0005, half_extent=(100, 100, 50))
     ctx = rt.Context(device=0, flags=rt.FLAG_TIMING)
     ctx.set_scene(scene)

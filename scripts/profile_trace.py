@@ -1,0 +1,20 @@
+#!/usr/bin/env python3
+"""Small driver for rocprofv3 runs: builds the C5 scene once and runs a few
+builds + traces in the requested mode (env PROF_MODE = reference | nearest)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import raytracebvh_amd as rt  # noqa: E402
+
+mode = os.environ.get("PROF_MODE", "nearest")
+flags = rt.FLAG_NEAREST_FIRST if mode == "nearest" else rt.FLAG_SORT_BOUNCE
+scene = rt.synthetic(10_000_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+W, H = 3840, 2160
+with rt.Context(device=0, flags=flags) as c:
+    c.set_scene(scene)
+    c.set_camera(*rt.camera_reference(W, H))
+    for _ in range(int(os.environ.get("PROF_ITERS", "3"))):
+        c.build()
+        c.trace(W, H, 1)
+print("done", mode)

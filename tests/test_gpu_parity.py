@@ -198,7 +198,8 @@ def test_build_10m_tree_properties():
 
 # ---------------------------------------------------------------- trace
 TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest": rt.FLAG_NEAREST_FIRST,
-               "first_version": 1 << rt.FLAG_VARIANT_SHIFT}
+               "first_version": 1 << rt.FLAG_VARIANT_SHIFT, "packet": rt.FLAG_PACKET_PRIMARY,
+               "nearest+packet": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY}
 
 
 def _trace_both(s, W, H, bounces, rows=None, flags=0):
@@ -228,7 +229,7 @@ def test_trace_matches_oracle_on_obj(name, W, H, bounces, mode):
     np.testing.assert_array_equal(inten, oint)
     assert sum(st["hits"]) == ost["hits"] and st["textured_hits"] == ost["textured_hits"]
     assert st["bounce_rays"] == ost["bounce"] and st["stack_overflows"] == 0
-    if mode != "nearest":   # the reference-order kernels take exactly the oracle's steps
+    if "nearest" not in mode:   # the reference-order kernels take exactly the oracle's steps
         assert sum(st["internal_visits"]) == ost["internal_visits"]
         assert sum(st["leaf_visits"]) == ost["leaf_visits"]
     else:
