@@ -31,10 +31,11 @@ PEAK_HBM_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic bytes of OUR layout (DESIGN.md "Byte model"), per unit
 B_INTERNAL_VISIT = 64            # one 64-B child-pair record
 B_LEAF_VISIT = 48                # one 48-B clip-space triangle record
-B_HIT_SHADE = 48 + 12 + 96 + 4 + 68   # leaf re-read, 3 indices, 3 vertices, matIndex, material
+B_HIT_SHADE = 16 + 48 + 12 + 96 + 4 + 68   # leaf tri id, clip triangle, 3 indices, 3 vertices, matIndex, material
 B_PRIMARY_OUT = 16               # color
 B_QUEUE = 32                     # one bounce-queue entry (write by primary, read by bounce)
 B_BOUNCE_RMW = 32                # color read + write
+B_HIT_RECORD = 8                 # (t, leaf) written by k_bounce_trav, read by k_bounce_shade
 B_BUILD_PER_TRI = 392            # DESIGN.md "Byte model": build kernels' algorithmic bytes per triangle
 
 WORKLOADS = {
@@ -56,14 +57,17 @@ def make_scene(rt, wl):
     return rt.synthetic(wl["ntris"], seed=wl["seed"], half_extent=wl["half"])
 
 
-def trace_bytes(st, pass_idx, rays_in, rays_live_out):
-    v_int, v_leaf, hits = st["internal_visits"][pass_idx], st["leaf_visits"][pass_idx], st["hits"][pass_idx]
-    b = B_INTERNAL_VISIT * v_int + B_LEAF_VISIT * v_leaf + B_HIT_SHADE * hits
-    if pass_idx == 0:
-        b += B_PRIMARY_OUT * rays_in + B_QUEUE * rays_live_out
-    else:
-        b += (B_QUEUE + B_BOUNCE_RMW) * rays_in
-    return b
+def trace_bytes(st, kernel, rays_in, rays_live_out):
+    """Algorithmic bytes of one launch (DESIGN.md "Byte model")."""
+    if kernel == "k_primary":
+        return (B_INTERNAL_VISIT * st["internal_visits"][0] + B_LEAF_VISIT * st["leaf_visits"][0]
+                + B_HIT_SHADE * st["hits"][0] + B_PRIMARY_OUT * rays_in + B_QUEUE * rays_live_out)
+    if kernel == "k_bounce_trav":
+        return (B_INTERNAL_VISIT * st["internal_visits"][1] + B_LEAF_VISIT * st["leaf_visits"][1]
+                + (B_QUEUE + B_HIT_RECORD) * rays_in)
+    # k_bounce_shade
+    return ((B_QUEUE + B_HIT_RECORD + B_BOUNCE_RMW) * rays_in + B_HIT_SHADE * st["hits"][1]
+            + B_QUEUE * rays_live_out)
 
 
 def load_pmc(workload, kernel):
@@ -202,14 +206,15 @@ def main():
     # reference order (the exact findCollision DFS) and nearest-first; the nearest-first
     # number is the headline only if its frame is bit-identical to the reference-order
     # frame of this same run (checked on every rank's bands)
-    ref = timed(rt.FLAG_SORT_BOUNCE)
-    near = timed(rt.FLAG_NEAREST_FIRST)
+    FAST = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE   # same results as the plain kernels (tests)
+    ref = timed(FAST)
+    near = timed(FAST | rt.FLAG_NEAREST_FIRST)
     same = torch.tensor([0.0 if torch.equal(ref["band"], near["band"]) else 1.0], device=dev)
     if world > 1:
         dist.all_reduce(same)
     identical = float(same.item()) == 0.0
     use = near if (identical and args.traversal != "reference") else ref
-    mode_flags = rt.FLAG_NEAREST_FIRST if use is near else rt.FLAG_SORT_BOUNCE
+    mode_flags = FAST | (rt.FLAG_NEAREST_FIRST if use is near else 0)
     rays_per_step, ms_step, value, tst = use["rays"], use["ms_step"], use["value"], use["stats"]
     traversal = {"mode": "nearest-first" if use is near else "reference-order",
                  "frames_identical": identical,
@@ -225,9 +230,11 @@ def main():
     kern = {}
     prim_rays = cst["primary_rays"]
     live = cst["bounce_rays"]
-    kern["k_primary"] = dict(ms=tst["ms_stage"][5], bytes=trace_bytes(cst, 0, prim_rays, live))
-    if bounces:
-        kern["k_bounce"] = dict(ms=tst["ms_stage"][6], bytes=trace_bytes(cst, 1, live, 0))
+    kern["k_primary"] = dict(ms=tst["ms_stage"][5], bytes=trace_bytes(cst, "k_primary", prim_rays, live))
+    if bounces:   # 1 bounce: the queue's rays are traced once and none is re-emitted
+        kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7], bytes=trace_bytes(cst, "k_bounce_trav", live, 0))
+        kern["k_bounce_shade"] = dict(ms=tst["ms_stage"][6] - tst["ms_stage"][7],
+                                      bytes=trace_bytes(cst, "k_bounce_shade", live, 0))
     dom = max(kern, key=lambda k: kern[k]["ms"])
     for k, v in kern.items():
         v["achieved_gbs"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0

@@ -35,6 +35,9 @@ struct rtbvh_ctx {
     uint32_t* d_sort_scratch = nullptr;
     float4 *d_tclip = nullptr, *d_leaf = nullptr;
     Inner* d_inner = nullptr;
+    Inner* d_inner4 = nullptr;               // 4-wide traversal view, built with RTBVH_FLAG_WIDE_BVH
+    uint32_t cap_T4 = 0;
+    bool wide_built = false;
     uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr;
     float* d_bounds = nullptr;
     float* d_rootbox = nullptr;
@@ -48,7 +51,8 @@ struct rtbvh_ctx {
     RayQ* d_q[2] = {nullptr, nullptr};
     uint32_t *d_bkin = nullptr, *d_bvin = nullptr, *d_bka = nullptr, *d_bva = nullptr, *d_bkb = nullptr,
              *d_bvb = nullptr, *d_bscratch = nullptr;   // bounce coherence sort
-    uint32_t* d_qcount = nullptr;             // [16]
+    uint32_t* d_qcount = nullptr;             // [32]: queue counts [0..15], bounce work counters [16..31]
+    float2* d_hit = nullptr;                  // per queued bounce ray: (t, leaf | INVALID)
     unsigned long long* d_counters = nullptr; // [8]
     bool traced = false;
 
@@ -56,7 +60,8 @@ struct rtbvh_ctx {
     // per trace 3 (before primary, after primary, after bounces)
     static constexpr int RING = 32;
     hipEvent_t evb[RING][6] = {};
-    hipEvent_t evt[RING][3] = {};
+    hipEvent_t evt[RING][5] = {};   // trace start, primary done, end, first bounce traversal start/end
+    bool evt_trav[RING] = {};
     uint32_t n_builds = 0, n_traces = 0;   // timed samples since reset
     hipEvent_t ev_ready = nullptr;
 };
@@ -127,7 +132,8 @@ rtbvh_status ensure_trace_capacity(rtbvh_ctx* c, size_t P) {
     HIPC(c, dalloc(c->d_bkb, P));
     HIPC(c, dalloc(c->d_bvb, P));
     HIPC(c, dalloc(c->d_bscratch, sort_scratch_words((uint32_t)P)));
-    if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 16));
+    HIPC(c, dalloc(c->d_hit, P));
+    if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 32));
     if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 16));
     c->cap_P = P;
     return RTBVH_OK;
@@ -162,6 +168,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
 TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks, float4* color, float* inten) {
     TraceArgs a{};
     a.inner = c->d_inner;
+    a.inner4 = c->d_inner4;
     a.leaf = c->d_leaf;
     a.tclip = c->d_tclip;
     a.verts = c->d_verts;
@@ -197,7 +204,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool count = (c->cfg.flags & RTBVH_FLAG_COUNT_VISITS) != 0;
     const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream;
     TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
-    HIPC(c, hipMemsetAsync(c->d_qcount, 0, 16 * sizeof(uint32_t), s));
+    HIPC(c, hipMemsetAsync(c->d_qcount, 0, 32 * sizeof(uint32_t), s));
     HIPC(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
@@ -206,8 +213,15 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t vsel = (c->cfg.flags >> RTBVH_FLAG_VARIANT_SHIFT) & 15u;
     if (vsel == 1) variant = 2;
     int pvariant = variant;   // primary kernel: 2 = wave packets
-    if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel == 0) pvariant = variant == 1 ? 4 : 3;
+    if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1) pvariant = variant == 1 ? 4 : 3;
     const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
+    const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && vsel != 1;
+    if (wide && !c->wide_built)
+        return fail(c, RTBVH_ERR_NOT_READY, "RTBVH_FLAG_WIDE_BVH trace needs a build made with that flag set");
+    const bool refill = ((c->cfg.flags & RTBVH_FLAG_REFILL_BOUNCE) != 0 || wide) && vsel != 1;
+    // A/B of the refill kernel's LDS stack depth: variant 2 -> none, 3 -> 8, 4 -> 20, else 16
+    const int lds_stack = vsel == 2 ? 0 : vsel == 3 ? 8 : vsel == 4 ? 20 : 16;
+    const int bmode = wide ? 2 : (variant == 1 ? 1 : 0);
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
     launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, pvariant, s);
     if (timing) HIPC(c, hipEventRecord(ev[1], s));
@@ -218,11 +232,20 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             perm = radix_sort_pairs(c->d_bkin, c->d_bvin, c->d_bka, c->d_bva, c->d_bkb, c->d_bvb, P, 30,
                                     c->d_bscratch, s).vals;
         }
-        launch_bounce(a, c->d_q[b & 1], &c->d_qcount[b], perm, c->d_q[(b + 1) & 1], &c->d_qcount[b + 1], count,
-                      b + 1 < bounces, variant, s);
+        if (refill) {
+            if (timing && b == 0) HIPC(c, hipEventRecord(ev[3], s));
+            launch_bounce_traverse(a, c->d_q[b & 1], &c->d_qcount[b], perm, count, bmode, c->d_hit,
+                                   &c->d_qcount[16 + b], lds_stack, s);
+            if (timing && b == 0) HIPC(c, hipEventRecord(ev[4], s));
+            launch_bounce_shade(a, c->d_q[b & 1], &c->d_qcount[b], c->d_hit, c->d_q[(b + 1) & 1],
+                                &c->d_qcount[b + 1], count, b + 1 < bounces, P, s);
+        } else
+            launch_bounce(a, c->d_q[b & 1], &c->d_qcount[b], perm, c->d_q[(b + 1) & 1], &c->d_qcount[b + 1], count,
+                          b + 1 < bounces, variant, s);
     }
     if (timing) {
         HIPC(c, hipEventRecord(ev[2], s));
+        c->evt_trav[c->n_traces % rtbvh_ctx::RING] = refill && bounces > 0;
         c->n_traces++;
     }
     c->W = W;
@@ -304,9 +327,9 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_inner4);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
-    dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount);
+    dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
     dfree(c->d_bscratch);
     dfree(c->d_counters);
@@ -382,6 +405,12 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     hipStream_t s = c->stream;
     const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0;
     BuildArgs a = build_args(c);
+    const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && c->T > 1;
+    if (wide && c->cap_T4 < c->T) {
+        HIPC(c, dalloc(c->d_inner4, 2 * (size_t)(c->T - 1)));
+        c->cap_T4 = c->T;
+    }
+    a.inner4 = wide ? c->d_inner4 : nullptr;
     hipEvent_t* ev = c->evb[c->n_builds % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (c->cfg.morton_mode == RTBVH_MORTON_CPUTESTS) {
@@ -402,6 +431,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (timing) HIPC(c, hipEventRecord(ev[5], s));
     if (timing) c->n_builds++;
     c->built = true;
+    c->wide_built = wide || c->T == 1;
     return check_launch(c, "build kernels");
 }
 
@@ -502,6 +532,17 @@ rtbvh_status rtbvh_read_bvh(rtbvh_ctx* c, rtbvh_node* out, uint32_t capacity) {
     return RTBVH_OK;
 }
 
+rtbvh_status rtbvh_read_wide(rtbvh_ctx* c, uint32_t* out, uint64_t capacity) {
+    if (!c || !out) return RTBVH_ERR_INVALID_ARG;
+    if (!c->built || !c->wide_built) return fail(c, RTBVH_ERR_NOT_READY, "no RTBVH_FLAG_WIDE_BVH build yet");
+    const size_t total = c->T > 1 ? 2 * (size_t)(c->T - 1) : 0;
+    if (capacity < total) return fail(c, RTBVH_ERR_INVALID_ARG, "read_wide: capacity < 2(n-1)");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (total) HIPC(c, hipMemcpy(out, c->d_inner4, total * sizeof(Inner), hipMemcpyDeviceToHost));
+    return RTBVH_OK;
+}
+
 rtbvh_status rtbvh_read_morton(rtbvh_ctx* c, uint32_t* codes) {
     if (!c || !codes) return RTBVH_ERR_INVALID_ARG;
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "no build yet");
@@ -551,6 +592,10 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         out->ms_stage[5] += ms / nt;
         HIPC(c, hipEventElapsedTime(&ms, c->evt[k][1], c->evt[k][2]));
         out->ms_stage[6] += ms / nt;
+        if (c->evt_trav[k]) {
+            HIPC(c, hipEventElapsedTime(&ms, c->evt[k][3], c->evt[k][4]));
+            out->ms_stage[7] += ms / nt;
+        }
     }
     out->timed_traces = nt;
     if (c->traced && c->d_counters) {

@@ -246,9 +246,22 @@ __device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
     hi = mk(__uint_as_float((uint32_t)(b >> 32)), __uint_as_float((uint32_t)c), __uint_as_float((uint32_t)(c >> 32)));
 }
 
+// 4-wide traversal view: the complete child-pair record of node p also goes to
+// inner4[2 * parent(p) + side(p)], so the records of two siblings share one 128-B
+// line (one HBM request fetches both; the traversal tests the four grandchild
+// boxes of a node at once).  Leaf children get a pseudo-record {leaf box, -, leaf, INVALID}.
+__device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
+                                             uint32_t cr) {
+    float4* d = reinterpret_cast<float4*>(dst);
+    d[0] = make_float4(lmin.x, lmin.y, lmin.z, lmax.x);
+    d[1] = make_float4(lmax.y, lmax.z, rmin.x, rmin.y);
+    d[2] = make_float4(rmin.z, rmax.x, rmax.y, rmax.z);
+    d[3] = make_float4(__uint_as_float(cl), __uint_as_float(cr), 0.f, 0.f);
+}
+
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __restrict__ inner,
                                             const uint32_t* __restrict__ pint, uint32_t* __restrict__ cnt,
-                                            float* __restrict__ rootbox) {
+                                            float* __restrict__ rootbox, Inner* __restrict__ inner4) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
@@ -260,10 +273,15 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
         asm volatile("" ::: "memory");
         f3 smin, smax;
         ld_box_sc1(side ? inner[p].lmin : inner[p].rmin, smin, smax);
+        e = pint[p];
+        if (inner4 && e != INVALID) {
+            const uint2 ids = *reinterpret_cast<const uint2*>(&inner[p].child_l);
+            if (side) store_record(inner4 + 2 * (size_t)(e >> 1) + (e & 1u), smin, smax, lo, hi, ids.x, ids.y);
+            else      store_record(inner4 + 2 * (size_t)(e >> 1) + (e & 1u), lo, hi, smin, smax, ids.x, ids.y);
+        }
         // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
         if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
         else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
-        e = pint[p];
         if (e == INVALID) {
             rootbox[0] = lo.x; rootbox[1] = lo.y; rootbox[2] = lo.z;
             rootbox[3] = hi.x; rootbox[4] = hi.y; rootbox[5] = hi.z;
@@ -283,7 +301,9 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
         a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
         return;
     }
-    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox);
+    const uint32_t e = a.pleaf[i];
+    if (a.inner4) store_record(a.inner4 + 2 * (size_t)(e >> 1) + (e & 1u), lo, hi, lo, hi, LEAF_BIT | i, INVALID);
+    refit_climb(lo, hi, e, a.inner, a.pint, a.refit_cnt, a.rootbox, a.inner4);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
@@ -295,7 +315,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
         for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
         return;
     }
-    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox);
+    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox, nullptr);
 }
 
 // reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k

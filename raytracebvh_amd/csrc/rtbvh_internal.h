@@ -46,6 +46,8 @@ struct BuildArgs {
     const uint32_t* sorted_vals;  // [T]
     float4* leaf;             // [4T] 64-B sorted leaf records
     Inner* inner;             // [T-1]
+    Inner* inner4;            // [2(T-1)] 4-wide traversal records (RTBVH_FLAG_WIDE_BVH) or null:
+                              // inner4[2p + side] = child-pair record of p's child on that side
     uint32_t* pleaf;          // [T]
     uint32_t* pint;           // [T-1]
     uint32_t* refit_cnt;      // [T-1]
@@ -63,6 +65,7 @@ void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t 
 // ---- trace (trace.hip) ------------------------------------------------------
 struct TraceArgs {
     const Inner* inner;
+    const Inner* inner4;      // 4-wide view (see BuildArgs::inner4) or null
     const float4* leaf;       // [4T] sorted leaf records (see build.hip)
     const float4* tclip;      // [3T] clip-space triangles in triangle order (hit shading)
     const float* verts;       // rtbvh_vertex AoS, 8 floats each
@@ -82,6 +85,13 @@ struct TraceArgs {
 void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, int variant, hipStream_t s);
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
                    uint32_t* qout_count, bool count, bool emit, int variant, hipStream_t s);
+// bounce pass as persistent refill traversal (hit records) + shading kernel; `next` is a
+// zeroed work counter; mode 0 reference order, 1 nearest-first, 2 nearest-first on inner4;
+// lds_stack = stack entries kept in LDS (0, 8, 16, 20)
+void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
+                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack, hipStream_t s);
+void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
+                         RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
 // coherence sort keys of a bounce queue: P entries (past *count: key 0xFFFFFFFF)
 void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, uint32_t P, uint32_t* keys,
                         uint32_t* vals, hipStream_t s);

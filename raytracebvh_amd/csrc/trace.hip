@@ -187,10 +187,15 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef const v4f __attribute__((address_space(4))) cv4f;
 
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef const v16f __attribute__((address_space(4))) cv16f;
+
 __device__ __forceinline__ float4 sload(const float4* p) {
     const v4f v = *(cv4f*)p;
     return make_float4(v.x, v.y, v.z, v.w);
 }
+// the whole 64-B record in one s_load_dwordx16 (one scalar-memory round trip per step)
+__device__ __forceinline__ v16f sload16(const void* p) { return *(cv16f*)p; }
 
 template <bool COUNT, bool NEAREST>
 __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
@@ -202,8 +207,9 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
     best = 0.f;
     best_leaf = 0;
     uint64_t mask = __ballot(valid);
-    int sp = 0;
-    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    int sp = 0;                      // entries on the wave stack; the top one is cached below
+    uint32_t node = (T == 1) ? LEAF_BIT : 0u, top_node = 0;
+    uint64_t top_mask = 0;
     if (mask == 0) return false;
     uint32_t guard = 2 * T + 2;
     while (true) {
@@ -211,11 +217,10 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
         bool pop = false;
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
-            const float4 a = sload(leaf + 4 * (size_t)j), b = sload(leaf + 4 * (size_t)j + 1);
-            const float e2z = sload(leaf + 4 * (size_t)j + 2).x;
+            const v16f q = sload16(leaf + 4 * (size_t)j);
             if (mask & lanebit) {
                 if (COUNT) c.leaf++;
-                const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
+                const float t = ray_triangle(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]));
                 if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < best_leaf))) {
                     best = t;
                     best_leaf = j;
@@ -224,15 +229,14 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
             }
             pop = true;
         } else {
-            const float4* r = reinterpret_cast<const float4*>(inner + node);
-            const float4 q0 = sload(r), q1 = sload(r + 1), q2 = sload(r + 2), q3f = sload(r + 3);
-            const uint32_t cl = __float_as_uint(q3f.x), cr = __float_as_uint(q3f.y);
+            const v16f q = sload16(inner + node);
+            const uint32_t cl = __float_as_uint(q[12]), cr = __float_as_uint(q[13]);
             bool lh = false, rh = false;
             float tl = 0.f, tr = 0.f;
             if (mask & lanebit) {
                 if (COUNT) c.internal++;
-                lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
-                rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
+                lh = ray_box(o, inv, q[0], q[1], q[2], q[3], q[4], q[5], hit, best, tl);
+                rh = ray_box(o, inv, q[6], q[7], q[8], q[9], q[10], q[11], hit, best, tr);
             }
             const uint64_t ml = __ballot(lh), mr = __ballot(rh);
             if ((ml | mr) == 0) {
@@ -246,13 +250,16 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
                 }
                 if (sp + 1 >= STACK_SIZE) { c.overflow++; pop = true; }
                 else {
-                    ++sp;
-                    if (lane == 0) {   // push the second child and its lanes
-                        const uint64_t m2 = swap ? ml : mr;
-                        s_st[3 * sp] = swap ? cl : cr;
-                        s_st[3 * sp + 1] = (uint32_t)m2;
-                        s_st[3 * sp + 2] = (uint32_t)(m2 >> 32);
+                    // push the second child and its lanes: the old top goes to LDS, the
+                    // new entry stays in SGPRs (top cache, as in the per-lane loop)
+                    if (sp > 0 && lane == 0) {
+                        s_st[3 * sp] = top_node;
+                        s_st[3 * sp + 1] = (uint32_t)top_mask;
+                        s_st[3 * sp + 2] = (uint32_t)(top_mask >> 32);
                     }
+                    ++sp;
+                    top_node = swap ? cl : cr;
+                    top_mask = swap ? ml : mr;
                     node = swap ? cr : cl;
                     mask = swap ? mr : ml;
                 }
@@ -263,12 +270,14 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
         }
         if (pop) {
             if (sp == 0) break;
-            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the lane-0 push has landed in LDS
-            node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
-            const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
-            const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
-            mask = ((uint64_t)hi << 32) | lo;
-            --sp;
+            node = top_node;
+            mask = top_mask;
+            if (--sp > 0) {   // refill the cached top from LDS (lane 0's earlier write)
+                top_node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
+                const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
+                top_mask = ((uint64_t)hi << 32) | lo;
+            }
         }
     }
     return hit;
@@ -477,6 +486,261 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_bounce(TraceArgs a, const
     flush_counts<COUNT>(a, c, hits, tex, 5);
 }
 
+// ---- bounce pass split in two: persistent traversal with lane refill + shading ----
+// The one-ray-per-lane bounce kernel keeps a wave until its slowest ray is done:
+// PMC on C5 showed ~12 of 64 lanes active per traversal step (1.6e8 wave loads for
+// 4.7e8 lane visits).  Here each lane that finishes its ray takes the next one from
+// the queue (one atomic per wave per refill, Aila & Laine's dynamic fetch), so the
+// wave stays full; the finished ray's (t, leaf) goes to a hit record, and the
+// shading runs afterwards as a plain one-thread-per-ray kernel (k_bounce_shade).
+// Per-lane traversal state and visit order are exactly those of traverse().
+constexpr uint32_t REFILL_MIN = 16;   // refill when at least this many lanes are idle
+constexpr int STACK4 = 100;           // 4-wide walk: <= 3 pushes per level of a <= 32-level tree
+
+// one nearest-first step on the 4-wide view (inner4): the four grandchild boxes of
+// binary node `node` come from one 128-B line; hit children are visited nearest
+// first, the others pushed with their entry distance, and a popped entry whose
+// entry distance is already beyond `best` is dropped without a fetch (the box test
+// at its visit would fail: best only decreases).  The (t, leaf) minimum kept is
+// the reference DFS's answer under the same condition as nearest-first.
+__device__ __forceinline__ void sort2(float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
+    const bool sw = tb < ta;
+    const float t = sw ? tb : ta;
+    const uint32_t i = sw ? ib : ia;
+    tb = sw ? ta : tb;
+    ib = sw ? ia : ib;
+    ta = t;
+    ia = i;
+}
+
+// Binary modes keep the stack entries [0, S) in LDS, [entry][lane] (a wave's lanes hit
+// 64 distinct banks whatever their depths), and only deeper entries in scratch: the
+// all-scratch stack of 8192 resident waves (17 KB each) does not fit in L2 and PMC
+// showed ~3.6 GB of stack write-back per C5 bounce pass.
+template <bool COUNT, int MODE, int S>
+__global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restrict__ inner,
+                                                          const float4* __restrict__ leaf, uint32_t T,
+                                                          const RayQ* __restrict__ qin,
+                                                          const uint32_t* __restrict__ qin_count,
+                                                          const uint32_t* __restrict__ perm,
+                                                          float2* __restrict__ hitrec, uint32_t* __restrict__ next,
+                                                          unsigned long long* __restrict__ counters) {
+    constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
+    const uint32_t n = *qin_count;
+    const uint32_t lane = lane_id();
+    Counts c = {0, 0, 0};
+    bool has = false, hit = false;
+    uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
+    int sp = 0;
+    float best = 0.f;
+    f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
+    __shared__ uint32_t s_stk[WIDE || S == 0 ? 1 : S][BLOCK];
+    uint32_t stack[WIDE ? 1 : STACK_SIZE - S];   // entries [S, STACK_SIZE)
+    uint2 wstack[WIDE ? STACK4 : 1];   // (node, entry distance bits)
+    const uint32_t tid = threadIdx.x;
+    auto spush = [&](uint32_t v) {
+        if (sp < S) s_stk[sp][tid] = v;
+        else stack[sp - S] = v;
+        ++sp;
+    };
+    auto spop_top = [&]() {   // --sp; refill the cached top from entry sp
+        if (--sp >= 0) top = sp < S ? s_stk[sp][tid] : stack[sp - S];
+    };
+    bool drained = false;
+    while (true) {
+        const uint64_t idle = __ballot(!has);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (!drained && (nidle >= REFILL_MIN || nidle == 64)) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(next, nidle);
+            base = __shfl(base, 0, 64);
+            if (base + nidle >= n) drained = true;
+            if (!has) {
+                const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+                const uint32_t p = base + (uint32_t)__popcll(idle & lt);
+                if (p < n) {
+                    r = perm ? perm[p] : p;
+                    const float4 q0 = reinterpret_cast<const float4*>(qin + r)[0];
+                    const float4 q1 = reinterpret_cast<const float4*>(qin + r)[1];
+                    o = mk(q0.z, q0.w, q1.x);
+                    d = mk(q1.y, q1.z, q1.w);
+                    inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+                    has = true;
+                    hit = false;
+                    best = 0.f;
+                    bl = 0;
+                    sp = 0;
+                    top = INVALID;
+                    node = (T == 1) ? LEAF_BIT : 0u;
+                    guard = 2 * T + 2;
+                }
+            }
+        }
+        if (__ballot(has) == 0) break;   // queue drained and every lane done
+        if (!has) continue;
+        bool done = false;
+        if (--guard == 0) {
+            c.overflow++;
+            done = true;
+        } else if (node & LEAF_BIT) {
+            const uint32_t j = node & ~LEAF_BIT;
+            const float4* rr = leaf + 4 * (size_t)j;
+            const float4 la = rr[0], lb = rr[1];
+            const float e2z = rr[2].x;
+            if (COUNT) c.leaf++;
+            const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
+            if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
+                best = t;
+                bl = j;
+                hit = true;
+            }
+            if (WIDE) {
+                node = INVALID;   // pop below
+            } else {
+                node = top;                             // pop
+                spop_top();
+                done = sp == -1;
+            }
+        } else if (WIDE) {
+            if (COUNT) c.internal++;
+            const float4* rr = reinterpret_cast<const float4*>(inner + 2 * (size_t)node);
+            const float4 a0 = rr[0], a1 = rr[1], a2 = rr[2];
+            const uint4 a3 = reinterpret_cast<const uint4*>(rr)[3];
+            const float4 b0 = rr[4], b1 = rr[5], b2 = rr[6];
+            const uint4 b3 = reinterpret_cast<const uint4*>(rr)[7];
+            float t0, t1, t2, t3;
+            const bool h0 = ray_box(o, inv, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, hit, best, t0);
+            const bool h1 = a3.y != INVALID && ray_box(o, inv, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, hit, best, t1);
+            const bool h2 = ray_box(o, inv, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, hit, best, t2);
+            const bool h3 = b3.y != INVALID && ray_box(o, inv, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, hit, best, t3);
+            const float INF = __builtin_inff();
+            float k0 = h0 ? t0 : INF, k1 = h1 ? t1 : INF, k2 = h2 ? t2 : INF, k3 = h3 ? t3 : INF;
+            uint32_t i0 = h0 ? a3.x : INVALID, i1 = h1 ? a3.y : INVALID, i2 = h2 ? b3.x : INVALID,
+                     i3 = h3 ? b3.y : INVALID;
+            // 4-element sorting network on the entry distance (missing children last)
+            sort2(k0, i0, k1, i1);
+            sort2(k2, i2, k3, i3);
+            sort2(k0, i0, k2, i2);
+            sort2(k1, i1, k3, i3);
+            sort2(k1, i1, k2, i2);
+            node = i0;   // nearest (INVALID when no child is hit -> pop below)
+            if (sp + 3 > STACK4) {
+                c.overflow++;
+                done = true;
+            } else {   // push the others farthest first
+                if (i3 != INVALID) wstack[sp++] = make_uint2(i3, __float_as_uint(k3));
+                if (i2 != INVALID) wstack[sp++] = make_uint2(i2, __float_as_uint(k2));
+                if (i1 != INVALID) wstack[sp++] = make_uint2(i1, __float_as_uint(k1));
+            }
+        } else {
+            if (COUNT) c.internal++;
+            const float4* rr = reinterpret_cast<const float4*>(inner + node);
+            const float4 q0 = rr[0], q1 = rr[1], q2 = rr[2];
+            const uint4 q3 = reinterpret_cast<const uint4*>(rr)[3];
+            float tl, tr;
+            const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
+            const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
+            if (!lh && !rh) {
+                node = top;                             // pop
+                spop_top();
+                done = sp == -1;
+            } else {
+                const bool swap = NEAREST && lh && rh && tr < tl;
+                if (lh && rh) {
+                    if (sp + 1 >= STACK_SIZE) {
+                        c.overflow++;
+                        node = top;
+                        spop_top();
+                        done = sp == -1;
+                    } else {
+                        spush(top);                     // push the second child
+                        top = swap ? q3.x : q3.y;
+                        node = swap ? q3.y : q3.x;
+                    }
+                } else {
+                    node = lh ? q3.x : q3.y;
+                }
+            }
+        }
+        if (WIDE && !done && node == INVALID) {   // pop, dropping entries that cannot improve
+            while (sp > 0) {
+                const uint2 e = wstack[--sp];
+                if (!hit || __uint_as_float(e.y) <= best) {
+                    node = e.x;
+                    break;
+                }
+            }
+            done = node == INVALID;
+        }
+        if (done) {
+            hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
+            has = false;
+        }
+    }
+    if (COUNT || c.overflow) {
+        unsigned long long v[3] = {c.internal, c.leaf, c.overflow};
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+        if (lane == 0) {
+            if (COUNT) {
+                atomicAdd(&counters[5], v[0]);
+                atomicAdd(&counters[6], v[1]);
+            }
+            if (v[2]) atomicAdd(&counters[8], v[2]);
+        }
+    }
+}
+
+// RayTraceReflection.hlsl:19-60 for every queued ray, from its hit record
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ* __restrict__ qin,
+                                                        const uint32_t* __restrict__ qin_count,
+                                                        const float2* __restrict__ hitrec, RayQ* __restrict__ qout,
+                                                        uint32_t* __restrict__ qout_count, int emit) {
+    const uint32_t n = *qin_count;
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (blockIdx.x * BLOCK >= n) return;   // whole block past the queue (wave_append below needs all lanes)
+    bool live = false;
+    uint32_t hits = 0, tex = 0;
+    RayQ e;
+    if (i < n) {
+        e = qin[i];
+        const float2 h2 = hitrec[i];
+        const uint32_t bl = __float_as_uint(h2.y);
+        const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
+        float4 col = a.color[e.idx];
+        float intensity = e.intensity;
+        if (bl != INVALID) {
+            hits = 1;
+            const HitInfo h = shade_hit(a, bl, o, d, h2.x);
+            tex = h.textured;
+            col = make_float4(lerpf(col.x, h.color.x, intensity), lerpf(col.y, h.color.y, intensity),
+                              lerpf(col.z, h.color.z, intensity), lerpf(col.w, h.color.w, intensity));
+            intensity *= h.shininess / 1000.f * 1;
+            const f3 ro = add(h.hitp, mul(h.nrm, .0001f));   // RAY_OFFSET .0001
+            const f3 rd = normalize(reflect(d, h.nrm));
+            e.intensity = intensity;
+            e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
+            e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
+            live = 0 < intensity;
+        } else {
+            col = make_float4(lerpf(col.x, .5f, intensity), lerpf(col.y, .5f, intensity),
+                              lerpf(col.z, .5f, intensity), lerpf(col.w, 1.f, intensity));
+            intensity = 0.f;
+        }
+        a.color[e.idx] = col;
+        if (a.intensity) a.intensity[e.idx] = intensity;
+    }
+    const uint32_t slot = wave_append(emit && live, qout_count);
+    if (emit && live) qout[slot] = e;
+    if (COUNT) {
+        Counts c = {0, 0, 0};
+        flush_counts<COUNT>(a, c, hits, tex, 5);
+    }
+}
+
 // bounce-ray coherence sort key (results do not depend on the order): direction
 // octant in bits 27..29, 9-bit-per-axis Morton code of the origin inside the scene
 // box in bits 0..26 (A/B vs direction-only / origin-only / mixed keys: DESIGN.md).
@@ -523,6 +787,21 @@ void launch_bounce_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_co
                        qout_count, (int)emit);
 }
 
+template <bool COUNT, int S>
+void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
+                          int mode, float2* hitrec, uint32_t* next, hipStream_t s) {
+    const uint32_t blocks = 2048;   // persistent: 8 waves/SIMD x 1024 SIMDs / 4 waves per block
+    if (mode == 2)
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, 0>), dim3(blocks), dim3(BLOCK), 0, s, a.inner4, a.leaf, a.T, qin,
+                           qin_count, perm, hitrec, next, a.counters);
+    else if (mode == 1)
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 1, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T, qin,
+                           qin_count, perm, hitrec, next, a.counters);
+    else
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 0, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T,
+                           qin, qin_count, perm, hitrec, next, a.counters);
+}
+
 }  // namespace
 
 #define RTBVH_VARIANTS(M)                                 \
@@ -554,6 +833,31 @@ void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_coun
 void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, uint32_t P, uint32_t* keys,
                         uint32_t* vals, hipStream_t s) {
     hipLaunchKernelGGL(k_bounce_keys, dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, q, count, box, P, keys, vals);
+}
+
+void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
+                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack, hipStream_t s) {
+#define RTBVH_TRAV(S)                                                                                 \
+    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, s) \
+           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, s))
+    switch (lds_stack) {
+        case 0: RTBVH_TRAV(0); break;
+        case 8: RTBVH_TRAV(8); break;
+        case 20: RTBVH_TRAV(20); break;
+        default: RTBVH_TRAV(16); break;
+    }
+#undef RTBVH_TRAV
+}
+
+void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
+                         RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s) {
+    if (P == 0) return;
+    if (count)
+        hipLaunchKernelGGL((k_bounce_shade<true>), dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a, qin, qin_count,
+                           hitrec, qout, qout_count, (int)emit);
+    else
+        hipLaunchKernelGGL((k_bounce_shade<false>), dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a, qin,
+                           qin_count, hitrec, qout, qout_count, (int)emit);
 }
 
 }  // namespace rtbvh

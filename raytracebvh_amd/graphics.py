@@ -114,6 +114,12 @@ class Context:
         self._check(_L.lib().rtbvh_read_bvh(self._h, ctypes.c_void_p(out.ctypes.data), len(out)))
         return out
 
+    def read_wide(self) -> np.ndarray:
+        """4-wide traversal view of a FLAG_WIDE_BVH build: (2(n-1), 16) uint32 records."""
+        out = np.zeros((max(2 * (self.num_tris - 1), 0), 16), np.uint32)
+        self._check(_L.lib().rtbvh_read_wide(self._h, _L.ptr(out), len(out)))
+        return out
+
     def read_morton(self) -> np.ndarray:
         out = np.zeros(self.num_tris, np.uint32)
         self._check(_L.lib().rtbvh_read_morton(self._h, _L.ptr(out)))

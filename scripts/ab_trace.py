@@ -19,11 +19,24 @@ def main():
     ntris = int(os.environ.get("AB_TRIS", "10000000"))
     W, H = int(os.environ.get("AB_W", "3840")), int(os.environ.get("AB_H", "2160"))
     rounds = int(os.environ.get("AB_ROUNDS", "5"))
-    variants = [("reference", 0), ("reference+sort", rt.FLAG_SORT_BOUNCE), ("nearest", rt.FLAG_NEAREST_FIRST),
-                ("nearest+sort", rt.FLAG_NEAREST_FIRST | rt.FLAG_SORT_BOUNCE), ("first_version", 1 << rt.FLAG_VARIANT_SHIFT),
-                ("packet", rt.FLAG_PACKET_PRIMARY), ("nearest+packet", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY)]
+    variants = [("reference+sort", rt.FLAG_SORT_BOUNCE), ("nearest", rt.FLAG_NEAREST_FIRST),
+                ("nearest+packet", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY),
+                ("refill", rt.FLAG_REFILL_BOUNCE | rt.FLAG_PACKET_PRIMARY),
+                ("refill+sort", rt.FLAG_REFILL_BOUNCE | rt.FLAG_PACKET_PRIMARY | rt.FLAG_SORT_BOUNCE),
+                ("nearest+refill", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE),
+                ("nearest+refill+sort", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
+                 | rt.FLAG_SORT_BOUNCE),
+                ("nearest+wide", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH),
+                ("nearest+wide+sort", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
+                 | rt.FLAG_SORT_BOUNCE)]
+    if os.environ.get("AB_SET") == "stack":   # LDS stack depth of the refill traversal
+        base = rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
+        V = rt.FLAG_VARIANT_SHIFT
+        variants = [("nearest+refill lds16", base), ("lds0", base | 2 << V), ("lds8", base | 3 << V),
+                    ("lds20", base | 4 << V), ("reference+refill lds16", rt.FLAG_REFILL_BOUNCE | rt.FLAG_PACKET_PRIMARY),
+                    ("reference+refill lds0", rt.FLAG_REFILL_BOUNCE | rt.FLAG_PACKET_PRIMARY | 2 << V)]
     scene = rt.synthetic(ntris, seed=0x5EED0005, half_extent=(100, 100, 50))
-    ctx = rt.Context(device=0, flags=rt.FLAG_TIMING)
+    ctx = rt.Context(device=0, flags=rt.FLAG_TIMING | rt.FLAG_WIDE_BVH)
     ctx.set_scene(scene)
     ctx.set_camera(*rt.camera_reference(W, H))
     ctx.build()

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Small driver for rocprofv3 runs: builds the C5 scene once and runs a few
-builds + traces in the requested mode (env PROF_MODE = reference | nearest)."""
+builds + traces in the requested mode.  PROF_MODE is a '+'-joined list of
+reference | nearest | sort | packet | refill | wide | count (e.g. "nearest+packet")."""
 import os
 import sys
 
@@ -8,7 +9,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import raytracebvh_amd as rt  # noqa: E402
 
 mode = os.environ.get("PROF_MODE", "nearest")
-flags = rt.FLAG_NEAREST_FIRST if mode == "nearest" else rt.FLAG_SORT_BOUNCE
+names = {"reference": 0, "nearest": rt.FLAG_NEAREST_FIRST, "sort": rt.FLAG_SORT_BOUNCE,
+         "packet": rt.FLAG_PACKET_PRIMARY, "count": rt.FLAG_COUNT_VISITS, "refill": rt.FLAG_REFILL_BOUNCE,
+         "wide": rt.FLAG_WIDE_BVH}
+flags = 0
+for m in mode.split("+"):
+    flags |= names[m]
 scene = rt.synthetic(10_000_000, seed=0x5EED0005, half_extent=(100, 100, 50))
 W, H = 3840, 2160
 with rt.Context(device=0, flags=flags) as c:
@@ -17,4 +23,6 @@ with rt.Context(device=0, flags=flags) as c:
     for _ in range(int(os.environ.get("PROF_ITERS", "3"))):
         c.build()
         c.trace(W, H, 1)
+    if flags & rt.FLAG_COUNT_VISITS:
+        print(c.stats())
 print("done", mode)

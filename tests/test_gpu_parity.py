@@ -199,7 +199,10 @@ def test_build_10m_tree_properties():
 # ---------------------------------------------------------------- trace
 TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest": rt.FLAG_NEAREST_FIRST,
                "first_version": 1 << rt.FLAG_VARIANT_SHIFT, "packet": rt.FLAG_PACKET_PRIMARY,
-               "nearest+packet": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY}
+               "nearest+packet": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY,
+               "refill+sort": rt.FLAG_REFILL_BOUNCE | rt.FLAG_SORT_BOUNCE,
+               "nearest+packet+refill": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE,
+               "nearest+packet+wide": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH}
 
 
 def _trace_both(s, W, H, bounces, rows=None, flags=0):
@@ -253,7 +256,7 @@ def test_trace_c5_full_frame_modes_agree():
     oracle by the tests above; the oracle itself is too slow for 16M rays here)."""
     s = rt.synthetic(10_000_000, seed=0x5EED0005, half_extent=(100, 100, 50))
     W, H = 3840, 2160
-    with rt.Context(device=0) as c:
+    with rt.Context(device=0, flags=rt.FLAG_WIDE_BVH) as c:
         c.set_scene(s)
         c.set_camera(*rt.camera_reference(W, H))
         c.build()
@@ -264,6 +267,51 @@ def test_trace_c5_full_frame_modes_agree():
             frames[mode] = c.read_framebuffer()
     for mode, fb in frames.items():
         assert np.array_equal(fb, frames["reference"]), mode
+
+
+def test_wide_trace_needs_wide_build():
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(64, 64))
+        c.build()
+        c.set_flags(rt.FLAG_WIDE_BVH)
+        with pytest.raises(RuntimeError, match="WIDE_BVH"):
+            c.trace(64, 64, 1)
+
+
+def test_wide_view_records_match_binary_tree():
+    """inner4[2p + side] is the child-pair record of p's child on that side (a pseudo
+    record for a leaf child): checked against the exported binary tree."""
+    s = rt.synthetic(20_000, seed=7, half_extent=(30, 30, 20))
+    W, H = 320, 240
+    with rt.Context(device=0, flags=rt.FLAG_WIDE_BVH) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(W, H))
+        c.build()
+        nodes = c.read_bvh()
+        w4 = c.read_wide()
+    T = s.num_tris
+    assert w4.shape == (2 * (T - 1), 16)
+    f = w4.view(np.float32)
+    par = nodes["parent"]
+    for k in (x for x in range(2 * T - 1) if x != T):   # every node but the root (reference layout: root = T)
+        e = par[k] - T                       # parent internal index
+        side = 0 if nodes["child_l"][par[k]] == k else 1
+        rec = w4[2 * e + side]
+        if k < T:   # leaf
+            assert rec[12] == (0x80000000 | k) and rec[13] == 0xFFFFFFFF
+            np.testing.assert_array_equal(f[2 * e + side][0:3], nodes["bb_min"][k])
+            np.testing.assert_array_equal(f[2 * e + side][3:6], nodes["bb_max"][k])
+        else:
+            cl, cr = nodes["child_l"][k], nodes["child_r"][k]
+            ids = [(0x80000000 | x) if x < T else x - T for x in (cl, cr)]
+            assert list(rec[12:14]) == ids
+            np.testing.assert_array_equal(f[2 * e + side][0:3], nodes["bb_min"][cl])
+            np.testing.assert_array_equal(f[2 * e + side][3:6], nodes["bb_max"][cl])
+            np.testing.assert_array_equal(f[2 * e + side][6:9], nodes["bb_min"][cr])
+            np.testing.assert_array_equal(f[2 * e + side][9:12], nodes["bb_max"][cr])
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
