@@ -57,13 +57,14 @@ def make_scene(rt, wl):
     return rt.synthetic(wl["ntris"], seed=wl["seed"], half_extent=wl["half"])
 
 
-def trace_bytes(st, kernel, rays_in, rays_live_out):
-    """Algorithmic bytes of one launch (DESIGN.md "Byte model")."""
+def trace_bytes(st, kernel, rays_in, rays_live_out, wide=False):
+    """Algorithmic bytes of one launch (DESIGN.md "Byte model"); on the 4-wide view a
+    bounce internal visit reads one 128-B record pair."""
     if kernel == "k_primary":
         return (B_INTERNAL_VISIT * st["internal_visits"][0] + B_LEAF_VISIT * st["leaf_visits"][0]
                 + B_HIT_SHADE * st["hits"][0] + B_PRIMARY_OUT * rays_in + B_QUEUE * rays_live_out)
     if kernel == "k_bounce_trav":
-        return (B_INTERNAL_VISIT * st["internal_visits"][1] + B_LEAF_VISIT * st["leaf_visits"][1]
+        return ((2 if wide else 1) * B_INTERNAL_VISIT * st["internal_visits"][1] + B_LEAF_VISIT * st["leaf_visits"][1]
                 + (B_QUEUE + B_HIT_RECORD) * rays_in)
     # k_bounce_shade
     return ((B_QUEUE + B_HIT_RECORD + B_BOUNCE_RMW) * rays_in + B_HIT_SHADE * st["hits"][1]
@@ -167,6 +168,18 @@ def main():
              "mtris_s": scene.num_tris / (bst["ms_build"] * 1e-3) / 1e6,
              "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
                                    [round(x, 4) for x in bst["ms_stage"][:5]]))}
+    # the same build also writing the 4-wide traversal view (RTBVH_FLAG_WIDE_BVH); the
+    # context keeps this build, so every traversal mode below can run on it
+    ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_WIDE_BVH)
+    ctx.build()
+    ctx.reset_stats()
+    for _ in range(args.build_iters):
+        ctx.build(sync=False)
+    ctx.synchronize()
+    wst = ctx.stats()
+    build["with_wide_view"] = {"ms": round(wst["ms_build"], 4),
+                               "mtris_s": round(scene.num_tris / (wst["ms_build"] * 1e-3) / 1e6, 1),
+                               "refit_ms": round(wst["ms_stage"][4], 4)}
 
     # ---- band buffers + RCCL gather plumbing (raytracebvh_amd/tiles.py)
     from raytracebvh_amd.tiles import BandGather
@@ -203,23 +216,33 @@ def main():
         return dict(ms_step=ms, rays=rays, value=rays / (ms * 1e-3) / 1e6, stats=ctx.stats(),
                     band=band.clone())
 
-    # reference order (the exact findCollision DFS) and nearest-first; the nearest-first
-    # number is the headline only if its frame is bit-identical to the reference-order
-    # frame of this same run (checked on every rank's bands)
+    # reference order (the exact findCollision DFS), nearest-first, and nearest-first on the
+    # 4-wide view; a nearest-first number is the headline only if its frame is bit-identical
+    # to the reference-order frame of this same run (checked on every rank's bands), and the
+    # wide mode's build cost is the one reported under build.with_wide_view
     FAST = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE   # same results as the plain kernels (tests)
-    ref = timed(FAST)
-    near = timed(FAST | rt.FLAG_NEAREST_FIRST)
-    same = torch.tensor([0.0 if torch.equal(ref["band"], near["band"]) else 1.0], device=dev)
-    if world > 1:
-        dist.all_reduce(same)
-    identical = float(same.item()) == 0.0
-    use = near if (identical and args.traversal != "reference") else ref
-    mode_flags = FAST | (rt.FLAG_NEAREST_FIRST if use is near else 0)
+    modes = {"reference-order": FAST, "nearest-first": FAST | rt.FLAG_NEAREST_FIRST,
+             "nearest-first-wide": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH}
+    res = {m: timed(f) for m, f in modes.items()}
+    ref = res["reference-order"]
+    traversal = {"frames_identical": {}}
+    use_name = "reference-order"
+    for m, r in res.items():
+        traversal[m.replace("-", "_") + "_mrays_s"] = round(r["value"], 2)
+        traversal[m.replace("-", "_") + "_ms"] = round(r["ms_step"], 4)
+        if m == "reference-order":
+            continue
+        same = torch.tensor([0.0 if torch.equal(ref["band"], r["band"]) else 1.0], device=dev)
+        if world > 1:
+            dist.all_reduce(same)
+        ident = float(same.item()) == 0.0
+        traversal["frames_identical"][m] = ident
+        if ident and args.traversal != "reference" and r["ms_step"] < res[use_name]["ms_step"]:
+            use_name = m
+    use = res[use_name]
+    traversal["mode"] = use_name
+    mode_flags = modes[use_name]
     rays_per_step, ms_step, value, tst = use["rays"], use["ms_step"], use["value"], use["stats"]
-    traversal = {"mode": "nearest-first" if use is near else "reference-order",
-                 "frames_identical": identical,
-                 "reference_order_mrays_s": round(ref["value"], 2), "reference_order_ms": round(ref["ms_step"], 4),
-                 "nearest_first_mrays_s": round(near["value"], 2), "nearest_first_ms": round(near["ms_step"], 4)}
 
     # ---- visit counts for the byte model (one extra, untimed trace of this rank's bands)
     ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_COUNT_VISITS | mode_flags)
@@ -232,7 +255,8 @@ def main():
     live = cst["bounce_rays"]
     kern["k_primary"] = dict(ms=tst["ms_stage"][5], bytes=trace_bytes(cst, "k_primary", prim_rays, live))
     if bounces:   # 1 bounce: the queue's rays are traced once and none is re-emitted
-        kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7], bytes=trace_bytes(cst, "k_bounce_trav", live, 0))
+        kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7], bytes=trace_bytes(cst, "k_bounce_trav", live, 0,
+                                                                          wide=use_name.endswith("wide")))
         kern["k_bounce_shade"] = dict(ms=tst["ms_stage"][6] - tst["ms_stage"][7],
                                       bytes=trace_bytes(cst, "k_bounce_shade", live, 0))
     dom = max(kern, key=lambda k: kern[k]["ms"])

@@ -536,7 +536,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
     __shared__ uint32_t s_stk[WIDE || S == 0 ? 1 : S][BLOCK];
     uint32_t stack[WIDE ? 1 : STACK_SIZE - S];   // entries [S, STACK_SIZE)
-    uint2 wstack[WIDE ? STACK4 : 1];   // (node, entry distance bits)
+    constexpr int SW = WIDE ? S : 0;             // 4-wide: (node, entry distance) pairs in LDS
+    __shared__ uint2 s_wstk[SW == 0 ? 1 : SW][BLOCK];
+    uint2 wstack[WIDE ? STACK4 - SW : 1];        // entries [SW, STACK4)
     const uint32_t tid = threadIdx.x;
     auto spush = [&](uint32_t v) {
         if (sp < S) s_stk[sp][tid] = v;
@@ -545,6 +547,12 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     };
     auto spop_top = [&]() {   // --sp; refill the cached top from entry sp
         if (--sp >= 0) top = sp < S ? s_stk[sp][tid] : stack[sp - S];
+    };
+    auto wpush = [&](uint32_t id, float t) {
+        const uint2 e = make_uint2(id, __float_as_uint(t));
+        if (sp < SW) s_wstk[sp][tid] = e;
+        else wstack[sp - SW] = e;
+        ++sp;
     };
     bool drained = false;
     while (true) {
@@ -628,9 +636,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 c.overflow++;
                 done = true;
             } else {   // push the others farthest first
-                if (i3 != INVALID) wstack[sp++] = make_uint2(i3, __float_as_uint(k3));
-                if (i2 != INVALID) wstack[sp++] = make_uint2(i2, __float_as_uint(k2));
-                if (i1 != INVALID) wstack[sp++] = make_uint2(i1, __float_as_uint(k1));
+                if (i3 != INVALID) wpush(i3, k3);
+                if (i2 != INVALID) wpush(i2, k2);
+                if (i1 != INVALID) wpush(i1, k1);
             }
         } else {
             if (COUNT) c.internal++;
@@ -664,7 +672,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         }
         if (WIDE && !done && node == INVALID) {   // pop, dropping entries that cannot improve
             while (sp > 0) {
-                const uint2 e = wstack[--sp];
+                --sp;
+                const uint2 e = sp < SW ? s_wstk[sp][tid] : wstack[sp - SW];
                 if (!hit || __uint_as_float(e.y) <= best) {
                     node = e.x;
                     break;
@@ -792,7 +801,7 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
                           int mode, float2* hitrec, uint32_t* next, hipStream_t s) {
     const uint32_t blocks = 2048;   // persistent: 8 waves/SIMD x 1024 SIMDs / 4 waves per block
     if (mode == 2)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, 0>), dim3(blocks), dim3(BLOCK), 0, s, a.inner4, a.leaf, a.T, qin,
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), 0, s, a.inner4, a.leaf, a.T, qin,
                            qin_count, perm, hitrec, next, a.counters);
     else if (mode == 1)
         hipLaunchKernelGGL((k_bounce_trav<COUNT, 1, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T, qin,

@@ -32,9 +32,8 @@ def main():
     if os.environ.get("AB_SET") == "stack":   # LDS stack depth of the refill traversal
         base = rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
         V = rt.FLAG_VARIANT_SHIFT
-        variants = [("nearest+refill lds16", base), ("lds0", base | 2 << V), ("lds8", base | 3 << V),
-                    ("lds20", base | 4 << V), ("reference+refill lds16", rt.FLAG_REFILL_BOUNCE | rt.FLAG_PACKET_PRIMARY),
-                    ("reference+refill lds0", rt.FLAG_REFILL_BOUNCE | rt.FLAG_PACKET_PRIMARY | 2 << V)]
+        variants = [("nearest+refill lds16", base), ("lds20", base | 4 << V),
+                    ("nearest+wide lds8", base | rt.FLAG_WIDE_BVH), ("nearest+wide lds0", base | rt.FLAG_WIDE_BVH | 2 << V)]
     scene = rt.synthetic(ntris, seed=0x5EED0005, half_extent=(100, 100, 50))
     ctx = rt.Context(device=0, flags=rt.FLAG_TIMING | rt.FLAG_WIDE_BVH)
     ctx.set_scene(scene)
