@@ -28,16 +28,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# algorithmic bytes of OUR layout (DESIGN.md "Byte model"), per unit
-B_INTERNAL_VISIT = 64            # one 64-B child-pair record
-B_LEAF_VISIT = 48                # one 48-B clip-space triangle record
-B_HIT_SHADE = 16 + 48 + 12 + 96 + 4 + 68   # leaf tri id, clip triangle, 3 indices, 3 vertices, matIndex, material
-B_PRIMARY_OUT = 16               # color
-B_QUEUE = 32                     # one bounce-queue entry (write by primary, read by bounce)
-B_BOUNCE_RMW = 32                # color read + write
-B_HIT_RECORD = 8                 # (t, leaf) written by k_bounce_trav, read by k_bounce_shade
-B_BUILD_PER_TRI = 392            # DESIGN.md "Byte model": build kernels' algorithmic bytes per triangle
-
+# algorithmic bytes per unit, SURVEY.md §8(d) (the reference's data per unit of work)
+S_INT = 56                       # internal visit: children ids 8 B + two child AABBs 48 B
+S_LEAF = 120                     # leaf visit: ids 8 + index 4 + 3 indices 12 + 3 Vertex 96
+S_PRIMARY = 56                   # reflectRay record write per primary ray
+S_BOUNCE = 112                   # reflectRay record read + write per bounce ray
+S_HIT = 72                       # matIndex + Material per hit
+S_TEX = 16                       # texel per textured hit
+S_BUILD_PER_TRI = 348            # B_build: Morton 80 + sort 160 + Karras 24 + refit 84
 WORKLOADS = {
     "c5": dict(name="C5: synthetic 10M tris (seed 0x5EED0005, box 100x100x50), 3840x2160, primary+1 bounce",
                ntris=10_000_000, seed=0x5EED0005, half=(100.0, 100.0, 50.0), W=3840, H=2160, bounces=1),
@@ -57,27 +55,33 @@ def make_scene(rt, wl):
     return rt.synthetic(wl["ntris"], seed=wl["seed"], half_extent=wl["half"])
 
 
-def trace_bytes(st, kernel, rays_in, rays_live_out, wide=False):
-    """Algorithmic bytes of one launch (DESIGN.md "Byte model"); on the 4-wide view a
-    bounce internal visit reads one 128-B record pair."""
+def trace_bytes(st, kernel, wide=False):
+    """Algorithmic bytes of one launch: SURVEY §8(d) per-unit figures x the units that
+    launch processes (its own visit counts).  A 4-wide visit tests the four grandchild
+    boxes = two binary child-pair records (2 x S_INT)."""
     if kernel == "k_primary":
-        return (B_INTERNAL_VISIT * st["internal_visits"][0] + B_LEAF_VISIT * st["leaf_visits"][0]
-                + B_HIT_SHADE * st["hits"][0] + B_PRIMARY_OUT * rays_in + B_QUEUE * rays_live_out)
+        return (S_INT * st["internal_visits"][0] + S_LEAF * st["leaf_visits"][0] + S_PRIMARY * st["primary_rays"]
+                + S_HIT * st["hits"][0] + S_TEX * st["textured_hits"])
     if kernel == "k_bounce_trav":
-        return ((2 if wide else 1) * B_INTERNAL_VISIT * st["internal_visits"][1] + B_LEAF_VISIT * st["leaf_visits"][1]
-                + (B_QUEUE + B_HIT_RECORD) * rays_in)
+        return (2 if wide else 1) * S_INT * st["internal_visits"][1] + S_LEAF * st["leaf_visits"][1]
     # k_bounce_shade
-    return ((B_QUEUE + B_HIT_RECORD + B_BOUNCE_RMW) * rays_in + B_HIT_SHADE * st["hits"][1]
-            + B_QUEUE * rays_live_out)
+    return S_BOUNCE * st["bounce_rays"] + S_HIT * st["hits"][1]
 
 
-def load_pmc(workload, kernel):
-    path = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+def frame_bytes(st):
+    """SURVEY §8(d) frame bytes from REFERENCE-ORDER visit counts."""
+    return (S_INT * sum(st["internal_visits"]) + S_LEAF * sum(st["leaf_visits"]) + S_PRIMARY * st["primary_rays"]
+            + S_BOUNCE * st["bounce_rays"] + S_HIT * sum(st["hits"]) + S_TEX * st["textured_hits"])
+
+
+def load_pmc(workload, mode, kernel):
+    """Per-launch HBM bytes of `kernel` from the PMC passes of the same traversal mode
+    (profiles/pmc_<workload>_<mode>.json, written by scripts/make_pmc_json.py)."""
+    path = os.path.join(REPO, "profiles", f"pmc_{workload}_{mode}.json")
     if not os.path.exists(path):
         return None
     try:
-        d = json.load(open(path))
-        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+        return json.load(open(path))["kernels"][kernel]["hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -166,6 +170,7 @@ def main():
     bst = ctx.stats()
     build = {"workload": f"{scene.num_tris} tris (bench scene)", "ms": bst["ms_build"],
              "mtris_s": scene.num_tris / (bst["ms_build"] * 1e-3) / 1e6,
+             "achieved_gbs": round(S_BUILD_PER_TRI * scene.num_tris / (bst["ms_build"] * 1e-3) / 1e9, 1),
              "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
                                    [round(x, 4) for x in bst["ms_stage"][:5]]))}
     # the same build also writing the 4-wide traversal view (RTBVH_FLAG_WIDE_BVH); the
@@ -244,29 +249,39 @@ def main():
     mode_flags = modes[use_name]
     rays_per_step, ms_step, value, tst = use["rays"], use["ms_step"], use["value"], use["stats"]
 
-    # ---- visit counts for the byte model (one extra, untimed trace of this rank's bands)
-    ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_COUNT_VISITS | mode_flags)
-    ctx.reset_stats()
-    ctx.trace_band_async(W, H, bounces, rank, world, band.data_ptr())
-    cst = ctx.stats()
+    # ---- visit counts for the byte model (extra, untimed traces of this rank's bands):
+    # the chosen mode's own counts, and the reference-order counts of SURVEY §8(d)
+    def counts(flags):
+        ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_COUNT_VISITS | flags)
+        ctx.reset_stats()
+        ctx.trace_band_async(W, H, bounces, rank, world, band.data_ptr())
+        return ctx.stats()
+    cst = counts(mode_flags)
+    rst = counts(modes["reference-order"])
     ctx.set_flags(rt.FLAG_TIMING)
-    kern = {}
-    prim_rays = cst["primary_rays"]
-    live = cst["bounce_rays"]
-    kern["k_primary"] = dict(ms=tst["ms_stage"][5], bytes=trace_bytes(cst, "k_primary", prim_rays, live))
-    if bounces:   # 1 bounce: the queue's rays are traced once and none is re-emitted
-        kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7], bytes=trace_bytes(cst, "k_bounce_trav", live, 0,
-                                                                          wide=use_name.endswith("wide")))
+    kern = {"k_primary": dict(ms=tst["ms_stage"][5], bytes=trace_bytes(cst, "k_primary"))}
+    if bounces:   # 1 bounce: the first pass's traversal kernel has its own events
+        kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7],
+                                     bytes=trace_bytes(cst, "k_bounce_trav", wide=use_name.endswith("wide")))
         kern["k_bounce_shade"] = dict(ms=tst["ms_stage"][6] - tst["ms_stage"][7],
-                                      bytes=trace_bytes(cst, "k_bounce_shade", live, 0))
+                                      bytes=trace_bytes(cst, "k_bounce_shade"))
     dom = max(kern, key=lambda k: kern[k]["ms"])
     for k, v in kern.items():
         v["achieved_gbs"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
-    traffic = load_pmc(args.workload, dom)
+    traffic = load_pmc(args.workload, use_name, dom)
     roofline = {"bound": "hbm", "achieved": round(kern[dom]["achieved_gbs"], 1), "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": round(kern[dom]["achieved_gbs"] / PEAK_HBM_GBS, 4),
                 "traffic": traffic, "kernel": dom, "kernel_ms": round(kern[dom]["ms"], 4),
                 "algorithmic_bytes": int(kern[dom]["bytes"])}
+    fb = frame_bytes(rst)
+    # SURVEY 8(d)'s whole-frame figure prices the REFERENCE-ORDER walk's visits; a traversal
+    # that visits fewer nodes than that walk can exceed 1 here, so it is reported beside the
+    # per-kernel roofline above (own visits), not instead of it
+    frame_roofline = {"definition": "SURVEY 8(d): reference-order visit counts x per-unit bytes / trace time "
+                                    "(work-equivalent rate; not HBM traffic)",
+                      "bytes": int(fb), "trace_ms": round(tst["ms_trace"], 4),
+                      "achieved_gbs": round(fb / (tst["ms_trace"] * 1e-3) / 1e9, 1),
+                      "frac": round(fb / (tst["ms_trace"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
 
     result = None
     if rank == 0:
@@ -285,7 +300,7 @@ def main():
                 s4 = c.stats()
             extras["c4_build"] = {"mtris_s": round(10_000_000 / (s4["ms_build"] * 1e-3) / 1e6, 1),
                                   "ms": round(s4["ms_build"], 4),
-                                  "achieved_gbs": round(B_BUILD_PER_TRI * 1e7 / (s4["ms_build"] * 1e-3) / 1e9, 1),
+                                  "achieved_gbs": round(S_BUILD_PER_TRI * 1e7 / (s4["ms_build"] * 1e-3) / 1e9, 1),
                                   "stages_ms": [round(x, 4) for x in s4["ms_stage"][:5]]}
             del c4
             s3 = make_scene(rt, WORKLOADS["c3"])
@@ -320,7 +335,9 @@ def main():
             "roofline": roofline,
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kern.items()},
-            "visits": {"internal": cst["internal_visits"], "leaf": cst["leaf_visits"], "hits": cst["hits"]},
+            "visits": {"internal": cst["internal_visits"], "leaf": cst["leaf_visits"], "hits": cst["hits"],
+                       "reference_order_internal": rst["internal_visits"], "reference_order_leaf": rst["leaf_visits"]},
+            "frame_roofline": frame_roofline,
             "traversal": traversal,
             "build": build,
             "cpu_baseline": cpu,
