@@ -213,7 +213,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t vsel = (c->cfg.flags >> RTBVH_FLAG_VARIANT_SHIFT) & 15u;
     if (vsel == 1) variant = 2;
     int pvariant = variant;   // primary kernel: 2 = wave packets
-    if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1) pvariant = variant == 1 ? 4 : 3;
+
     const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
     const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && vsel != 1;
     if (wide && !c->wide_built)
@@ -222,6 +222,8 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     // A/B of the refill kernel's LDS stack depth: variant 2 -> none, 3 -> 8, 4 -> 20, else 16
     const int lds_stack = vsel == 2 ? 0 : vsel == 3 ? 8 : vsel == 4 ? 20 : 16;
     const int bmode = wide ? 2 : (variant == 1 ? 1 : 0);
+    if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1)
+        pvariant = wide ? 5 : (variant == 1 ? 4 : 3);
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
     launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, pvariant, s);
     if (timing) HIPC(c, hipEventRecord(ev[1], s));

@@ -29,6 +29,18 @@ constexpr uint32_t BLOCK = 256;
 constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
 
 struct Counts { uint32_t internal, leaf, overflow; };
+constexpr int STACK4 = 100;   // 4-wide walks: <= 3 pushes per level of a <= 32-level tree
+
+// Make loaded values live at this point, so the compiler issues every load of a
+// record together (one memory round trip) instead of sinking some of them below
+// an early-exit branch that needs only part of the record (ISA showed the leaf's
+// v0 fetched in a second dependent round trip after the determinant test).
+__device__ __forceinline__ void pin(float4& a) {
+    float x = a.x, y = a.y, z = a.z, w = a.w;
+    asm volatile("" : "+v"(x), "+v"(y), "+v"(z), "+v"(w));
+    a = make_float4(x, y, z, w);
+}
+__device__ __forceinline__ void pin(float& a) { asm volatile("" : "+v"(a)); }
 
 // rayTriangleCollision, RayTraceTraversal.hlsl:41-86, with edge1/edge2 precomputed
 // by the build (identical floats: the same single subtraction)
@@ -81,8 +93,9 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
             const float4* r = leaf + 4 * (size_t)j;
-            const float4 a = r[0], b = r[1];
-            const float e2z = r[2].x;
+            float4 a = r[0], b = r[1];
+            float e2z = r[2].x;
+            pin(a); pin(b); pin(e2z);
             if (COUNT) c.leaf++;
             const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
             if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < best_leaf))) {
@@ -141,8 +154,9 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
             const float4* r = leaf + 4 * (size_t)j;
-            const float4 a = r[0], b = r[1];
-            const float e2z = r[2].x;
+            float4 a = r[0], b = r[1];
+            float e2z = r[2].x;
+            pin(a); pin(b); pin(e2z);
             if (COUNT) c.leaf++;
             const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
             if (t != -1.f && (!hit || t < best)) {
@@ -283,12 +297,107 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
     return hit;
 }
 
+// ---- wave-packet traversal on the 4-wide view (primary rays) -------------------
+// As traverse_packet, but one step reads the 128-B record pair inner4[2p], inner4[2p+1]
+// (two s_load_dwordx16 of one line): the boxes of p's four grandchildren.  Children
+// are taken left to right (the left-first DFS's order LL, LR, RL, RR).  The per-lane
+// result is the (t, leaf) minimum, as for the 4-wide bounce walk.  A/B (C5): a
+// front-to-back order (box zmin: primary rays run along +z) made the per-lane visits
+// 6% fewer but lost the compiler's wave-uniform tracking of the node id and ran 1.6x
+// slower, so there is one order.
+template <bool COUNT>
+__device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
+                                                 uint32_t T, f3 o, f3 d, f3 inv, bool valid, float& best,
+                                                 uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*STACK4] */) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lanebit = 1ull << lane;
+    bool hit = false;
+    best = 0.f;
+    best_leaf = 0;
+    uint64_t mask = __ballot(valid);
+    int sp = 0;
+    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    if (mask == 0) return false;
+    uint32_t guard = 2 * T + 2;
+    while (true) {
+        if (--guard == 0) { c.overflow++; break; }
+        node = __builtin_amdgcn_readfirstlane(node);   // wave-uniform: keeps the record fetch on s_load
+        bool pop = false;
+        if (node & LEAF_BIT) {
+            const uint32_t j = node & ~LEAF_BIT;
+            const v16f q = sload16(leaf + 4 * (size_t)j);
+            if (mask & lanebit) {
+                if (COUNT) c.leaf++;
+                const float t = ray_triangle(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]));
+                if (t != -1.f && (!hit || t < best || (t == best && j < best_leaf))) {
+                    best = t;
+                    best_leaf = j;
+                    hit = true;
+                }
+            }
+            pop = true;
+        } else {
+            const v16f A = sload16(inner4 + 2 * (size_t)node);
+            const v16f B = sload16(inner4 + 2 * (size_t)node + 1);
+            uint32_t id[4] = {__float_as_uint(A[12]), __float_as_uint(A[13]), __float_as_uint(B[12]),
+                              __float_as_uint(B[13])};
+            bool h[4] = {false, false, false, false};
+            float t[4] = {0.f, 0.f, 0.f, 0.f};
+            if (mask & lanebit) {
+                if (COUNT) c.internal++;
+                h[0] = ray_box(o, inv, A[0], A[1], A[2], A[3], A[4], A[5], hit, best, t[0]);
+                h[1] = ray_box(o, inv, A[6], A[7], A[8], A[9], A[10], A[11], hit, best, t[1]) & (id[1] != INVALID);
+                h[2] = ray_box(o, inv, B[0], B[1], B[2], B[3], B[4], B[5], hit, best, t[2]);
+                h[3] = ray_box(o, inv, B[6], B[7], B[8], B[9], B[10], B[11], hit, best, t[3]) & (id[3] != INVALID);
+            }
+            uint64_t m[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) m[k] = __ballot(h[k]);
+            // children left to right (compile-time indices only: no private arrays)
+            const uint32_t* oi = id;
+            const uint64_t* om = m;
+            const int first = om[0] ? 0 : om[1] ? 1 : om[2] ? 2 : om[3] ? 3 : -1;
+            if (first < 0) {
+                pop = true;
+            } else if (sp + 3 > STACK4) {
+                c.overflow++;
+                pop = true;
+            } else {
+#pragma unroll
+                for (int k = 3; k >= 1; --k) {   // push the later children, farthest first
+                    if (k > first && om[k]) {
+                        if (lane == 0) {
+                            s_st[3 * sp] = oi[k];
+                            s_st[3 * sp + 1] = (uint32_t)om[k];
+                            s_st[3 * sp + 2] = (uint32_t)(om[k] >> 32);
+                        }
+                        ++sp;
+                    }
+                }
+                node = first == 0 ? oi[0] : first == 1 ? oi[1] : first == 2 ? oi[2] : oi[3];
+                mask = first == 0 ? om[0] : first == 1 ? om[1] : first == 2 ? om[2] : om[3];
+            }
+        }
+        if (pop) {
+            if (sp == 0) break;
+            --sp;
+            node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
+            mask = ((uint64_t)hi << 32) | lo;
+        }
+    }
+    return hit;
+}
+
 // kernel variants: 0 = reference order (default), 1 = nearest-first,
 // 2 = the first version (reference order) kept for A/B
 // 3 = reference order with wave-packet primary rays, 4 = nearest-first with packets
+// 5 = 4-wide packets (left-to-right order, (t, leaf) minimum)
 template <int V> struct TV {
     static constexpr bool NEAREST = (V == 1 || V == 4);
-    static constexpr bool PACKET = (V == 3 || V == 4);
+    static constexpr bool PACKET = (V == 3 || V == 4 || V == 5);
+    static constexpr bool WIDE = (V == 5);
     static constexpr int OCC = (V == 2) ? 1 : 8;   // 8 waves/SIMD => <= 64 VGPRs (A/B: -25% bounce time)
 };
 
@@ -387,7 +496,8 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
 template <bool COUNT, int V>
 __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ* __restrict__ q,
                                                                uint32_t* __restrict__ qcount, int emit) {
-    __shared__ uint32_t s_pst[TV<V>::PACKET ? 4 * 3 * STACK_SIZE : 1];
+    constexpr int PST = TV<V>::WIDE ? 3 * STACK4 : 3 * STACK_SIZE;   // per-wave packet stack words
+    __shared__ uint32_t s_pst[TV<V>::PACKET ? 4 * PST : 1];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t band = blockIdx.y * a.nranks + a.rank;
@@ -405,9 +515,12 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
     float best = 0.f;
     uint32_t bl = 0;
     bool phit = false;
-    if (TV<V>::PACKET)   // whole wave, before any divergence
+    if (TV<V>::WIDE)     // whole wave, before any divergence
+        phit = traverse_packet4<COUNT>(a.inner4, a.leaf, a.T, o, d, inv, valid, best, bl, c,
+                                                       s_pst + w * PST);
+    else if (TV<V>::PACKET)
         phit = traverse_packet<COUNT, TV<V>::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, best, bl, c,
-                                                      s_pst + w * 3 * STACK_SIZE);
+                                                      s_pst + w * PST);
     if (valid) {
         float4 color;
         float intensity = 0.f;
@@ -495,7 +608,6 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_bounce(TraceArgs a, const
 // shading runs afterwards as a plain one-thread-per-ray kernel (k_bounce_shade).
 // Per-lane traversal state and visit order are exactly those of traverse().
 constexpr uint32_t REFILL_MIN = 16;   // refill when at least this many lanes are idle
-constexpr int STACK4 = 100;           // 4-wide walk: <= 3 pushes per level of a <= 32-level tree
 
 // one nearest-first step on the 4-wide view (inner4): the four grandchild boxes of
 // binary node `node` come from one 128-B line; hit children are visited nearest
@@ -593,8 +705,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         } else if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
             const float4* rr = leaf + 4 * (size_t)j;
-            const float4 la = rr[0], lb = rr[1];
-            const float e2z = rr[2].x;
+            float4 la = rr[0], lb = rr[1];
+            float e2z = rr[2].x;
+            pin(la); pin(lb); pin(e2z);
             if (COUNT) c.leaf++;
             const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
             if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
@@ -618,9 +731,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             const uint4 b3 = reinterpret_cast<const uint4*>(rr)[7];
             float t0, t1, t2, t3;
             const bool h0 = ray_box(o, inv, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, hit, best, t0);
-            const bool h1 = a3.y != INVALID && ray_box(o, inv, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, hit, best, t1);
+            const bool h1 = ray_box(o, inv, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, hit, best, t1) & (a3.y != INVALID);
             const bool h2 = ray_box(o, inv, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, hit, best, t2);
-            const bool h3 = b3.y != INVALID && ray_box(o, inv, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, hit, best, t3);
+            const bool h3 = ray_box(o, inv, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, hit, best, t3) & (b3.y != INVALID);
             const float INF = __builtin_inff();
             float k0 = h0 ? t0 : INF, k1 = h1 ? t1 : INF, k2 = h2 ? t2 : INF, k3 = h3 ? t3 : INF;
             uint32_t i0 = h0 ? a3.x : INVALID, i1 = h1 ? a3.y : INVALID, i2 = h2 ? b3.x : INVALID,
@@ -819,6 +932,7 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
         case 2: count ? M(true, 2) : M(false, 2); break;  \
         case 3: count ? M(true, 3) : M(false, 3); break;  \
         case 4: count ? M(true, 4) : M(false, 4); break;  \
+        case 5: count ? M(true, 5) : M(false, 5); break;  \
         default: count ? M(true, 0) : M(false, 0); break; \
     }
 

@@ -34,6 +34,11 @@ def main():
         V = rt.FLAG_VARIANT_SHIFT
         variants = [("nearest+refill lds16", base), ("lds20", base | 4 << V),
                     ("nearest+wide lds8", base | rt.FLAG_WIDE_BVH), ("nearest+wide lds0", base | rt.FLAG_WIDE_BVH | 2 << V)]
+    if os.environ.get("AB_SET") == "wide":
+        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
+        variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),
+                    ("nearest+wide", base | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH),
+                    ("wide (left-to-right packets)", base | rt.FLAG_WIDE_BVH)]
     scene = rt.synthetic(ntris, seed=0x5EED0005, half_extent=(100, 100, 50))
     ctx = rt.Context(device=0, flags=rt.FLAG_TIMING | rt.FLAG_WIDE_BVH)
     ctx.set_scene(scene)
