@@ -221,6 +221,12 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool refill = ((c->cfg.flags & RTBVH_FLAG_REFILL_BOUNCE) != 0 || wide) && vsel != 1;
     // A/B of the refill kernel's LDS stack depth: variant 2 -> none, 3 -> 8, 4 -> 20, else 16
     const int lds_stack = vsel == 2 ? 0 : vsel == 3 ? 8 : vsel == 4 ? 20 : 16;
+    // ... and of the refill policy (idle lanes that trigger it, rays per atomic claim):
+    // 5 -> (16, none), 6 -> (8, 128), 7 -> (16, 128), 8 -> (8, 256), 9 -> (16, 64), 10 -> (4, 128);
+    // default (32, none)
+    const uint32_t refill_min = vsel == 5 ? 16 : vsel == 6 ? 8 : vsel == 7 ? 16 : vsel == 8 ? 8 : vsel == 9 ? 16
+                              : vsel == 10 ? 4 : 0;
+    const uint32_t chunk = vsel == 6 || vsel == 7 || vsel == 10 ? 128 : vsel == 8 ? 256 : vsel == 9 ? 64 : 0;
     const int bmode = wide ? 2 : (variant == 1 ? 1 : 0);
     if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1)
         pvariant = wide ? 5 : (variant == 1 ? 4 : 3);
@@ -237,7 +243,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (refill) {
             if (timing && b == 0) HIPC(c, hipEventRecord(ev[3], s));
             launch_bounce_traverse(a, c->d_q[b & 1], &c->d_qcount[b], perm, count, bmode, c->d_hit,
-                                   &c->d_qcount[16 + b], lds_stack, s);
+                                   &c->d_qcount[16 + b], lds_stack, refill_min, chunk, s);
             if (timing && b == 0) HIPC(c, hipEventRecord(ev[4], s));
             launch_bounce_shade(a, c->d_q[b & 1], &c->d_qcount[b], c->d_hit, c->d_q[(b + 1) & 1],
                                 &c->d_qcount[b + 1], count, b + 1 < bounces, P, s);

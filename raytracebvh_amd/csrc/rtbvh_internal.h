@@ -87,9 +87,11 @@ void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_coun
                    uint32_t* qout_count, bool count, bool emit, int variant, hipStream_t s);
 // bounce pass as persistent refill traversal (hit records) + shading kernel; `next` is a
 // zeroed work counter; mode 0 reference order, 1 nearest-first, 2 nearest-first on inner4;
-// lds_stack = stack entries kept in LDS (0, 8, 16, 20)
+// lds_stack = stack entries kept in LDS (0, 8, 16, 20); refill_min = idle lanes that trigger a
+// refill (0: default); chunk = rays one work-counter atomic claims for the wave (0: as many as idle)
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack, hipStream_t s);
+                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
+                            uint32_t refill_min, uint32_t chunk, hipStream_t s);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
 // coherence sort keys of a bounce queue: P entries (past *count: key 0xFFFFFFFF)

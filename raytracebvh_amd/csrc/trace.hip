@@ -607,7 +607,10 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_bounce(TraceArgs a, const
 // wave stays full; the finished ray's (t, leaf) goes to a hit record, and the
 // shading runs afterwards as a plain one-thread-per-ray kernel (k_bounce_shade).
 // Per-lane traversal state and visit order are exactly those of traverse().
-constexpr uint32_t REFILL_MIN = 16;   // refill when at least this many lanes are idle
+// default: refill when at least this many lanes are idle.  A/B on C5 (bounce pass):
+// 4 -> 15.6 ms, 8 -> 9.2, 16 -> 5.5, 24 -> 4.13, 32 -> 3.87, 40 -> 3.84, 48 -> 3.90,
+// 64 -> 5.36; claiming chunks of 64-256 rays per atomic at 4-16 idle lanes: 4.1-4.5
+constexpr uint32_t REFILL_MIN = 32;
 
 // one nearest-first step on the 4-wide view (inner4): the four grandchild boxes of
 // binary node `node` come from one 128-B line; hit children are visited nearest
@@ -636,7 +639,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                                                           const uint32_t* __restrict__ qin_count,
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
-                                                          unsigned long long* __restrict__ counters) {
+                                                          unsigned long long* __restrict__ counters,
+                                                          uint32_t refill_min, uint32_t chunk) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     const uint32_t n = *qin_count;
     const uint32_t lane = lane_id();
@@ -667,18 +671,28 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         ++sp;
     };
     bool drained = false;
+    // rays [cnext, cend) of the queue belong to this wave; with chunk > 0 one atomic
+    // claims `chunk` rays and later refills take from them without touching the
+    // global counter (chunks lost to the plain threshold in the A/B above: the tail
+    // of the last claimed chunks outweighs the saved atomics)
+    uint32_t cnext = 0, cend = 0;
     while (true) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (!drained && (nidle >= REFILL_MIN || nidle == 64)) {
+        if (!drained && (nidle >= refill_min || nidle == 64)) {
+            const uint32_t avail = cend - cnext;
             uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(next, nidle);
-            base = __shfl(base, 0, 64);
-            if (base + nidle >= n) drained = true;
+            const uint32_t want = chunk ? chunk : nidle;
+            if (avail < nidle) {
+                if (lane == 0) base = atomicAdd(next, want);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (base >= n) drained = true;
+            }
             if (!has) {
                 const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-                const uint32_t p = base + (uint32_t)__popcll(idle & lt);
-                if (p < n) {
+                const uint32_t k = (uint32_t)__popcll(idle & lt);
+                const uint32_t p = k < avail ? cnext + k : base + (k - avail);
+                if (p < n && (k < avail || !drained)) {
                     r = perm ? perm[p] : p;
                     const float4 q0 = reinterpret_cast<const float4*>(qin + r)[0];
                     const float4 q1 = reinterpret_cast<const float4*>(qin + r)[1];
@@ -695,19 +709,42 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                     guard = 2 * T + 2;
                 }
             }
+            if (avail >= nidle) {
+                cnext += nidle;
+            } else if (!drained) {
+                cnext = base + (nidle - avail);
+                cend = base + want;
+                if (cnext >= n) drained = true;   // nothing left after these
+            } else {
+                cnext = cend;
+            }
         }
-        if (__ballot(has) == 0) break;   // queue drained and every lane done
+        // every refill either hands out a ray or moves toward `drained`, so a wave with no
+        // ray left loops back to refill until the queue is drained
+        if (__ballot(has) == 0 && drained) break;
         if (!has) continue;
         bool done = false;
+        // one fetch for every active lane, leaf or internal, before the branch: a wave
+        // holding both kinds would otherwise wait for two dependent round trips
+        // (leaf and child-pair records are both 64-B aligned records of 64 B; the
+        // 4-wide record pair adds a second 64 B for internal lanes)
+        const bool isleaf = (node & LEAF_BIT) != 0;
+        const float4* rr = isleaf ? leaf + 4 * (size_t)(node & ~LEAF_BIT)
+                                  : reinterpret_cast<const float4*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
+        float4 q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
+        float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f), q5 = q4, q6 = q4, q7 = q4;
+        if (WIDE && !isleaf) {
+            q4 = rr[4]; q5 = rr[5]; q6 = rr[6]; q7 = rr[7];
+        }
+        pin(q0); pin(q1); pin(q2); pin(q3);
+        if (WIDE) { pin(q4); pin(q5); pin(q6); pin(q7); }
         if (--guard == 0) {
             c.overflow++;
             done = true;
-        } else if (node & LEAF_BIT) {
+        } else if (isleaf) {
             const uint32_t j = node & ~LEAF_BIT;
-            const float4* rr = leaf + 4 * (size_t)j;
-            float4 la = rr[0], lb = rr[1];
-            float e2z = rr[2].x;
-            pin(la); pin(lb); pin(e2z);
+            const float4 la = q0, lb = q1;
+            const float e2z = q2.x;
             if (COUNT) c.leaf++;
             const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
             if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
@@ -724,11 +761,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             }
         } else if (WIDE) {
             if (COUNT) c.internal++;
-            const float4* rr = reinterpret_cast<const float4*>(inner + 2 * (size_t)node);
-            const float4 a0 = rr[0], a1 = rr[1], a2 = rr[2];
-            const uint4 a3 = reinterpret_cast<const uint4*>(rr)[3];
-            const float4 b0 = rr[4], b1 = rr[5], b2 = rr[6];
-            const uint4 b3 = reinterpret_cast<const uint4*>(rr)[7];
+            const float4 a0 = q0, a1 = q1, a2 = q2, b0 = q4, b1 = q5, b2 = q6;
+            const uint4 a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
+            const uint4 b3 = make_uint4(__float_as_uint(q7.x), __float_as_uint(q7.y), 0u, 0u);
             float t0, t1, t2, t3;
             const bool h0 = ray_box(o, inv, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, hit, best, t0);
             const bool h1 = ray_box(o, inv, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, hit, best, t1) & (a3.y != INVALID);
@@ -755,9 +790,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             }
         } else {
             if (COUNT) c.internal++;
-            const float4* rr = reinterpret_cast<const float4*>(inner + node);
-            const float4 q0 = rr[0], q1 = rr[1], q2 = rr[2];
-            const uint4 q3 = reinterpret_cast<const uint4*>(rr)[3];
+            const uint32_t cl = __float_as_uint(q3.x), cr = __float_as_uint(q3.y);
             float tl, tr;
             const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
             const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
@@ -775,11 +808,11 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                         done = sp == -1;
                     } else {
                         spush(top);                     // push the second child
-                        top = swap ? q3.x : q3.y;
-                        node = swap ? q3.y : q3.x;
+                        top = swap ? cl : cr;
+                        node = swap ? cr : cl;
                     }
                 } else {
-                    node = lh ? q3.x : q3.y;
+                    node = lh ? cl : cr;
                 }
             }
         }
@@ -911,17 +944,18 @@ void launch_bounce_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_co
 
 template <bool COUNT, int S>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                          int mode, float2* hitrec, uint32_t* next, hipStream_t s) {
+                          int mode, float2* hitrec, uint32_t* next, uint32_t refill_min, uint32_t chunk,
+                          hipStream_t s) {
     const uint32_t blocks = 2048;   // persistent: 8 waves/SIMD x 1024 SIMDs / 4 waves per block
     if (mode == 2)
         hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), 0, s, a.inner4, a.leaf, a.T, qin,
-                           qin_count, perm, hitrec, next, a.counters);
+                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk);
     else if (mode == 1)
         hipLaunchKernelGGL((k_bounce_trav<COUNT, 1, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T, qin,
-                           qin_count, perm, hitrec, next, a.counters);
+                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk);
     else
         hipLaunchKernelGGL((k_bounce_trav<COUNT, 0, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T,
-                           qin, qin_count, perm, hitrec, next, a.counters);
+                           qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk);
 }
 
 }  // namespace
@@ -959,10 +993,12 @@ void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, 
 }
 
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack, hipStream_t s) {
-#define RTBVH_TRAV(S)                                                                                 \
-    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, s) \
-           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, s))
+                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
+                            uint32_t refill_min, uint32_t chunk, hipStream_t s) {
+    if (refill_min == 0) refill_min = REFILL_MIN;
+#define RTBVH_TRAV(S)                                                                                        \
+    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, s) \
+           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, s))
     switch (lds_stack) {
         case 0: RTBVH_TRAV(0); break;
         case 8: RTBVH_TRAV(8); break;

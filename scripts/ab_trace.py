@@ -34,6 +34,12 @@ def main():
         V = rt.FLAG_VARIANT_SHIFT
         variants = [("nearest+refill lds16", base), ("lds20", base | 4 << V),
                     ("nearest+wide lds8", base | rt.FLAG_WIDE_BVH), ("nearest+wide lds0", base | rt.FLAG_WIDE_BVH | 2 << V)]
+    if os.environ.get("AB_SET") == "refill":   # idle lanes that trigger a refill
+        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+        V = rt.FLAG_VARIANT_SHIFT
+        variants = [("wide refill32", base), ("refill16", base | 5 << V), ("thr8 chunk128", base | 6 << V), ("thr16 chunk128", base | 7 << V),
+                    ("thr8 chunk256", base | 8 << V), ("thr16 chunk64", base | 9 << V), ("thr4 chunk128", base | 10 << V),
+                    ("binary nearest thr8 chunk128", base & ~rt.FLAG_WIDE_BVH | 6 << V)]
     if os.environ.get("AB_SET") == "wide":
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
         variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),
