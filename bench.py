@@ -273,6 +273,12 @@ def main():
                 "unit": "GB/s", "frac": round(kern[dom]["achieved_gbs"] / PEAK_HBM_GBS, 4),
                 "traffic": traffic, "kernel": dom, "kernel_ms": round(kern[dom]["ms"], 4),
                 "algorithmic_bytes": int(kern[dom]["bytes"])}
+    if traffic:
+        # the algorithmic bytes are node/leaf bytes per visit; the upper tree levels stay in
+        # L2, so the measured HBM rate (PMC bytes of the same kernel) is the second number
+        tg = traffic / (kern[dom]["ms"] * 1e-3) / 1e9
+        roofline.update({"traffic_gbs": round(tg, 1), "traffic_frac": round(tg / PEAK_HBM_GBS, 4),
+                         "cache_served_frac": round(max(0.0, 1.0 - traffic / kern[dom]["bytes"]), 4)})
     fb = frame_bytes(rst)
     # SURVEY 8(d)'s whole-frame figure prices the REFERENCE-ORDER walk's visits; a traversal
     # that visits fewer nodes than that walk can exceed 1 here, so it is reported beside the
