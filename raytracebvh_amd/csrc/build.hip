@@ -182,6 +182,8 @@ __device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t
     const uint32_t l = (uint32_t)loc, r = (uint32_t)(loc + 1);
     inner[i].child_l = left_leaf ? (LEAF_BIT | l) : l;
     inner[i].child_r = right_leaf ? (LEAF_BIT | r) : r;
+    inner[i].range_lo = (uint32_t)(I < bound_start ? I : bound_start);
+    inner[i].range_hi = (uint32_t)(I > bound_start ? I : bound_start);
     if (left_leaf) pleaf[l] = i << 1; else pint[l] = i << 1;
     if (right_leaf) pleaf[r] = (i << 1) | 1u; else pint[r] = (i << 1) | 1u;
 }
@@ -246,22 +248,9 @@ __device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
     hi = mk(__uint_as_float((uint32_t)(b >> 32)), __uint_as_float((uint32_t)c), __uint_as_float((uint32_t)(c >> 32)));
 }
 
-// 4-wide traversal view: the complete child-pair record of node p also goes to
-// inner4[2 * parent(p) + side(p)], so the records of two siblings share one 128-B
-// line (one HBM request fetches both; the traversal tests the four grandchild
-// boxes of a node at once).  Leaf children get a pseudo-record {leaf box, -, leaf, INVALID}.
-__device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
-                                             uint32_t cr) {
-    float4* d = reinterpret_cast<float4*>(dst);
-    d[0] = make_float4(lmin.x, lmin.y, lmin.z, lmax.x);
-    d[1] = make_float4(lmax.y, lmax.z, rmin.x, rmin.y);
-    d[2] = make_float4(rmin.z, rmax.x, rmax.y, rmax.z);
-    d[3] = make_float4(__uint_as_float(cl), __uint_as_float(cr), 0.f, 0.f);
-}
-
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __restrict__ inner,
                                             const uint32_t* __restrict__ pint, uint32_t* __restrict__ cnt,
-                                            float* __restrict__ rootbox, Inner* __restrict__ inner4) {
+                                            float* __restrict__ rootbox) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
@@ -274,11 +263,6 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
         f3 smin, smax;
         ld_box_sc1(side ? inner[p].lmin : inner[p].rmin, smin, smax);
         e = pint[p];
-        if (inner4 && e != INVALID) {
-            const uint2 ids = *reinterpret_cast<const uint2*>(&inner[p].child_l);
-            if (side) store_record(inner4 + 2 * (size_t)(e >> 1) + (e & 1u), smin, smax, lo, hi, ids.x, ids.y);
-            else      store_record(inner4 + 2 * (size_t)(e >> 1) + (e & 1u), lo, hi, smin, smax, ids.x, ids.y);
-        }
         // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
         if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
         else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
@@ -290,20 +274,92 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
     }
 }
 
+// Block-local refit: the workgroup of leaves [a, a + BLOCK) joins every internal node
+// whose leaf range lies inside that block through LDS (ticket + both child boxes), so
+// only nodes whose range crosses a block boundary -- about log2(T / BLOCK) per leaf
+// path's top -- use the global sc1 hand-off of refit_climb.  Both children of a node
+// are climbed by threads of the same block exactly when the node's range is inside
+// the block, so a node takes one protocol for both of its arrivals.  The boxes still
+// go to the node's 64-B record in HBM (plain stores: read by later kernels only).
 __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    __shared__ uint32_t s_cnt[BLOCK];
+    __shared__ float s_box[BLOCK][2][6];
+    const uint32_t base = blockIdx.x * BLOCK;
+    const uint32_t i = base + threadIdx.x;
+    s_cnt[threadIdx.x] = 0;
+    __syncthreads();
     if (i >= a.T) return;
     const float4* r = a.leaf + 4 * (size_t)i;
     const float4 b0 = r[2], b1 = r[3];
-    const f3 lo = mk(b0.z, b0.w, b1.x), hi = mk(b1.y, b1.z, b1.w);
+    f3 lo = mk(b0.z, b0.w, b1.x), hi = mk(b1.y, b1.z, b1.w);
     if (a.T == 1) {
         a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
         a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
         return;
     }
-    const uint32_t e = a.pleaf[i];
-    if (a.inner4) store_record(a.inner4 + 2 * (size_t)(e >> 1) + (e & 1u), lo, hi, lo, hi, LEAF_BIT | i, INVALID);
-    refit_climb(lo, hi, e, a.inner, a.pint, a.refit_cnt, a.rootbox, a.inner4);
+    uint32_t e = a.pleaf[i];
+    const uint32_t end = base + BLOCK;
+    for (int level = 0; level < 2 * STACK_SIZE; level++) {
+        const uint32_t p = e >> 1, side = e & 1u;
+        const uint4 q3 = reinterpret_cast<const uint4*>(&a.inner[p])[3];   // ids, range
+        const uint32_t pe = a.pint[p];
+        if (!(p >= base && p < end && q3.z >= base && q3.w < end)) {      // leaves the block
+            refit_climb(lo, hi, e, a.inner, a.pint, a.refit_cnt, a.rootbox);
+            return;
+        }
+        float* own = side ? a.inner[p].rmin : a.inner[p].lmin;
+        own[0] = lo.x; own[1] = lo.y; own[2] = lo.z; own[3] = hi.x; own[4] = hi.y; own[5] = hi.z;
+        float* sb = s_box[p - base][side];
+        sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the LDS box lands before the ticket
+        const uint32_t old = atomicAdd(&s_cnt[p - base], 1u);
+        if (old == 0) return;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const float* ob = s_box[p - base][side ^ 1u];
+        const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
+        // union in (childL, childR) order, as the reference
+        if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
+        else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
+        e = pe;
+        if (e == INVALID) {
+            a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
+            a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+            return;
+        }
+    }
+}
+
+// 4-wide traversal view, after refit: thread p gathers the 64-B records of p's two
+// children (a pseudo-record {box, box, leaf, INVALID} for a leaf child) and writes
+// them as one 128-B line, inner4[2p] and inner4[2p+1].  A/B on C5: writing the same
+// records from inside the refit climb (scattered 64-B stores) cost 0.73 ms.
+__global__ __launch_bounds__(BLOCK) void k_wide_view(BuildArgs a) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p + 1 >= a.T) return;
+    const uint4 ids = reinterpret_cast<const uint4*>(&a.inner[p])[3];
+    float4 out[8];
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+        const uint32_t cid = side ? ids.y : ids.x;
+        if (cid & LEAF_BIT) {
+            const float4* r = a.leaf + 4 * (size_t)(cid & ~LEAF_BIT);
+            const float4 b0 = r[2], b1 = r[3];   // {.., .., bmin.xy}, {bmin.z, bmax.xyz}
+            out[4 * side + 0] = make_float4(b0.z, b0.w, b1.x, b1.y);
+            out[4 * side + 1] = make_float4(b1.z, b1.w, b0.z, b0.w);
+            out[4 * side + 2] = make_float4(b1.x, b1.y, b1.z, b1.w);
+            out[4 * side + 3] = make_float4(__uint_as_float(cid), __uint_as_float(INVALID), 0.f, 0.f);
+        } else {
+            const float4* r = reinterpret_cast<const float4*>(a.inner + cid);
+            out[4 * side + 0] = r[0];
+            out[4 * side + 1] = r[1];
+            out[4 * side + 2] = r[2];
+            const float4 q = r[3];
+            out[4 * side + 3] = make_float4(q.x, q.y, 0.f, 0.f);
+        }
+    }
+    float4* dst = reinterpret_cast<float4*>(a.inner4 + 2 * (size_t)p);
+#pragma unroll
+    for (int k = 0; k < 8; k++) dst[k] = out[k];
 }
 
 __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
@@ -315,7 +371,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
         for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
         return;
     }
-    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox, nullptr);
+    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox);
 }
 
 // reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k
@@ -375,6 +431,7 @@ void launch_leaf_karras(const BuildArgs& a, hipStream_t s) {
 }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    if (a.inner4 && a.T > 1) hipLaunchKernelGGL(k_wide_view, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
 }
 void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
     hipLaunchKernelGGL(k_export, dim3(blocks_for(2 * (size_t)a.T - 1)), dim3(BLOCK), 0, s, a, (RefNode*)out);

@@ -25,7 +25,7 @@ struct alignas(64) Inner {
     float lmin[3], lmax[3];
     float rmin[3], rmax[3];
     uint32_t child_l, child_r;
-    uint32_t pad0, pad1;
+    uint32_t range_lo, range_hi;   // sorted-leaf range [lo, hi] of node k (build only; refit locality)
 };
 static_assert(sizeof(Inner) == 64, "Inner must be one 64-B record");
 
