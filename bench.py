@@ -173,18 +173,6 @@ def main():
              "achieved_gbs": round(S_BUILD_PER_TRI * scene.num_tris / (bst["ms_build"] * 1e-3) / 1e9, 1),
              "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
                                    [round(x, 4) for x in bst["ms_stage"][:5]]))}
-    # the same build also writing the 4-wide traversal view (RTBVH_FLAG_WIDE_BVH); the
-    # context keeps this build, so every traversal mode below can run on it
-    ctx.set_flags(rt.FLAG_TIMING | rt.FLAG_WIDE_BVH)
-    ctx.build()
-    ctx.reset_stats()
-    for _ in range(args.build_iters):
-        ctx.build(sync=False)
-    ctx.synchronize()
-    wst = ctx.stats()
-    build["with_wide_view"] = {"ms": round(wst["ms_build"], 4),
-                               "mtris_s": round(scene.num_tris / (wst["ms_build"] * 1e-3) / 1e6, 1),
-                               "refit_ms": round(wst["ms_stage"][4], 4)}
 
     # ---- band buffers + RCCL gather plumbing (raytracebvh_amd/tiles.py)
     from raytracebvh_amd.tiles import BandGather
@@ -224,7 +212,7 @@ def main():
     # reference order (the exact findCollision DFS), nearest-first, and nearest-first on the
     # 4-wide view; a nearest-first number is the headline only if its frame is bit-identical
     # to the reference-order frame of this same run (checked on every rank's bands), and the
-    # wide mode's build cost is the one reported under build.with_wide_view
+    # build above serves all three (one node layout)
     FAST = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE   # same results as the plain kernels (tests)
     modes = {"reference-order": FAST, "nearest-first": FAST | rt.FLAG_NEAREST_FIRST,
              "nearest-first-wide": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH}

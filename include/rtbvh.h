@@ -107,9 +107,9 @@ enum {
                                              visit sequence, same results) */
     RTBVH_FLAG_REFILL_BOUNCE = 1u << 6,   /* bounce rays: persistent traversal whose lanes take a new
                                              ray as soon as theirs is done, then a shading pass */
-    RTBVH_FLAG_WIDE_BVH = 1u << 7,        /* build: also write the 4-wide view (sibling records paired in
-                                             128-B lines); trace: bounce rays walk it nearest-first
-                                             (lexicographic (t, leaf) minimum, as NEAREST_FIRST) */
+    RTBVH_FLAG_WIDE_BVH = 1u << 7,        /* trace: walk the node records 4-wide (a node's four grandchild
+                                             boxes share one 128-B line), keeping the lexicographic
+                                             (t, leaf) minimum as NEAREST_FIRST does */
     /* bits 8..11: kernel variant for A/B measurement (0 = default, 1 = first version) */
     RTBVH_FLAG_VARIANT_SHIFT = 8
 };
@@ -191,10 +191,11 @@ rtbvh_status rtbvh_read_intensity(rtbvh_ctx* ctx, float* intensity);
 const float* rtbvh_framebuffer_device(rtbvh_ctx* ctx);
 /* BVHTree UAV u0 in the reference layout (2n-1 nodes, see rtbvh_node). */
 rtbvh_status rtbvh_read_bvh(rtbvh_ctx* ctx, rtbvh_node* out, uint32_t capacity);
-/* 4-wide traversal view (RTBVH_FLAG_WIDE_BVH builds): 2(n-1) records of 16 u32 each,
+/* Node records in slots (the layout both traversal walks read): 2(n-1) records of 16 u32,
  * record 2p+side = {box of child c's left child (min xyz, max xyz), box of its right child,
- * id_l, id_r, 0, 0} for c = child `side` of internal node p; ids: internal k, or
- * 0x80000000|j for sorted leaf j; a leaf child c gives {its box, its box, 0x80000000|c, ~0u}. */
+ * id_l, id_r, c, 0} for c = child `side` of internal node p; ids: internal k, or
+ * 0x80000000|j for sorted leaf j; a leaf child c gives {its box, its box, 0x80000000|c, ~0u,
+ * 0x80000000|c, 0}.  (The root's record follows at slot 2(n-1).) */
 rtbvh_status rtbvh_read_wide(rtbvh_ctx* ctx, uint32_t* records, uint64_t capacity);
 /* Per-triangle Morton codes in triangle order (MortonCodes.hlsl:104-112). */
 rtbvh_status rtbvh_read_morton(rtbvh_ctx* ctx, uint32_t* codes);

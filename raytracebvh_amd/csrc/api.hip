@@ -35,9 +35,7 @@ struct rtbvh_ctx {
     uint32_t* d_sort_scratch = nullptr;
     float4 *d_tclip = nullptr, *d_leaf = nullptr;
     Inner* d_inner = nullptr;
-    Inner* d_inner4 = nullptr;               // 4-wide traversal view, built with RTBVH_FLAG_WIDE_BVH
-    uint32_t cap_T4 = 0;
-    bool wide_built = false;
+    Inner* d_rec = nullptr;                  // node records in slots (rtbvh_device.h), 2T-1
     uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr;
     float* d_bounds = nullptr;
     float* d_rootbox = nullptr;
@@ -110,6 +108,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_tclip, 3 * n));
     HIPC(c, dalloc(c->d_leaf, 4 * n));
     HIPC(c, dalloc(c->d_inner, ni));
+    HIPC(c, dalloc(c->d_rec, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
     HIPC(c, dalloc(c->d_cnt, ni));
@@ -158,6 +157,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.sorted_vals = c->sorted.vals;
     a.leaf = c->d_leaf;
     a.inner = c->d_inner;
+    a.rec = c->d_rec;
     a.pleaf = c->d_pleaf;
     a.pint = c->d_pint;
     a.refit_cnt = c->d_cnt;
@@ -167,8 +167,8 @@ BuildArgs build_args(rtbvh_ctx* c) {
 
 TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks, float4* color, float* inten) {
     TraceArgs a{};
-    a.inner = c->d_inner;
-    a.inner4 = c->d_inner4;
+    a.inner = c->d_rec;
+    a.inner4 = c->d_rec;
     a.leaf = c->d_leaf;
     a.tclip = c->d_tclip;
     a.verts = c->d_verts;
@@ -216,8 +216,6 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
 
     const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
     const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && vsel != 1;
-    if (wide && !c->wide_built)
-        return fail(c, RTBVH_ERR_NOT_READY, "RTBVH_FLAG_WIDE_BVH trace needs a build made with that flag set");
     const bool refill = ((c->cfg.flags & RTBVH_FLAG_REFILL_BOUNCE) != 0 || wide) && vsel != 1;
     // A/B of the refill kernel's LDS stack depth: variant 2 -> none, 3 -> 8, 4 -> 20, else 16
     const int lds_stack = vsel == 2 ? 0 : vsel == 3 ? 8 : vsel == 4 ? 20 : 16;
@@ -335,7 +333,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_inner4);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_rec);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
@@ -413,12 +411,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     hipStream_t s = c->stream;
     const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0;
     BuildArgs a = build_args(c);
-    const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && c->T > 1;
-    if (wide && c->cap_T4 < c->T) {
-        HIPC(c, dalloc(c->d_inner4, 2 * (size_t)(c->T - 1)));
-        c->cap_T4 = c->T;
-    }
-    a.inner4 = wide ? c->d_inner4 : nullptr;
     hipEvent_t* ev = c->evb[c->n_builds % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (c->cfg.morton_mode == RTBVH_MORTON_CPUTESTS) {
@@ -439,7 +431,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (timing) HIPC(c, hipEventRecord(ev[5], s));
     if (timing) c->n_builds++;
     c->built = true;
-    c->wide_built = wide || c->T == 1;
     return check_launch(c, "build kernels");
 }
 
@@ -542,12 +533,12 @@ rtbvh_status rtbvh_read_bvh(rtbvh_ctx* c, rtbvh_node* out, uint32_t capacity) {
 
 rtbvh_status rtbvh_read_wide(rtbvh_ctx* c, uint32_t* out, uint64_t capacity) {
     if (!c || !out) return RTBVH_ERR_INVALID_ARG;
-    if (!c->built || !c->wide_built) return fail(c, RTBVH_ERR_NOT_READY, "no RTBVH_FLAG_WIDE_BVH build yet");
+    if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "no build yet");
     const size_t total = c->T > 1 ? 2 * (size_t)(c->T - 1) : 0;
     if (capacity < total) return fail(c, RTBVH_ERR_INVALID_ARG, "read_wide: capacity < 2(n-1)");
     HIPC(c, hipSetDevice(c->cfg.device));
     HIPC(c, hipStreamSynchronize(c->stream));
-    if (total) HIPC(c, hipMemcpy(out, c->d_inner4, total * sizeof(Inner), hipMemcpyDeviceToHost));
+    if (total) HIPC(c, hipMemcpy(out, c->d_rec, total * sizeof(Inner), hipMemcpyDeviceToHost));
     return RTBVH_OK;
 }
 

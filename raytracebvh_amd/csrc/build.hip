@@ -182,8 +182,8 @@ __device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t
     const uint32_t l = (uint32_t)loc, r = (uint32_t)(loc + 1);
     inner[i].child_l = left_leaf ? (LEAF_BIT | l) : l;
     inner[i].child_r = right_leaf ? (LEAF_BIT | r) : r;
-    inner[i].range_lo = (uint32_t)(I < bound_start ? I : bound_start);
-    inner[i].range_hi = (uint32_t)(I > bound_start ? I : bound_start);
+    inner[i].aux0 = (uint32_t)(I < bound_start ? I : bound_start);   // leaf range of node i
+    inner[i].aux1 = (uint32_t)(I > bound_start ? I : bound_start);
     if (left_leaf) pleaf[l] = i << 1; else pint[l] = i << 1;
     if (right_leaf) pleaf[r] = (i << 1) | 1u; else pint[r] = (i << 1) | 1u;
 }
@@ -248,9 +248,22 @@ __device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
     hi = mk(__uint_as_float((uint32_t)(b >> 32)), __uint_as_float((uint32_t)c), __uint_as_float((uint32_t)(c >> 32)));
 }
 
+// the complete record of node p: its children's boxes (left, right), their ids, p itself
+__device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
+                                             uint32_t cr, uint32_t own) {
+    float4* d = reinterpret_cast<float4*>(dst);
+    d[0] = make_float4(lmin.x, lmin.y, lmin.z, lmax.x);
+    d[1] = make_float4(lmax.y, lmax.z, rmin.x, rmin.y);
+    d[2] = make_float4(rmin.z, rmax.x, rmax.y, rmax.z);
+    d[3] = make_float4(__uint_as_float(cl), __uint_as_float(cr), __uint_as_float(own), 0.f);
+}
+__device__ __forceinline__ uint32_t slot_of(uint32_t parent_code, uint32_t T) {
+    return parent_code == INVALID ? 2 * T - 2 : parent_code;
+}
+
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __restrict__ inner,
                                             const uint32_t* __restrict__ pint, uint32_t* __restrict__ cnt,
-                                            float* __restrict__ rootbox) {
+                                            float* __restrict__ rootbox, Inner* __restrict__ rec, uint32_t T) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
@@ -263,6 +276,9 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
         f3 smin, smax;
         ld_box_sc1(side ? inner[p].lmin : inner[p].rmin, smin, smax);
         e = pint[p];
+        const uint2 ids = *reinterpret_cast<const uint2*>(&inner[p].child_l);
+        if (side) store_record(rec + slot_of(e, T), smin, smax, lo, hi, ids.x, ids.y, p);
+        else      store_record(rec + slot_of(e, T), lo, hi, smin, smax, ids.x, ids.y, p);
         // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
         if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
         else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
@@ -298,17 +314,16 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
         return;
     }
     uint32_t e = a.pleaf[i];
+    store_record(a.rec + e, lo, hi, lo, hi, LEAF_BIT | i, INVALID, LEAF_BIT | i);   // leaf pseudo-record
     const uint32_t end = base + BLOCK;
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
-        const uint4 q3 = reinterpret_cast<const uint4*>(&a.inner[p])[3];   // ids, range
+        const uint4 q3 = reinterpret_cast<const uint4*>(&a.inner[p])[3];   // ids, leaf range
         const uint32_t pe = a.pint[p];
         if (!(p >= base && p < end && q3.z >= base && q3.w < end)) {      // leaves the block
-            refit_climb(lo, hi, e, a.inner, a.pint, a.refit_cnt, a.rootbox);
+            refit_climb(lo, hi, e, a.inner, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
             return;
         }
-        float* own = side ? a.inner[p].rmin : a.inner[p].lmin;
-        own[0] = lo.x; own[1] = lo.y; own[2] = lo.z; own[3] = hi.x; own[4] = hi.y; own[5] = hi.z;
         float* sb = s_box[p - base][side];
         sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the LDS box lands before the ticket
@@ -317,6 +332,8 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const float* ob = s_box[p - base][side ^ 1u];
         const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
+        if (side) store_record(a.rec + slot_of(pe, a.T), smin, smax, lo, hi, q3.x, q3.y, p);
+        else      store_record(a.rec + slot_of(pe, a.T), lo, hi, smin, smax, q3.x, q3.y, p);
         // union in (childL, childR) order, as the reference
         if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
         else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
@@ -329,39 +346,6 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
     }
 }
 
-// 4-wide traversal view, after refit: thread p gathers the 64-B records of p's two
-// children (a pseudo-record {box, box, leaf, INVALID} for a leaf child) and writes
-// them as one 128-B line, inner4[2p] and inner4[2p+1].  A/B on C5: writing the same
-// records from inside the refit climb (scattered 64-B stores) cost 0.73 ms.
-__global__ __launch_bounds__(BLOCK) void k_wide_view(BuildArgs a) {
-    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
-    if (p + 1 >= a.T) return;
-    const uint4 ids = reinterpret_cast<const uint4*>(&a.inner[p])[3];
-    float4 out[8];
-#pragma unroll
-    for (int side = 0; side < 2; side++) {
-        const uint32_t cid = side ? ids.y : ids.x;
-        if (cid & LEAF_BIT) {
-            const float4* r = a.leaf + 4 * (size_t)(cid & ~LEAF_BIT);
-            const float4 b0 = r[2], b1 = r[3];   // {.., .., bmin.xy}, {bmin.z, bmax.xyz}
-            out[4 * side + 0] = make_float4(b0.z, b0.w, b1.x, b1.y);
-            out[4 * side + 1] = make_float4(b1.z, b1.w, b0.z, b0.w);
-            out[4 * side + 2] = make_float4(b1.x, b1.y, b1.z, b1.w);
-            out[4 * side + 3] = make_float4(__uint_as_float(cid), __uint_as_float(INVALID), 0.f, 0.f);
-        } else {
-            const float4* r = reinterpret_cast<const float4*>(a.inner + cid);
-            out[4 * side + 0] = r[0];
-            out[4 * side + 1] = r[1];
-            out[4 * side + 2] = r[2];
-            const float4 q = r[3];
-            out[4 * side + 3] = make_float4(q.x, q.y, 0.f, 0.f);
-        }
-    }
-    float4* dst = reinterpret_cast<float4*>(a.inner4 + 2 * (size_t)p);
-#pragma unroll
-    for (int k = 0; k < 8; k++) dst[k] = out[k];
-}
-
 __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= a.T) return;
@@ -371,7 +355,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
         for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
         return;
     }
-    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox);
+    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
 }
 
 // reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k
@@ -405,7 +389,8 @@ __global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restri
         box = a.rootbox;
     } else {
         o.parent = (e >> 1) + T;
-        box = (e & 1u) ? a.inner[e >> 1].rmin : a.inner[e >> 1].lmin;
+        const Inner& pr = a.rec[slot_of(a.pint[e >> 1], T)];   // the parent's record
+        box = (e & 1u) ? pr.rmin : pr.lmin;
     }
     for (int k = 0; k < 3; k++) { o.bb_min[k] = box[k]; o.bb_max[k] = box[3 + k]; }
     out[r] = o;
@@ -431,7 +416,6 @@ void launch_leaf_karras(const BuildArgs& a, hipStream_t s) {
 }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
-    if (a.inner4 && a.T > 1) hipLaunchKernelGGL(k_wide_view, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
 }
 void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
     hipLaunchKernelGGL(k_export, dim3(blocks_for(2 * (size_t)a.T - 1)), dim3(BLOCK), 0, s, a, (RefNode*)out);

@@ -7,9 +7,17 @@
 //   keys/vals u32[T] x2  radix ping-pong (Morton code, triangle id)
 //   leaf   float4[4*T]   64-B leaf records in SORTED order: {v0.xyz, e1.x}, {e1.yz, e2.xy},
 //                        {e2.z, tri, bmin.xy}, {bmin.z, bmax.xyz}; e1 = v1-v0, e2 = v2-v0
-//   inner  Inner[T-1]    64-B child-pair records; internal node k, root = 0
+//   rec    Inner[2T-1]   64-B node records in SLOTS: the record of internal node k (the boxes
+//                        and ids of its two children, and k itself) sits at slot
+//                        pint[k] = 2*parent + side, the root's at slot 2T-2; slot pleaf[j]
+//                        holds a pseudo-record {box_j, box_j, LEAF_BIT|j, INVALID} for leaf j.
+//                        So the records of two siblings share one 128-B line: the binary
+//                        walks step to slot 2k+side, the 4-wide walks read slots 2k, 2k+1
+//                        (the four grandchild boxes of k) in one line.
+//   inner  Inner[T-1]    build scratch indexed by node: Karras ids + leaf range, and the
+//                        box hand-off of refit nodes that span workgroups
 //   pleaf  u32[T], pint u32[T-1]   parent<<1 | side (side 0 = left child)
-// Node ids inside kernels: internal k -> k, leaf j -> LEAF_BIT | j.
+// Node ids: internal k -> k, leaf j -> LEAF_BIT | j.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,7 +33,7 @@ struct alignas(64) Inner {
     float lmin[3], lmax[3];
     float rmin[3], rmax[3];
     uint32_t child_l, child_r;
-    uint32_t range_lo, range_hi;   // sorted-leaf range [lo, hi] of node k (build only; refit locality)
+    uint32_t aux0, aux1;   // rec: aux0 = own node index; scratch: sorted-leaf range [aux0, aux1]
 };
 static_assert(sizeof(Inner) == 64, "Inner must be one 64-B record");
 

@@ -45,9 +45,8 @@ struct BuildArgs {
     const uint32_t* sorted_keys;  // [T]
     const uint32_t* sorted_vals;  // [T]
     float4* leaf;             // [4T] 64-B sorted leaf records
-    Inner* inner;             // [T-1]
-    Inner* inner4;            // [2(T-1)] 4-wide traversal records (RTBVH_FLAG_WIDE_BVH) or null:
-                              // inner4[2p + side] = child-pair record of p's child on that side
+    Inner* inner;             // [T-1] build scratch (Karras ids + ranges, refit hand-off)
+    Inner* rec;               // [2T-1] node records in slots (rtbvh_device.h)
     uint32_t* pleaf;          // [T]
     uint32_t* pint;           // [T-1]
     uint32_t* refit_cnt;      // [T-1]
@@ -64,8 +63,8 @@ void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t 
 
 // ---- trace (trace.hip) ------------------------------------------------------
 struct TraceArgs {
-    const Inner* inner;
-    const Inner* inner4;      // 4-wide view (see BuildArgs::inner4) or null
+    const Inner* inner;       // node records in slots (BuildArgs::rec); the 4-wide walks read the same array
+    const Inner* inner4;      // == inner
     const float4* leaf;       // [4T] sorted leaf records (see build.hip)
     const float4* tclip;      // [3T] clip-space triangles in triangle order (hit shading)
     const float* verts;       // rtbvh_vertex AoS, 8 floats each

@@ -29,6 +29,14 @@ constexpr uint32_t BLOCK = 256;
 constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
 
 struct Counts { uint32_t internal, leaf, overflow; };
+
+// Node records live in SLOTS (rtbvh_device.h): the binary walks keep slots on their
+// stacks.  The record of internal node k holds k's own index, so its internal
+// children's records are at slots 2k and 2k+1; a leaf child is LEAF_BIT | j.
+__device__ __forceinline__ uint32_t child_slot(uint32_t id, uint32_t own, uint32_t side) {
+    return (id & LEAF_BIT) ? id : 2 * own + side;
+}
+__device__ __forceinline__ uint32_t root_slot(uint32_t T) { return T == 1 ? LEAF_BIT : 2 * T - 2; }
 constexpr int STACK4 = 100;   // 4-wide walks: <= 3 pushes per level of a <= 32-level tree
 
 // Make loaded values live at this point, so the compiler issues every load of a
@@ -86,7 +94,7 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
     uint32_t stack[STACK_SIZE];   // reference entries [0, sp) below the cached top
     int sp = 0;                   // reference stack index; stack[0] is the sentinel = top at start
     uint32_t top = INVALID;
-    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    uint32_t node = root_slot(T);
     uint32_t guard = 2 * T + 2;   // a valid tree is walked in <= 2T-1 steps
     do {
         if (--guard == 0) { c.overflow++; break; }
@@ -111,6 +119,7 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
         const float4* r = reinterpret_cast<const float4*>(inner + node);
         const float4 q0 = r[0], q1 = r[1], q2 = r[2];
         const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
+        const uint32_t cl = child_slot(q3.x, q3.z, 0), cr = child_slot(q3.y, q3.z, 1);
         float tl, tr;
         const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
         const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
@@ -127,9 +136,9 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
                     continue;
                 }
                 stack[sp++] = top;                      // push the second child
-                top = swap ? q3.x : q3.y;
+                top = swap ? cl : cr;
             }
-            node = swap ? q3.y : (lh ? q3.x : q3.y);
+            node = swap ? cr : (lh ? cl : cr);
         }
     } while (sp != -1);
     return hit;
@@ -147,7 +156,7 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
     uint32_t stack[STACK_SIZE];
     int sp = 0;
     stack[0] = INVALID;
-    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    uint32_t node = root_slot(T);
     uint32_t guard = 2 * T + 2;
     do {
         if (--guard == 0) { c.overflow++; break; }
@@ -171,6 +180,7 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
         const float4* r = reinterpret_cast<const float4*>(inner + node);
         const float4 q0 = r[0], q1 = r[1], q2 = r[2];
         const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
+        const uint32_t cl = child_slot(q3.x, q3.z, 0), cr = child_slot(q3.y, q3.z, 1);
         float tl, tr;
         const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
         const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
@@ -179,9 +189,9 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
         } else {
             if (lh && rh) {
                 if (sp + 1 >= STACK_SIZE) { c.overflow++; node = stack[sp--]; continue; }
-                stack[++sp] = q3.y;
+                stack[++sp] = cr;
             }
-            node = lh ? q3.x : q3.y;
+            node = lh ? cl : cr;
         }
     } while (sp != -1);
     return hit;
@@ -222,7 +232,7 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
     best_leaf = 0;
     uint64_t mask = __ballot(valid);
     int sp = 0;                      // entries on the wave stack; the top one is cached below
-    uint32_t node = (T == 1) ? LEAF_BIT : 0u, top_node = 0;
+    uint32_t node = root_slot(T), top_node = 0;
     uint64_t top_mask = 0;
     if (mask == 0) return false;
     uint32_t guard = 2 * T + 2;
@@ -244,7 +254,8 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
             pop = true;
         } else {
             const v16f q = sload16(inner + node);
-            const uint32_t cl = __float_as_uint(q[12]), cr = __float_as_uint(q[13]);
+            const uint32_t own = __float_as_uint(q[14]);
+            const uint32_t cl = child_slot(__float_as_uint(q[12]), own, 0), cr = child_slot(__float_as_uint(q[13]), own, 1);
             bool lh = false, rh = false;
             float tl = 0.f, tr = 0.f;
             if (mask & lanebit) {
@@ -705,7 +716,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                     bl = 0;
                     sp = 0;
                     top = INVALID;
-                    node = (T == 1) ? LEAF_BIT : 0u;
+                    node = WIDE ? ((T == 1) ? LEAF_BIT : 0u) : root_slot(T);
                     guard = 2 * T + 2;
                 }
             }
@@ -790,7 +801,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             }
         } else {
             if (COUNT) c.internal++;
-            const uint32_t cl = __float_as_uint(q3.x), cr = __float_as_uint(q3.y);
+            const uint32_t own = __float_as_uint(q3.z);
+            const uint32_t cl = child_slot(__float_as_uint(q3.x), own, 0), cr = child_slot(__float_as_uint(q3.y), own, 1);
             float tl, tr;
             const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
             const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);

@@ -115,7 +115,7 @@ class Context:
         return out
 
     def read_wide(self) -> np.ndarray:
-        """4-wide traversal view of a FLAG_WIDE_BVH build: (2(n-1), 16) uint32 records."""
+        """Node records in slots (both walks' layout): (2(n-1), 16) uint32 records, see rtbvh_read_wide."""
         out = np.zeros((max(2 * (self.num_tris - 1), 0), 16), np.uint32)
         self._check(_L.lib().rtbvh_read_wide(self._h, _L.ptr(out), len(out)))
         return out

@@ -270,21 +270,26 @@ def test_trace_c5_full_frame_modes_agree():
         assert np.array_equal(fb, frames["reference"]), mode
 
 
-def test_wide_trace_needs_wide_build():
+def test_wide_trace_on_any_build():
+    """One node layout serves both walks: a build made without the wide flag traces
+    with FLAG_WIDE_BVH to the same frame as the binary walk."""
     d = load_scene_fixture("Test")
     s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
     with rt.Context(device=0) as c:
         c.set_scene(s)
-        c.set_camera(*rt.camera_reference(64, 64))
+        c.set_camera(*rt.camera_reference(320, 240))
         c.build()
-        c.set_flags(rt.FLAG_WIDE_BVH)
-        with pytest.raises(RuntimeError, match="WIDE_BVH"):
-            c.trace(64, 64, 1)
+        c.trace(320, 240, 1)
+        ref = c.read_framebuffer()
+        c.set_flags(rt.FLAG_WIDE_BVH | rt.FLAG_PACKET_PRIMARY)
+        c.trace(320, 240, 1)
+        assert np.array_equal(c.read_framebuffer(), ref)
 
 
 def test_wide_view_records_match_binary_tree():
-    """inner4[2p + side] is the child-pair record of p's child on that side (a pseudo
-    record for a leaf child): checked against the exported binary tree."""
+    """Slot 2p + side holds the record of p's child on that side (its children's boxes
+    and ids, and its own index; a pseudo record for a leaf child): checked against the
+    exported binary tree."""
     s = rt.synthetic(20_000, seed=7, half_extent=(30, 30, 20))
     W, H = 320, 240
     with rt.Context(device=0, flags=rt.FLAG_WIDE_BVH) as c:
@@ -302,13 +307,13 @@ def test_wide_view_records_match_binary_tree():
         side = 0 if nodes["child_l"][par[k]] == k else 1
         rec = w4[2 * e + side]
         if k < T:   # leaf
-            assert rec[12] == (0x80000000 | k) and rec[13] == 0xFFFFFFFF
+            assert rec[12] == (0x80000000 | k) and rec[13] == 0xFFFFFFFF and rec[14] == (0x80000000 | k)
             np.testing.assert_array_equal(f[2 * e + side][0:3], nodes["bb_min"][k])
             np.testing.assert_array_equal(f[2 * e + side][3:6], nodes["bb_max"][k])
         else:
             cl, cr = nodes["child_l"][k], nodes["child_r"][k]
             ids = [(0x80000000 | x) if x < T else x - T for x in (cl, cr)]
-            assert list(rec[12:14]) == ids
+            assert list(rec[12:15]) == ids + [k - T]
             np.testing.assert_array_equal(f[2 * e + side][0:3], nodes["bb_min"][cl])
             np.testing.assert_array_equal(f[2 * e + side][3:6], nodes["bb_max"][cl])
             np.testing.assert_array_equal(f[2 * e + side][6:9], nodes["bb_min"][cr])
