@@ -7,6 +7,11 @@ distribution), each rank traces its bands into a compact buffer
 (rtbvh_trace_band_async), and rank 0 gathers the buffers over torch.distributed
 ("nccl" = RCCL over xGMI on MI355X; "gloo" in the CPU tests) and scatters the rows
 into the frame.  The only collective of the path is that gather.
+
+Frames in flight: with `nbuf=2` the band buffer of frame i+1 is a different buffer
+than frame i's, so frame i's gather (on the collective's own stream) runs while
+frame i+1 is traced; `assemble(i)` makes the compute stream wait for gather i before
+the buffer is traced into again.
 """
 from __future__ import annotations
 
@@ -19,36 +24,54 @@ def band_row_ids(H: int, rank: int, nranks: int) -> list:
 
 
 class BandGather:
-    """Band buffer of this rank and, on rank 0, the assembled frame."""
+    """Band buffer(s) of this rank and, on rank 0, the assembled frame."""
 
-    def __init__(self, W: int, H: int, rank: int, world: int, device, dtype=None):
+    def __init__(self, W: int, H: int, rank: int, world: int, device, dtype=None, nbuf: int = 1):
         import torch
 
         dtype = dtype or torch.float32
         self.W, self.H, self.rank, self.world = W, H, rank, world
+        self.nbuf = nbuf if world > 1 else 1
         self.rows = [len(band_row_ids(H, r, world)) for r in range(world)]
         self.max_rows = max(self.rows)
         # every rank sends a buffer of the same (max) size: dist.gather needs equal shapes
-        self.band = torch.zeros((self.max_rows, W, 4), dtype=dtype, device=device)
+        self.bands = [torch.zeros((self.max_rows, W, 4), dtype=dtype, device=device) for _ in range(self.nbuf)]
+        self.band = self.bands[0]
         self.frame = None
-        self.gather_list = None
+        self.gather_lists = None
         self.row_idx = None
         if world == 1:
             self.frame = self.band
         elif rank == 0:
             self.frame = torch.empty((H, W, 4), dtype=dtype, device=device)
-            self.gather_list = [torch.empty_like(self.band) for _ in range(world)]
+            self.gather_lists = [[torch.empty_like(self.band) for _ in range(world)] for _ in range(self.nbuf)]
             self.row_idx = [torch.tensor(band_row_ids(H, r, world), dtype=torch.long, device=device)
                             for r in range(world)]
 
-    def gather(self):
-        """Collect every rank's bands on rank 0 and assemble the frame there."""
+    def band_buffer(self, i: int):
+        """The buffer frame i is traced into."""
+        return self.bands[i % self.nbuf]
+
+    def gather_async(self, i: int):
+        """Start gathering frame i's bands to rank 0; returns a handle for assemble()."""
         if self.world == 1:
-            return self.frame
+            return None
         import torch.distributed as dist
 
-        dist.gather(self.band, self.gather_list if self.rank == 0 else None, dst=0)
+        k = i % self.nbuf
+        return dist.gather(self.bands[k], self.gather_lists[k] if self.rank == 0 else None, dst=0, async_op=True)
+
+    def assemble(self, i: int, handle):
+        """Wait (on the stream) for gather i and, on rank 0, scatter its rows into the frame."""
+        if self.world == 1:
+            return self.frame
+        handle.wait()
         if self.rank == 0:
+            gl = self.gather_lists[i % self.nbuf]
             for r in range(self.world):
-                self.frame.index_copy_(0, self.row_idx[r], self.gather_list[r][: self.rows[r]])
+                self.frame.index_copy_(0, self.row_idx[r], gl[r][: self.rows[r]])
         return self.frame
+
+    def gather(self, i: int = 0):
+        """Collect frame i's bands on rank 0 and assemble the frame there (synchronous)."""
+        return self.assemble(i, self.gather_async(i))
