@@ -95,7 +95,9 @@ enum {
 enum {
     RTBVH_FLAG_TIMING = 1u << 0,         /* record per-stage hipEvent times (rtbvh_get_stats) */
     RTBVH_FLAG_COUNT_VISITS = 1u << 1,   /* count traversal visits (slower; for the byte model) */
-    RTBVH_FLAG_REFRACT_RECORDS = 1u << 2, /* also build refractRay records (RayTraceLaunch.hlsl:70-80) */
+    RTBVH_FLAG_REFRACT_RECORDS = 1u << 2, /* keep the reflectRay and refractRay RayPresent records
+                                             (RayTraceLaunch.hlsl:48-80, RayTraceReflection.hlsl:24-55)
+                                             for rtbvh_read_rays */
     RTBVH_FLAG_SORT_BOUNCE = 1u << 3,     /* sort live bounce rays by (octant, origin Morton) before
                                              tracing them: same results, better coherence for the
                                              reference-order traversal */
@@ -201,7 +203,9 @@ rtbvh_status rtbvh_read_wide(rtbvh_ctx* ctx, uint32_t* records, uint64_t capacit
 rtbvh_status rtbvh_read_morton(rtbvh_ctx* ctx, uint32_t* codes);
 /* Stable radix order: sorted codes and the triangle id of each sorted position. */
 rtbvh_status rtbvh_read_sorted(rtbvh_ctx* ctx, uint32_t* sorted_codes, uint32_t* tri_ids);
-/* refractRay records (RTBVH_FLAG_REFRACT_RECORDS) and reflectRay records of the last trace. */
+/* reflectRay (after the last pass) and refractRay records of the last trace, one per traced
+ * pixel in framebuffer order; needs RTBVH_FLAG_REFRACT_RECORDS at trace time.  Ray fields
+ * HLSL leaves unset (a hit whose intensity is 0) are 0.  Either pointer may be NULL. */
 rtbvh_status rtbvh_read_rays(rtbvh_ctx* ctx, rtbvh_ray_present* reflect_out, rtbvh_ray_present* refract_out);
 rtbvh_status rtbvh_get_stats(rtbvh_ctx* ctx, rtbvh_stats* out);
 /* Restart the timing averages of rtbvh_get_stats. */

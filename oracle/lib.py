@@ -66,6 +66,8 @@ def lib():
         L.orc_trace.argtypes = [ctypes.POINTER(_Scene), u32p, ctypes.c_uint32, u32p, u32p,
                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
+        L.orc_trace_ex.restype = ctypes.c_int
+        L.orc_trace_ex.argtypes = L.orc_trace.argtypes + [u32p, u32p]
         L.orc_camera_reference.argtypes = [ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]
         L.orc_fnv1a64.restype = ctypes.c_uint64
         L.orc_fnv1a64.argtypes = [u32p, ctypes.c_uint64]
@@ -170,7 +172,9 @@ def build(scene: Scene, wvp, morton_mode=MORTON_CPUTESTS, delta_mode=DELTA_CLZ64
 
 
 def trace(scene: Scene, nodes: np.ndarray, wvp, wv, W, H, bounces, row_begin=0, row_end=None,
-          row_step=1, want_intensity=False):
+          row_step=1, want_intensity=False, want_records=False):
+    """Oracle frame (rgba, intensity, stats); with want_records also the reflectRay and
+    refractRay RayPresent records as (rows, W, 14) float32 (orc_trace_ex)."""
     n = scene.num_tris
     if row_end is None:
         row_end = H
@@ -181,14 +185,19 @@ def trace(scene: Scene, nodes: np.ndarray, wvp, wv, W, H, bounces, row_begin=0, 
     wvp = np.ascontiguousarray(wvp, dtype=np.float32)
     wv = np.ascontiguousarray(wv, dtype=np.float32)
     nodes = np.ascontiguousarray(nodes)
-    rc = lib().orc_trace(ctypes.byref(scene.c), ctypes.c_void_p(nodes.ctypes.data), n, _p(wvp), _p(wv),
-                         W, H, bounces, row_begin, row_end, row_step, _p(rgba),
-                         _p(inten) if inten is not None else None, _p(counters))
+    refl = np.zeros((rows, W, 14), dtype=np.float32) if want_records else None
+    refr = np.zeros((rows, W, 14), dtype=np.float32) if want_records else None
+    rc = lib().orc_trace_ex(ctypes.byref(scene.c), ctypes.c_void_p(nodes.ctypes.data), n, _p(wvp), _p(wv),
+                            W, H, bounces, row_begin, row_end, row_step, _p(rgba),
+                            _p(inten) if inten is not None else None, _p(counters),
+                            _p(refl) if refl is not None else None, _p(refr) if refr is not None else None)
     if rc != 0:
         raise RuntimeError(f"orc_trace failed ({rc})")
     keys = ["primary", "bounce", "internal_visits", "leaf_visits", "hits", "textured_hits",
             "stack_overflows", "max_stack"]
     stats = {k: int(v) for k, v in zip(keys, counters)}
+    if want_records:
+        return rgba, inten, stats, refl, refr
     return rgba, inten, stats
 
 

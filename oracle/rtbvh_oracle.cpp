@@ -493,6 +493,32 @@ inline Ray make_ray(f3 o, f3 d) {
     return r;
 }
 
+// HLSL refract(i, n, eta) as the intrinsic is documented: cosi = dot(-i, n),
+// cost2 = 1 - eta*eta*(1 - cosi*cosi), t = eta*i + (eta*cosi - sqrt(|cost2|))*n,
+// result t * (cost2 > 0).  Used by RayTraceLaunch.hlsl:76-78 (parity unpinned:
+// no reference test covers refraction).
+inline f3 refract_hlsl(f3 i, f3 n, float eta) {
+    const float cosi = dot(mk(-i.x, -i.y, -i.z), n);
+    const float cost2 = 1.0f - eta * eta * (1.0f - cosi * cosi);
+    const float s = eta * cosi - sqrtf(fabsf(cost2));
+    const f3 t = add(mul(i, eta), mul(n, s));
+    const float keep = cost2 > 0.0f ? 1.0f : 0.0f;
+    return mul(t, keep);
+}
+
+// RayPresent (RayTraceGlobal.hlsl:30-35): intensity, origin, direction, invDirection, color
+inline void put_record(float* r, float intensity, const Ray* ray, f4 color) {
+    r[0] = intensity;
+    if (ray) {
+        r[1] = ray->o.x; r[2] = ray->o.y; r[3] = ray->o.z;
+        r[4] = ray->d.x; r[5] = ray->d.y; r[6] = ray->d.z;
+        r[7] = ray->inv.x; r[8] = ray->inv.y; r[9] = ray->inv.z;
+    } else {
+        for (int k = 1; k < 10; k++) r[k] = 0.f;
+    }
+    r[10] = color.x; r[11] = color.y; r[12] = color.z; r[13] = color.w;
+}
+
 }  // namespace
 
 extern "C" {
@@ -501,6 +527,14 @@ int orc_trace(const orc_scene* s, const orc_node* nodes, uint32_t n, const float
               const float wv[16], uint32_t W, uint32_t H, uint32_t bounces, uint32_t row_begin,
               uint32_t row_end, uint32_t row_step, float* rgba, float* intensity_out,
               uint64_t* counters) {
+    return orc_trace_ex(s, nodes, n, wvp, wv, W, H, bounces, row_begin, row_end, row_step, rgba, intensity_out,
+                        counters, nullptr, nullptr);
+}
+
+int orc_trace_ex(const orc_scene* s, const orc_node* nodes, uint32_t n, const float wvp[16],
+                 const float wv[16], uint32_t W, uint32_t H, uint32_t bounces, uint32_t row_begin,
+                 uint32_t row_end, uint32_t row_step, float* rgba, float* intensity_out,
+                 uint64_t* counters, float* refl_rec, float* refr_rec) {
     if (n == 0 || row_step == 0) return 1;
     uint64_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const float hw = (float)(W >> 1), hh = (float)(H >> 1);
@@ -516,6 +550,8 @@ int orc_trace(const orc_scene* s, const orc_node* nodes, uint32_t n, const float
             f4 color;
             float intensity;
             Ray bray;
+            bool have_bray = false;
+            const size_t o = (size_t)out_row * W + x;
             if (h.hit) {
                 cnt[4]++;
                 f3 hit = add(ray.o, mul(ray.d, h.dist));                          // getHitLoc :15-19
@@ -527,11 +563,20 @@ int orc_trace(const orc_scene* s, const orc_node* nodes, uint32_t n, const float
                 bool tx;
                 color = shade(c, h.tri, uv, &tx);
                 cnt[5] += tx;
-                if (intensity != 0)
+                if (intensity != 0) {
                     bray = make_ray(add(hit, mul(nrm, .001f)), normalize(reflect(ray.d, nrm)));  // :61-67
+                    have_bray = true;
+                }
+                if (refr_rec) {   // :70-80; the ray stays zero when the intensity is 0 (unset in HLSL)
+                    const float ri = (1.f - m.alpha) * 1;
+                    Ray rr;
+                    if (ri != 0) rr = make_ray(sub(hit, mul(nrm, .001f)), normalize(refract_hlsl(ray.d, nrm, m.optical_density)));
+                    put_record(refr_rec + 14 * o, ri, ri != 0 ? &rr : nullptr, mk4(1.f, 1.f, 1.f, 1.f));
+                }
             } else {
                 color = mk4(.5f, .5f, .5f, 1.f);                                   // :85 clearRayPresent
                 intensity = 0;
+                if (refr_rec) put_record(refr_rec + 14 * o, 0.f, nullptr, color);
             }
             // RayTraceReflection.hlsl:17-60, `bounces` passes (Graphics.cpp:795)
             for (uint32_t b = 0; b < bounces && 0 < intensity; b++) {
@@ -551,13 +596,14 @@ int orc_trace(const orc_scene* s, const orc_node* nodes, uint32_t n, const float
                                 lerpf(color.z, sc.z, intensity), lerpf(color.w, sc.w, intensity));
                     intensity *= m.shininess / 1000.f * 1;
                     bray = make_ray(add(hit, mul(nrm, .0001f)), normalize(reflect(bray.d, nrm)));
+                    have_bray = true;
                 } else {
                     color = mk4(lerpf(color.x, .5f, intensity), lerpf(color.y, .5f, intensity),
                                 lerpf(color.z, .5f, intensity), lerpf(color.w, 1.f, intensity));
                     intensity = 0;
                 }
             }
-            size_t o = (size_t)out_row * W + x;
+            if (refl_rec) put_record(refl_rec + 14 * o, intensity, have_bray ? &bray : nullptr, color);
             if (rgba) { rgba[4 * o] = color.x; rgba[4 * o + 1] = color.y; rgba[4 * o + 2] = color.z; rgba[4 * o + 3] = color.w; }
             if (intensity_out) intensity_out[o] = intensity;
             cnt[2] += c.int_visits;

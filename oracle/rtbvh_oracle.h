@@ -105,6 +105,15 @@ int orc_trace(const orc_scene* s, const orc_node* nodes, uint32_t n,
               const float wvp[16], const float wv[16], uint32_t W, uint32_t H,
               uint32_t bounces, uint32_t row_begin, uint32_t row_end, uint32_t row_step,
               float* rgba, float* intensity, uint64_t* counters);
+/* orc_trace plus the per-pixel RayPresent records (RayTraceGlobal.hlsl:30-35; 14 floats:
+ * intensity, origin, direction, invDirection, color): reflectRay after the last pass
+ * (RayTraceLaunch.hlsl:48-67, RayTraceReflection.hlsl:24-55) and refractRay
+ * (RayTraceLaunch.hlsl:70-80).  Ray fields HLSL leaves unset (zero intensity at the
+ * hit) are written as 0.  Either record pointer may be NULL. */
+int orc_trace_ex(const orc_scene* s, const orc_node* nodes, uint32_t n,
+                 const float wvp[16], const float wv[16], uint32_t W, uint32_t H,
+                 uint32_t bounces, uint32_t row_begin, uint32_t row_end, uint32_t row_step,
+                 float* rgba, float* intensity, uint64_t* counters, float* refl_rec, float* refr_rec);
 
 /* ---- misc ------------------------------------------------------------------ */
 /* XMMatrixLookAtLH * XMMatrixPerspectiveFovLH as Graphics.cpp:44-53 (row-vector

@@ -36,6 +36,9 @@ struct rtbvh_ctx {
     float4 *d_tclip = nullptr, *d_leaf = nullptr;
     Inner* d_inner = nullptr;
     Inner* d_rec = nullptr;                  // node records in slots (rtbvh_device.h), 2T-1
+    float* d_refl_rec = nullptr;             // RTBVH_FLAG_REFRACT_RECORDS: reflectRay / refractRay
+    float* d_refr_rec = nullptr;             //   RayPresent records, 14 floats per traced pixel
+    size_t cap_rec = 0, rec_P = 0;           // record capacity; pixels of the last records trace
     uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr;
     float* d_bounds = nullptr;
     float* d_rootbox = nullptr;
@@ -216,7 +219,9 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
 
     const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
     const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && vsel != 1;
-    const bool refill = ((c->cfg.flags & RTBVH_FLAG_REFILL_BOUNCE) != 0 || wide) && vsel != 1;
+    const bool records = (c->cfg.flags & RTBVH_FLAG_REFRACT_RECORDS) != 0;
+    // the records are written by k_primary and k_bounce_shade: the split bounce path
+    const bool refill = ((c->cfg.flags & RTBVH_FLAG_REFILL_BOUNCE) != 0 || wide || records) && vsel != 1;
     // A/B of the refill kernel's LDS stack depth: variant 2 -> none, 3 -> 8, 4 -> 20, else 16
     const int lds_stack = vsel == 2 ? 0 : vsel == 3 ? 8 : vsel == 4 ? 20 : 16;
     // ... and of the refill policy (idle lanes that trigger it, rays per atomic claim):
@@ -229,6 +234,16 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1)
         pvariant = wide ? 5 : (variant == 1 ? 4 : 3);
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
+    if (records) {
+        if (c->cap_rec < P) {
+            HIPC(c, dalloc(c->d_refl_rec, 14 * (size_t)P));
+            HIPC(c, dalloc(c->d_refr_rec, 14 * (size_t)P));
+            c->cap_rec = P;
+        }
+        a.refl_rec = c->d_refl_rec;
+        a.refr_rec = c->d_refr_rec;
+    }
+    c->rec_P = records ? P : 0;
     launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, pvariant, s);
     if (timing) HIPC(c, hipEventRecord(ev[1], s));
     for (uint32_t b = 0; b < bounces; b++) {
@@ -337,7 +352,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
-    dfree(c->d_bscratch);
+    dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);
     dfree(c->d_counters);
     for (auto& row : c->evb)
         for (auto& e : row)
@@ -559,8 +574,16 @@ rtbvh_status rtbvh_read_sorted(rtbvh_ctx* c, uint32_t* keys, uint32_t* ids) {
     return RTBVH_OK;
 }
 
-rtbvh_status rtbvh_read_rays(rtbvh_ctx* c, rtbvh_ray_present*, rtbvh_ray_present*) {
-    return fail(c, RTBVH_ERR_INVALID_ARG, "read_rays: ray records are not kept in this version");
+rtbvh_status rtbvh_read_rays(rtbvh_ctx* c, rtbvh_ray_present* reflect_out, rtbvh_ray_present* refract_out) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    if (!c->traced || c->rec_P == 0)
+        return fail(c, RTBVH_ERR_NOT_READY, "read_rays: the last trace ran without RTBVH_FLAG_REFRACT_RECORDS");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const size_t bytes = c->rec_P * sizeof(rtbvh_ray_present);
+    if (reflect_out) HIPC(c, hipMemcpy(reflect_out, c->d_refl_rec, bytes, hipMemcpyDeviceToHost));
+    if (refract_out) HIPC(c, hipMemcpy(refract_out, c->d_refr_rec, bytes, hipMemcpyDeviceToHost));
+    return RTBVH_OK;
 }
 
 rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {

@@ -422,9 +422,36 @@ __device__ __forceinline__ bool trace_ray(const Inner* __restrict__ inner, const
 struct HitInfo {
     float4 color;   // renderPixel(...) * specular
     f3 hitp, nrm;
-    float shininess;
+    float shininess, alpha, optical_density;
     bool textured;
 };
+
+// HLSL refract(i, n, eta) as documented (see oracle refract_hlsl; same operation order)
+__device__ __forceinline__ f3 refract_hlsl(f3 i, f3 n, float eta) {
+    const float cosi = dot(mk(-i.x, -i.y, -i.z), n);
+    const float cost2 = 1.0f - eta * eta * (1.0f - cosi * cosi);
+    const float s = eta * cosi - sqrtf(fabsf(cost2));
+    const f3 t = add(mul(i, eta), mul(n, s));
+    const float keep = cost2 > 0.0f ? 1.0f : 0.0f;
+    return mul(t, keep);
+}
+
+// RayPresent record (RayTraceGlobal.hlsl:30-35), 14 floats at 56*idx (8-B aligned):
+// intensity, origin, direction, invDirection, color.  `ray` false writes a zero ray
+// (fields HLSL leaves unset when the intensity is 0, and clearRayPresent on a miss).
+__device__ __forceinline__ void put_record(float* rec, size_t idx, float intensity, bool ray, f3 o, f3 d,
+                                           float4 color) {
+    float2* r = reinterpret_cast<float2*>(rec + 14 * idx);
+    if (!ray) { o = mk(0.f, 0.f, 0.f); d = o; }
+    const f3 inv = ray ? mk(1.f / d.x, 1.f / d.y, 1.f / d.z) : mk(0.f, 0.f, 0.f);
+    r[0] = make_float2(intensity, o.x);
+    r[1] = make_float2(o.y, o.z);
+    r[2] = make_float2(d.x, d.y);
+    r[3] = make_float2(d.z, inv.x);
+    r[4] = make_float2(inv.y, inv.z);
+    r[5] = make_float2(color.x, color.y);
+    r[6] = make_float2(color.z, color.w);
+}
 
 // getHitLoc (:15-19) + getNromalTexCoord (RayTraceHelper.hlsl:12-35) + renderPixel*specular
 // (RayTraceRender.hlsl:16-29, RayTraceLaunch.hlsl:57-59) for the hit triangle only
@@ -464,6 +491,8 @@ __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_l
                           sat(m.ambient[2] + m.diffuse[2] * tz) * m.specular[2],
                           sat(m.ambient[3] + m.diffuse[3] * tw) * m.specular[3]);
     h.shininess = m.shininess;
+    h.alpha = m.alpha;
+    h.optical_density = m.optical_density;
     return h;
 }
 
@@ -550,8 +579,22 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
                 e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
                 live = true;
             }
+            if (a.refl_rec) {   // :48-67 (the ray is set only when the intensity is not 0)
+                const bool rr = intensity != 0;
+                put_record(a.refl_rec, out, intensity, rr, rr ? add(h.hitp, mul(h.nrm, .001f)) : o,
+                           rr ? normalize(reflect(d, h.nrm)) : d, color);
+            }
+            if (a.refr_rec) {   // :70-80, REFRACTION_DECAY 1
+                const float ri = (1.f - h.alpha) * 1;
+                const bool rr = ri != 0;
+                put_record(a.refr_rec, out, ri, rr, rr ? sub(h.hitp, mul(h.nrm, .001f)) : o,
+                           rr ? normalize(refract_hlsl(d, h.nrm, h.optical_density)) : d,
+                           make_float4(1.f, 1.f, 1.f, 1.f));
+            }
         } else {
             color = make_float4(.5f, .5f, .5f, 1.f);   // getBackground, :85-86
+            if (a.refl_rec) put_record(a.refl_rec, out, 0.f, false, o, d, color);   // clearRayPresent
+            if (a.refr_rec) put_record(a.refr_rec, out, 0.f, false, o, d, color);
         }
         a.color[out] = color;
         if (a.intensity) a.intensity[out] = intensity;
@@ -892,10 +935,16 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
             e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
             e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
             live = 0 < intensity;
+            if (a.refl_rec) put_record(a.refl_rec, e.idx, intensity, true, ro, rd, col);   // :42-46
         } else {
             col = make_float4(lerpf(col.x, .5f, intensity), lerpf(col.y, .5f, intensity),
                               lerpf(col.z, .5f, intensity), lerpf(col.w, 1.f, intensity));
             intensity = 0.f;
+            if (a.refl_rec) {   // :50-55: the ray stays, intensity 0, colour blended
+                float* r = a.refl_rec + 14 * (size_t)e.idx;
+                r[0] = 0.f;
+                r[10] = col.x; r[11] = col.y; r[12] = col.z; r[13] = col.w;
+            }
         }
         a.color[e.idx] = col;
         if (a.intensity) a.intensity[e.idx] = intensity;

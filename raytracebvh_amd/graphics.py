@@ -101,6 +101,15 @@ class Context:
         self._check(_L.lib().rtbvh_read_framebuffer(self._h, _L.ptr(out)))
         return out
 
+    def read_rays(self):
+        """(reflectRay, refractRay) RayPresent records of the last full-frame trace made with
+        FLAG_REFRACT_RECORDS, each (H, W, 14) float32: intensity, origin, direction,
+        invDirection, color (RayTraceGlobal.hlsl:30-35)."""
+        refl = np.zeros((self.height, self.width, 14), np.float32)
+        refr = np.zeros((self.height, self.width, 14), np.float32)
+        self._check(_L.lib().rtbvh_read_rays(self._h, _L.ptr(refl), _L.ptr(refr)))
+        return refl, refr
+
     def read_intensity(self) -> np.ndarray:
         out = np.zeros((self.height, self.width), np.float32)
         self._check(_L.lib().rtbvh_read_intensity(self._h, _L.ptr(out)))

@@ -241,6 +241,39 @@ def test_trace_matches_oracle_on_obj(name, W, H, bounces, mode):
     assert ost["hits"] > 0
 
 
+@pytest.mark.parametrize("name,W,H,bounces", [("Rect", 320, 240, 1), ("Test", 800, 800, 3), ("Test", 640, 360, 0)])
+def test_ray_records_match_oracle(name, W, H, bounces):
+    """reflectRay / refractRay RayPresent records (RTBVH_FLAG_REFRACT_RECORDS) vs the oracle,
+    bit for bit (NaN where both have NaN: refract of a total internal reflection)."""
+    d = load_scene_fixture(name)
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=rt.FLAG_REFRACT_RECORDS | rt.FLAG_PACKET_PRIMARY) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, bounces)
+        refl, refr = c.read_rays()
+        fb = c.read_framebuffer()
+        nodes = c.read_bvh()
+    ofb, _, _, orefl, orefr = orc.trace(_oscene(s), nodes, wvp, wv, W, H, bounces, want_records=True)
+    assert np.array_equal(fb, ofb)
+    np.testing.assert_array_equal(refl, orefl)
+    np.testing.assert_array_equal(refr, orefr)
+    assert np.array_equal(refl[..., 10:14], fb)   # the record's colour is the framebuffer
+    assert (refl[..., 0] > 0).any() or bounces > 0
+
+
+def test_read_rays_needs_records_flag():
+    d = load_scene_fixture("Rect")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(64, 64))
+        c.compute_bvh(64, 64, 1)
+        with pytest.raises(RuntimeError, match="REFRACT_RECORDS"):
+            c.read_rays()
+
+
 @pytest.mark.parametrize("mode", list(TRACE_MODES))
 def test_trace_synthetic_sampled_rows(mode):
     """C5 scene at reduced size: 500k triangles, 1920x1080, every 37th row vs oracle."""
