@@ -78,10 +78,17 @@ typedef struct {
     float color[4];
 } rtbvh_ray_present;
 
-/* An RGBA8 texture (sRGB encoded, as the reference's R8G8B8A8_UNORM_SRGB, Image.cpp:9) */
+/* An RGBA8 texture (sRGB encoded, as the reference's R8G8B8A8_UNORM_SRGB, Image.cpp:9).
+ * Row 0 is the first row ilCopyPixels returns (Image.cpp:48-49; DevIL without IL_ORIGIN_SET
+ * keeps the file's own row order: the bottom row first for BMP, the top row for JPEG) and
+ * is texture row v = 0.  Sampling (RayTraceRender.hlsl:22-26, sampler Image.cpp:154-169:
+ * MIN_MAG_MIP_LINEAR, WRAP, SampleLevel 0), as restated here (parity unpinned: DevIL and
+ * the D3D filter precision are not available): texels decoded sRGB -> linear through the
+ * table of rtbvh_srgb_table (alpha / 255), x = u*W - 0.5, y = v*H - 0.5, wrap, and
+ * bilinear in fp32 as lerp(lerp(t00, t10, fx), lerp(t01, t11, fx), fy). */
 typedef struct {
     uint32_t width, height;
-    const uint8_t* rgba8; /* width*height*4 bytes, row 0 = first row of the image */
+    const uint8_t* rgba8; /* width*height*4 bytes */
 } rtbvh_texture;
 
 enum {
@@ -230,6 +237,13 @@ rtbvh_status rtbvh_build_from_codes(rtbvh_ctx* ctx, const uint32_t* sorted_codes
                                     const float* leaf_boxes, uint32_t n, rtbvh_node* out);
 
 /* ---- host-side scene helpers (ObjLoader replacement, camera) ---------------- */
+/* Decode an uncompressed BMP (BI_RGB 1/4/8-bit paletted or 24/32-bit, BI_BITFIELDS 32-bit) into RGBA8 rows in
+ * file order (bottom row first for the usual positive height), as DevIL hands them to
+ * Image.cpp:48-49.  Free with rtbvh_texture_free. */
+rtbvh_status rtbvh_texture_load_bmp(const char* path, rtbvh_texture* out);
+void rtbvh_texture_free(rtbvh_texture* tex);
+/* The 256-entry sRGB -> linear table the texture sampling uses (IEC 61966-2-1, in double). */
+void rtbvh_srgb_table(float out[256]);
 typedef struct rtbvh_scene rtbvh_scene;
 /* ObjLoader::Load (ObjectFileLoader.cpp:212-547) incl. its de-duplication rules. */
 rtbvh_status rtbvh_scene_load_obj(const char* path, rtbvh_scene** out);

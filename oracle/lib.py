@@ -21,6 +21,10 @@ NODE_DTYPE = np.dtype([("parent", "<u4"), ("child_l", "<u4"), ("child_r", "<u4")
 assert NODE_DTYPE.itemsize == 44
 
 
+class _Texture(ctypes.Structure):   # orc_texture
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("rgba8", ctypes.c_void_p)]
+
+
 class _Scene(ctypes.Structure):
     _fields_ = [("verts", ctypes.c_void_p), ("num_verts", ctypes.c_uint32),
                 ("indices", ctypes.c_void_p), ("num_indices", ctypes.c_uint32),
@@ -69,6 +73,7 @@ def lib():
         L.orc_trace_ex.restype = ctypes.c_int
         L.orc_trace_ex.argtypes = L.orc_trace.argtypes + [u32p, u32p]
         L.orc_camera_reference.argtypes = [ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]
+        L.orc_sample_texture.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, u32p]
         L.orc_fnv1a64.restype = ctypes.c_uint64
         L.orc_fnv1a64.argtypes = [u32p, ctypes.c_uint64]
         L.orc_num_threads.restype = ctypes.c_int
@@ -84,13 +89,18 @@ def _p(a: np.ndarray):
 class Scene:
     """Holds numpy arrays alive for the C struct view."""
 
-    def __init__(self, vertices, indices, mat_indices, material_blob):
+    def __init__(self, vertices, indices, mat_indices, material_blob, textures=()):
         self.vertices = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 8)
         self.indices = np.ascontiguousarray(indices, dtype=np.uint32)
         self.mat_indices = np.ascontiguousarray(mat_indices, dtype=np.uint32)
         self.material_blob = np.ascontiguousarray(material_blob, dtype=np.uint8).reshape(-1, 68)
+        self.textures = [np.ascontiguousarray(t, dtype=np.uint8) for t in textures]   # (H, W, 4)
+        self._tex = (_Texture * max(len(self.textures), 1))()
+        for k, t in enumerate(self.textures):
+            self._tex[k] = _Texture(t.shape[1], t.shape[0], t.ctypes.data)
         self.c = _Scene(_p(self.vertices), len(self.vertices), _p(self.indices), len(self.indices),
-                        _p(self.mat_indices), _p(self.material_blob), len(self.material_blob), None, 0)
+                        _p(self.mat_indices), _p(self.material_blob), len(self.material_blob),
+                        ctypes.cast(self._tex, ctypes.c_void_p) if self.textures else None, len(self.textures))
 
     @property
     def num_tris(self) -> int:
@@ -199,6 +209,15 @@ def trace(scene: Scene, nodes: np.ndarray, wvp, wv, W, H, bounces, row_begin=0, 
     if want_records:
         return rgba, inten, stats, refl, refr
     return rgba, inten, stats
+
+
+def sample_texture(tex: np.ndarray, u: float, v: float) -> np.ndarray:
+    """orc_sample_texture on an (H, W, 4) uint8 texture."""
+    tex = np.ascontiguousarray(tex, dtype=np.uint8)
+    t = _Texture(tex.shape[1], tex.shape[0], tex.ctypes.data)
+    out = np.zeros(4, np.float32)
+    lib().orc_sample_texture(ctypes.byref(t), u, v, _p(out))
+    return out
 
 
 def camera_reference(W, H):

@@ -473,13 +473,54 @@ void normal_texcoord(const Tri& t, f3 pt, float uv[2], f3& n) {
     n = add(add(mul(t.nrm[0], a1), mul(t.nrm[1], a2)), mul(t.nrm[2], a3));
 }
 
+// diffuseTex[k].SampleLevel(compSample, uv, 0), RayTraceRender.hlsl:22-26, with the
+// sampler of Image.cpp:154-169 (MIN_MAG_MIP_LINEAR, WRAP) on R8G8B8A8_UNORM_SRGB
+// texels (Image.cpp:9).  Restated (parity unpinned: no DevIL, no D3D filter): texels
+// decoded sRGB -> linear (IEC 61966-2-1 in double, rounded to float; alpha / 255),
+// x = u*W - 0.5, y = v*H - 0.5, wrap, bilinear as lerp(lerp(t00, t10, fx), lerp(t01, t11, fx), fy).
+struct SrgbTable {
+    float v[256];
+    SrgbTable() {
+        for (int i = 0; i < 256; i++) {
+            const double c = i / 255.0;
+            v[i] = (float)(c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4));
+        }
+    }
+};
+const float* srgb_table() {
+    static const SrgbTable tab;   // thread-safe one-time init
+    return tab.v;
+}
+f4 texel(const orc_texture& t, uint32_t x, uint32_t y) {
+    const uint8_t* p = t.rgba8 + ((size_t)y * t.width + x) * 4;
+    const float* tab = srgb_table();
+    return mk4(tab[p[0]], tab[p[1]], tab[p[2]], (float)p[3] / 255.f);
+}
+uint32_t wrap_index(float f, uint32_t n) {
+    if (!(std::fabs(f) < 2147483648.f)) f = 0.f;
+    int64_t i = (int64_t)f % (int64_t)n;
+    return (uint32_t)(i < 0 ? i + n : i);
+}
+f4 sample_texture(const orc_texture& t, float u, float v) {
+    const float x = u * (float)t.width - 0.5f, y = v * (float)t.height - 0.5f;
+    const float x0 = std::floor(x), y0 = std::floor(y);
+    const float fx = x - x0, fy = y - y0;
+    const uint32_t ix = wrap_index(x0, t.width), iy = wrap_index(y0, t.height);
+    const uint32_t ix1 = ix + 1 == t.width ? 0u : ix + 1, iy1 = iy + 1 == t.height ? 0u : iy + 1;
+    const f4 t00 = texel(t, ix, iy), t10 = texel(t, ix1, iy), t01 = texel(t, ix, iy1), t11 = texel(t, ix1, iy1);
+    const f4 top = mk4(lerpf(t00.x, t10.x, fx), lerpf(t00.y, t10.y, fx), lerpf(t00.z, t10.z, fx), lerpf(t00.w, t10.w, fx));
+    const f4 bot = mk4(lerpf(t01.x, t11.x, fx), lerpf(t01.y, t11.y, fx), lerpf(t01.z, t11.z, fx), lerpf(t01.w, t11.w, fx));
+    return mk4(lerpf(top.x, bot.x, fy), lerpf(top.y, bot.y, fy), lerpf(top.z, bot.z, fy), lerpf(top.w, bot.w, fy));
+}
+
 // renderPixel * specular, RayTraceRender.hlsl:16-29 + RayTraceLaunch.hlsl:57-59.
-// Textures: white (texture sampling is a later row).
+// A material with texNum != -1 but no texture bound samples white.
 f4 shade(const Ctx& c, uint32_t tri, const float uv[2], bool* textured) {
-    (void)uv;
     const orc_material& m = c.s->materials[c.s->mat_indices[tri]];
     f4 tex = mk4(1, 1, 1, 1);
     *textured = m.tex_num != -1;
+    if (*textured && (uint32_t)m.tex_num < c.s->num_textures)
+        tex = sample_texture(c.s->textures[m.tex_num], uv[0], uv[1]);
     f4 col = mk4(sat(m.ambient[0] + m.diffuse[0] * tex.x), sat(m.ambient[1] + m.diffuse[1] * tex.y),
                  sat(m.ambient[2] + m.diffuse[2] * tex.z), sat(m.ambient[3] + m.diffuse[3] * tex.w));
     return mk4(col.x * m.specular[0], col.y * m.specular[1], col.z * m.specular[2], col.w * m.specular[3]);
@@ -614,6 +655,11 @@ int orc_trace_ex(const orc_scene* s, const orc_node* nodes, uint32_t n, const fl
     }
     if (counters) for (int k = 0; k < 8; k++) counters[k] = cnt[k];
     return 0;
+}
+
+void orc_sample_texture(const orc_texture* t, float u, float v, float out[4]) {
+    const f4 r = sample_texture(*t, u, v);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
 }
 
 /* Graphics.cpp:44-53 with XMMatrixLookAtLH / XMMatrixPerspectiveFovLH restated

@@ -115,6 +115,10 @@ int orc_trace_ex(const orc_scene* s, const orc_node* nodes, uint32_t n,
                  uint32_t bounces, uint32_t row_begin, uint32_t row_end, uint32_t row_step,
                  float* rgba, float* intensity, uint64_t* counters, float* refl_rec, float* refr_rec);
 
+/* diffuseTex.SampleLevel(linear, wrap, uv, 0) on an sRGB RGBA8 texture, as restated for
+ * RayTraceRender.hlsl:22-26 (include/rtbvh.h rtbvh_texture). */
+void orc_sample_texture(const orc_texture* t, float u, float v, float out[4]);
+
 /* ---- misc ------------------------------------------------------------------ */
 /* XMMatrixLookAtLH * XMMatrixPerspectiveFovLH as Graphics.cpp:44-53 (row-vector
  * convention, float32, libm sinf/cosf).  wvp and wv row-major 4x4. */

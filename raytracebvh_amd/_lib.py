@@ -34,7 +34,7 @@ EXPORTS = [
     "rtbvh_scene_synthetic", "rtbvh_scene_free", "rtbvh_scene_num_vertices", "rtbvh_scene_num_indices",
     "rtbvh_scene_num_materials", "rtbvh_scene_num_textures", "rtbvh_scene_vertices", "rtbvh_scene_indices",
     "rtbvh_scene_mat_indices", "rtbvh_scene_materials", "rtbvh_scene_texture_path", "rtbvh_set_scene_obj",
-    "rtbvh_camera_reference",
+    "rtbvh_camera_reference", "rtbvh_texture_load_bmp", "rtbvh_texture_free", "rtbvh_srgb_table",
 ]
 
 NODE_DTYPE = np.dtype([("parent", "<u4"), ("child_l", "<u4"), ("child_r", "<u4"), ("code", "<u4"),
@@ -49,6 +49,11 @@ class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("morton_mode", ctypes.c_uint32), ("delta_mode", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("scene_bb_min", ctypes.c_float * 3),
                 ("scene_bb_max", ctypes.c_float * 3), ("stream", ctypes.c_void_p)]
+
+
+class Texture(ctypes.Structure):
+    """rtbvh_texture: RGBA8 texels, row 0 = texture row v = 0 (include/rtbvh.h)."""
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("rgba8", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -138,6 +143,9 @@ def lib() -> ctypes.CDLL:
         "rtbvh_scene_texture_path": (ctypes.c_char_p, [vp, u32]),
         "rtbvh_set_scene_obj": (i32, [vp, vp, vp, u32]),
         "rtbvh_camera_reference": (None, [u32, u32, vp, vp]),
+        "rtbvh_texture_load_bmp": (i32, [ctypes.c_char_p, vp]),
+        "rtbvh_texture_free": (None, [vp]),
+        "rtbvh_srgb_table": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -36,6 +36,10 @@ struct rtbvh_ctx {
     float4 *d_tclip = nullptr, *d_leaf = nullptr;
     Inner* d_inner = nullptr;
     Inner* d_rec = nullptr;                  // node records in slots (rtbvh_device.h), 2T-1
+    uint32_t* d_texels = nullptr;            // textures (rtbvh_texture), concatenated RGBA8
+    uint4* d_texinfo = nullptr;
+    float* d_srgb = nullptr;
+    uint32_t ntex = 0;
     float* d_refl_rec = nullptr;             // RTBVH_FLAG_REFRACT_RECORDS: reflectRay / refractRay
     float* d_refr_rec = nullptr;             //   RayPresent records, 14 floats per traced pixel
     size_t cap_rec = 0, rec_P = 0;           // record capacity; pixels of the last records trace
@@ -177,6 +181,10 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.verts = c->d_verts;
     a.idx = c->d_idx;
     a.matidx = c->d_matidx;
+    a.texels = c->d_texels;
+    a.texinfo = c->d_texinfo;
+    a.srgb = c->d_srgb;
+    a.ntex = c->ntex;
     a.mats = c->d_mats;
     a.T = c->T;
     a.W = W;
@@ -353,6 +361,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
     dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);
+    dfree(c->d_texels); dfree(c->d_texinfo); dfree(c->d_srgb);
     dfree(c->d_counters);
     for (auto& row : c->evb)
         for (auto& e : row)
@@ -371,8 +380,10 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
                              uint32_t nidx, const uint32_t* mat_idx, const rtbvh_material* mats, uint32_t nmats,
                              const rtbvh_texture* textures, uint32_t ntex) {
     if (!c) return RTBVH_ERR_INVALID_ARG;
-    (void)textures;
-    (void)ntex;
+    if (ntex && !textures) return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: ntex > 0 without textures");
+    for (uint32_t k = 0; k < ntex; k++)
+        if (textures[k].width == 0 || textures[k].height == 0 || !textures[k].rgba8)
+            return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: empty texture");
     if (!verts || !indices || !mat_idx || !mats || nverts == 0 || nidx == 0 || nidx % 3 != 0 || nmats == 0)
         return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: empty or ragged input");
     const uint32_t T = nidx / 3;
@@ -397,6 +408,28 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
         HIPC(c, hipMemcpy(c->d_idx, indices, sizeof(uint32_t) * nidx, hipMemcpyHostToDevice));
         HIPC(c, hipMemcpy(c->d_matidx, mat_idx, sizeof(uint32_t) * T, hipMemcpyHostToDevice));
         HIPC(c, hipMemcpy(c->d_mats, mats, sizeof(rtbvh_material) * nmats, hipMemcpyHostToDevice));
+        // textures: one texel array + a {first texel, width, height} table (t4-t5 of
+        // RayTraceGlobal.hlsl:114-115, any count here)
+        std::vector<uint4> info(ntex ? ntex : 1);
+        size_t total = 0;
+        for (uint32_t k = 0; k < ntex; k++) {
+            info[k] = make_uint4((uint32_t)total, textures[k].width, textures[k].height, 0u);
+            total += (size_t)textures[k].width * textures[k].height;
+        }
+        if (total >= (1ull << 32)) return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: textures too large");
+        HIPC(c, dalloc(c->d_texels, total ? total : 1));
+        HIPC(c, dalloc(c->d_texinfo, info.size()));
+        for (uint32_t k = 0; k < ntex; k++)
+            HIPC(c, hipMemcpy(c->d_texels + info[k].x, textures[k].rgba8,
+                              (size_t)textures[k].width * textures[k].height * 4, hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_texinfo, info.data(), sizeof(uint4) * info.size(), hipMemcpyHostToDevice));
+        if (!c->d_srgb) {
+            float tab[256];
+            rtbvh_srgb_table(tab);
+            HIPC(c, dalloc(c->d_srgb, 256));
+            HIPC(c, hipMemcpy(c->d_srgb, tab, sizeof(tab), hipMemcpyHostToDevice));
+        }
+        c->ntex = ntex;
     } catch (const std::bad_alloc&) {
         return fail(c, RTBVH_ERR_OOM, "set_scene: host allocation failed");
     }

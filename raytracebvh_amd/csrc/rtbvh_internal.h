@@ -71,6 +71,10 @@ struct TraceArgs {
     const uint32_t* idx;
     const uint32_t* matidx;
     const Mat* mats;
+    const uint32_t* texels;   // RGBA8 texels of every texture, concatenated (u32 per texel)
+    const uint4* texinfo;     // per texture: {first texel, width, height, 0}
+    const float* srgb;        // [256] sRGB -> linear (rtbvh_srgb_table)
+    uint32_t ntex;
     uint32_t T, W, H, rank, nranks;
     Mat4 wv;
     float4* color;            // output pixels (compacted band rows when nranks > 1)

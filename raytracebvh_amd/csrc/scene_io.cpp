@@ -347,3 +347,98 @@ void rtbvh_camera_reference(uint32_t W, uint32_t H, float wvp[16], float wv[16])
 }
 
 }  // extern "C"
+
+// ---- textures ------------------------------------------------------------------
+extern "C" {
+
+void rtbvh_srgb_table(float out[256]) {
+    for (int i = 0; i < 256; i++) {
+        const double c = i / 255.0;
+        out[i] = (float)(c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4));
+    }
+}
+
+static uint32_t rd_u32(const uint8_t* p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
+static uint16_t rd_u16(const uint8_t* p) { return (uint16_t)(p[0] | p[1] << 8); }
+
+rtbvh_status rtbvh_texture_load_bmp(const char* path, rtbvh_texture* out) {
+    if (!path || !out) return RTBVH_ERR_INVALID_ARG;
+    out->width = out->height = 0;
+    out->rgba8 = nullptr;
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return RTBVH_ERR_IO;
+    std::vector<uint8_t> b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (b.size() < 54 || b[0] != 'B' || b[1] != 'M') return RTBVH_ERR_IO;
+    const uint32_t off = rd_u32(&b[10]), hsize = rd_u32(&b[14]);
+    const int32_t w = (int32_t)rd_u32(&b[18]), h = (int32_t)rd_u32(&b[22]);
+    const uint16_t bpp = rd_u16(&b[28]);
+    const uint32_t comp = hsize >= 40 ? rd_u32(&b[30]) : 0;
+    const bool paletted = bpp == 1 || bpp == 4 || bpp == 8;
+    if (w <= 0 || h == 0 || !(paletted || bpp == 24 || bpp == 32) || !(comp == 0 || (comp == 3 && bpp == 32)))
+        return RTBVH_ERR_IO;
+    // palette (BGRA quads after the info header), 2^bpp or biClrUsed entries
+    uint32_t npal = 0;
+    const uint8_t* pal = nullptr;
+    if (paletted) {
+        const uint32_t used = hsize >= 36 ? rd_u32(&b[46]) : 0;
+        npal = used ? used : (1u << bpp);
+        if (npal > 256 || 14 + (size_t)hsize + 4 * npal > b.size()) return RTBVH_ERR_IO;
+        pal = &b[14 + hsize];
+    }
+    const uint32_t W = (uint32_t)w, H = (uint32_t)(h < 0 ? -h : h);
+    uint32_t mr = 0x00FF0000u, mg = 0x0000FF00u, mb = 0x000000FFu, ma = bpp == 32 ? 0xFF000000u : 0u;
+    if (comp == 3 && b.size() >= 14 + 52) {
+        mr = rd_u32(&b[54]); mg = rd_u32(&b[58]); mb = rd_u32(&b[62]);
+        ma = hsize >= 56 ? rd_u32(&b[66]) : 0u;
+    }
+    const size_t stride = ((size_t)W * bpp / 8 + 3) & ~(size_t)3;
+    if ((size_t)off + stride * H > b.size()) return RTBVH_ERR_IO;
+    auto chan = [](uint32_t px, uint32_t m) -> uint8_t {
+        if (!m) return 255;
+        int sh = 0;
+        while (!((m >> sh) & 1u)) sh++;
+        const uint32_t v = (px & m) >> sh, mx = m >> sh;
+        return (uint8_t)(mx == 255 ? v : (v * 255 + mx / 2) / mx);
+    };
+    uint8_t* px = (uint8_t*)std::malloc((size_t)W * H * 4);
+    if (!px) return RTBVH_ERR_OOM;
+    for (uint32_t r = 0; r < H; r++) {   // file order: row r of the pixel array
+        const uint8_t* src = &b[off + stride * r];
+        uint8_t* dst = px + (size_t)r * W * 4;
+        for (uint32_t x = 0; x < W; x++) {
+            if (paletted) {
+                const uint32_t bit = x * bpp;
+                uint32_t k = (src[bit >> 3] >> (8 - bpp - (bit & 7))) & ((1u << bpp) - 1u);
+                if (k >= npal) k = 0;
+                dst[4 * x + 0] = pal[4 * k + 2];
+                dst[4 * x + 1] = pal[4 * k + 1];
+                dst[4 * x + 2] = pal[4 * k + 0];
+                dst[4 * x + 3] = 255;
+            } else if (bpp == 24) {
+                dst[4 * x + 0] = src[3 * x + 2];
+                dst[4 * x + 1] = src[3 * x + 1];
+                dst[4 * x + 2] = src[3 * x + 0];
+                dst[4 * x + 3] = 255;
+            } else {
+                const uint32_t v = rd_u32(src + 4 * x);
+                dst[4 * x + 0] = chan(v, mr);
+                dst[4 * x + 1] = chan(v, mg);
+                dst[4 * x + 2] = chan(v, mb);
+                dst[4 * x + 3] = chan(v, ma);
+            }
+        }
+    }
+    out->width = W;
+    out->height = H;
+    out->rgba8 = px;
+    return RTBVH_OK;
+}
+
+void rtbvh_texture_free(rtbvh_texture* tex) {
+    if (!tex) return;
+    std::free((void*)tex->rgba8);
+    tex->rgba8 = nullptr;
+    tex->width = tex->height = 0;
+}
+
+}  // extern "C"

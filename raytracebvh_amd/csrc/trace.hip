@@ -453,10 +453,37 @@ __device__ __forceinline__ void put_record(float* rec, size_t idx, float intensi
     r[6] = make_float2(color.z, color.w);
 }
 
+// diffuseTex[k].SampleLevel(compSample, uv, 0) as restated in include/rtbvh.h
+// (rtbvh_texture): sRGB texels -> linear by table, wrap, fp32 bilinear.
+__device__ __forceinline__ float4 texel(const TraceArgs& a, uint32_t first, uint32_t w, uint32_t x, uint32_t y) {
+    const uint32_t p = a.texels[first + (size_t)y * w + x];
+    return make_float4(a.srgb[p & 255u], a.srgb[(p >> 8) & 255u], a.srgb[(p >> 16) & 255u], (float)(p >> 24) / 255.f);
+}
+__device__ __forceinline__ uint32_t wrap_index(float f, uint32_t n) {
+    if (!(fabsf(f) < 2147483648.f)) f = 0.f;   // NaN / huge coordinates: texel 0 (never out of bounds)
+    int64_t i = (int64_t)f % (int64_t)n;
+    return (uint32_t)(i < 0 ? i + n : i);
+}
+__device__ __forceinline__ float4 sample_texture(const TraceArgs& a, uint32_t k, float u, float v) {
+    const uint4 ti = a.texinfo[k];
+    const float x = u * (float)ti.y - 0.5f, y = v * (float)ti.z - 0.5f;
+    const float x0 = floorf(x), y0 = floorf(y);
+    const float fx = x - x0, fy = y - y0;
+    const uint32_t ix = wrap_index(x0, ti.y), iy = wrap_index(y0, ti.z);
+    const uint32_t ix1 = ix + 1 == ti.y ? 0u : ix + 1, iy1 = iy + 1 == ti.z ? 0u : iy + 1;
+    const float4 t00 = texel(a, ti.x, ti.y, ix, iy), t10 = texel(a, ti.x, ti.y, ix1, iy);
+    const float4 t01 = texel(a, ti.x, ti.y, ix, iy1), t11 = texel(a, ti.x, ti.y, ix1, iy1);
+    const float4 top = make_float4(lerpf(t00.x, t10.x, fx), lerpf(t00.y, t10.y, fx), lerpf(t00.z, t10.z, fx),
+                                   lerpf(t00.w, t10.w, fx));
+    const float4 bot = make_float4(lerpf(t01.x, t11.x, fx), lerpf(t01.y, t11.y, fx), lerpf(t01.z, t11.z, fx),
+                                   lerpf(t01.w, t11.w, fx));
+    return make_float4(lerpf(top.x, bot.x, fy), lerpf(top.y, bot.y, fy), lerpf(top.z, bot.z, fy),
+                       lerpf(top.w, bot.w, fy));
+}
+
 // getHitLoc (:15-19) + getNromalTexCoord (RayTraceHelper.hlsl:12-35) + renderPixel*specular
 // (RayTraceRender.hlsl:16-29, RayTraceLaunch.hlsl:57-59) for the hit triangle only
 // (the reference transforms all three vertices at every leaf it visits).
-// Texture sampling: white.
 __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_leaf, f3 o, f3 d, float t) {
     HitInfo h;
     const uint32_t tri = __float_as_uint(a.leaf[4 * (size_t)best_leaf + 2].y);
@@ -480,12 +507,14 @@ __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_l
     const float w3 = magnitude(cross(v0, v1)) / a_0;
     const float tu = (uv[0][0] * w1 + uv[1][0] * w2) + uv[2][0] * w3;
     const float tv = (uv[0][1] * w1 + uv[1][1] * w2) + uv[2][1] * w3;
-    (void)tu;
-    (void)tv;
     h.nrm = add(add(mul(n[0], w1), mul(n[1], w2)), mul(n[2], w3));
     const Mat& m = a.mats[a.matidx[tri]];
     h.textured = m.tex_num != -1;
-    const float tx = 1.f, ty = 1.f, tz = 1.f, tw = 1.f;
+    float tx = 1.f, ty = 1.f, tz = 1.f, tw = 1.f;   // RayTraceRender.hlsl:19
+    if (h.textured && (uint32_t)m.tex_num < a.ntex) {   // :22-26 (no texture bound: white)
+        const float4 t = sample_texture(a, (uint32_t)m.tex_num, tu, tv);
+        tx = t.x; ty = t.y; tz = t.z; tw = t.w;
+    }
     h.color = make_float4(sat(m.ambient[0] + m.diffuse[0] * tx) * m.specular[0],
                           sat(m.ambient[1] + m.diffuse[1] * ty) * m.specular[1],
                           sat(m.ambient[2] + m.diffuse[2] * tz) * m.specular[2],

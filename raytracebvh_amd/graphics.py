@@ -61,9 +61,13 @@ class Context:
     # -- inputs --
     def set_scene(self, scene: Scene):
         self._scene = scene   # keep arrays alive for the duration of the call (copied by the library)
+        tex = (_L.Texture * max(len(scene.textures), 1))()
+        for k, t in enumerate(scene.textures):
+            tex[k] = _L.Texture(t.shape[1], t.shape[0], t.ctypes.data)
         self._check(_L.lib().rtbvh_set_scene(self._h, _L.ptr(scene.vertices), len(scene.vertices),
                                              _L.ptr(scene.indices), len(scene.indices), _L.ptr(scene.mat_indices),
-                                             _L.ptr(scene.materials), len(scene.materials), None, 0))
+                                             _L.ptr(scene.materials), len(scene.materials),
+                                             ctypes.byref(tex) if scene.textures else None, len(scene.textures)))
         self.num_tris = scene.num_tris
 
     def set_camera(self, wvp, wv):

@@ -21,6 +21,7 @@ class Scene:
     mat_indices: np.ndarray              # (T,) u32
     materials: np.ndarray                # (M,) MATERIAL_DTYPE (68-B MaterialUpload)
     texture_paths: list = field(default_factory=list)
+    textures: list = field(default_factory=list)   # (H, W, 4) uint8 per texNum, row 0 = v = 0
 
     def __post_init__(self):
         self.vertices = np.ascontiguousarray(self.vertices, dtype=np.float32).reshape(-1, 8)
@@ -30,6 +31,8 @@ class Scene:
         if m.dtype != _L.MATERIAL_DTYPE:
             m = np.frombuffer(np.ascontiguousarray(m, dtype=np.uint8).tobytes(), dtype=_L.MATERIAL_DTYPE).copy()
         self.materials = m
+        self.textures = [np.ascontiguousarray(t, dtype=np.uint8).reshape(t.shape[0], t.shape[1], 4)
+                         for t in self.textures]
 
     @property
     def num_tris(self) -> int:
@@ -71,15 +74,46 @@ def _from_native(handle) -> Scene:
     return Scene(verts.reshape(-1, 8), idx, midx, mats.view(_L.MATERIAL_DTYPE), paths)
 
 
-def load_obj(path: str) -> Scene:
-    """ObjLoader::Load (ObjectFileLoader.cpp:470-547) via the native loader."""
+def load_texture(path: str) -> np.ndarray:
+    """Image::loadImage (Image.cpp:35-61): RGBA8 rows in the order DevIL hands them over
+    without IL_ORIGIN_SET -- the file's own order (BMP: bottom row first, native decoder
+    rtbvh_texture_load_bmp; other formats: PIL, top row first)."""
+    if path.lower().endswith(".bmp"):
+        L = _L.lib()
+        t = _L.Texture()
+        _L.check(L.rtbvh_texture_load_bmp(os.fsencode(path), ctypes.byref(t)))
+        try:
+            return np.ctypeslib.as_array(ctypes.cast(t.rgba8, ctypes.POINTER(ctypes.c_uint8)),
+                                         shape=(t.height, t.width, 4)).copy()
+        finally:
+            L.rtbvh_texture_free(ctypes.byref(t))
+    from PIL import Image   # JPEG etc. (DevIL is not available; PIL is host-side image I/O)
+    with Image.open(path) as im:
+        return np.asarray(im.convert("RGBA"), dtype=np.uint8).copy()
+
+
+def load_obj(path: str, load_textures: bool = True) -> Scene:
+    """ObjLoader::Load (ObjectFileLoader.cpp:470-547) via the native loader, plus the map_Kd
+    textures (ObjectFileLoader.cpp:459-461 numbers them in material order).  A texture that
+    cannot be read is reported and replaced by one white texel (the reference prints the
+    error and continues, ObjectFileLoader.cpp:199-208)."""
     L = _L.lib()
     h = ctypes.c_void_p()
     _L.check(L.rtbvh_scene_load_obj(os.fsencode(path), ctypes.byref(h)))
     try:
-        return _from_native(h)
+        sc = _from_native(h)
     finally:
         L.rtbvh_scene_free(h)
+    if load_textures:
+        base = os.path.dirname(os.path.abspath(path))
+        for name in sc.texture_paths:
+            try:
+                sc.textures.append(load_texture(os.path.join(base, name)))
+            except Exception as e:   # noqa: BLE001
+                import warnings
+                warnings.warn(f"texture {name}: {e}; using white")
+                sc.textures.append(np.full((1, 1, 4), 255, np.uint8))
+    return sc
 
 
 def synthetic(ntris: int, seed: int = 0x5EED0004, half_extent=(50.0, 50.0, 50.0)) -> Scene:
@@ -99,6 +133,13 @@ def load_npz(path: str) -> Scene:
     z = np.load(path)
     names = [str(x) for x in z["texture_names"]] if "texture_names" in z else []
     return Scene(z["vertices"], z["indices"], z["mat_indices"], z["material_blob"], names)
+
+
+def srgb_table() -> np.ndarray:
+    """The sRGB -> linear table of the texture sampler (rtbvh_srgb_table)."""
+    out = np.zeros(256, np.float32)
+    _L.lib().rtbvh_srgb_table(_L.ptr(out))
+    return out
 
 
 def camera_reference(width: int, height: int):

@@ -263,6 +263,39 @@ def test_ray_records_match_oracle(name, W, H, bounces):
     assert (refl[..., 0] > 0).any() or bounces > 0
 
 
+def _textures(seed=3):
+    """Synthetic sRGB textures of odd sizes (the reference's image files are not on the GPU box;
+    decoding is pinned on CPU against PIL, tests/test_host.py)."""
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, (37, 53, 4), dtype=np.uint8), rng.integers(0, 256, (64, 29, 4), dtype=np.uint8)]
+
+
+@pytest.mark.parametrize("name,W,H,bounces", [("Test", 1920, 1080, 1), ("Image_Test", 1920, 1080, 0),
+                                               ("Test", 800, 800, 3), ("Rect", 320, 240, 1)])
+def test_textured_frames_match_oracle(name, W, H, bounces):
+    """renderPixel with diffuse textures (RayTraceRender.hlsl:22-26): GPU vs oracle, bit for bit,
+    for every traversal mode family; the textures must change the frame."""
+    d = load_scene_fixture(name)
+    tex = _textures()
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"], textures=tex)
+    os_ = orc.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"], textures=tex)
+    wvp, wv = rt.camera_reference(W, H)
+    for flags in (0, rt.FLAG_PACKET_PRIMARY | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH):
+        with rt.Context(device=0, flags=flags | rt.FLAG_COUNT_VISITS) as c:
+            c.set_scene(s)
+            c.set_camera(wvp, wv)
+            c.compute_bvh(W, H, bounces)
+            fb = c.read_framebuffer()
+            st = c.stats()
+            nodes = c.read_bvh()
+        ofb, _, ost = orc.trace(os_, nodes, wvp, wv, W, H, bounces)
+        np.testing.assert_allclose(fb, ofb, atol=RGB_TOL, rtol=0)
+        assert np.array_equal(fb, ofb)
+        assert st["textured_hits"] == ost["textured_hits"] > 0
+    white, _, _ = orc.trace(_oscene(s), nodes, wvp, wv, W, H, bounces)
+    assert not np.array_equal(white, ofb)
+
+
 def test_read_rays_needs_records_flag():
     d = load_scene_fixture("Rect")
     s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])

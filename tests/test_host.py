@@ -9,6 +9,7 @@ import pytest
 
 import raytracebvh_amd as rt
 from raytracebvh_amd import _lib
+from oracle import lib as orc
 from tests.conftest import REPO, load_scene_fixture
 
 
@@ -45,7 +46,7 @@ def test_obj_loader_quirks(tmp_path):
     (tmp_path / "q.obj").write_text(
         "mtllib q.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\nvn 0 0 -1\nvt 0 0\n"
         "usemtl B\nf 1/1/1 2/1/1 3/1/1\nusemtl A\nf 1/1/2 2/1/2 3/1/1\n")
-    s = rt.load_obj(str(tmp_path / "q.obj"))
+    s = rt.load_obj(str(tmp_path / "q.obj"), load_textures=False)
     assert len(s.vertices) == 3                      # normals differing only in z merged
     np.testing.assert_array_equal(s.indices, [0, 1, 2, 0, 1, 2])
     np.testing.assert_array_equal(s.mat_indices, [1, 0])
@@ -118,3 +119,64 @@ def test_create_without_gpu_fails_cleanly():
     with pytest.raises(rt.RtbvhError) as e:
         rt.Context()
     assert e.value.status == _lib.ERR_NO_DEVICE
+
+
+# ---------------------------------------------------------------- textures
+def _bmp_cases(tmp_path):
+    from PIL import Image
+    rng = np.random.default_rng(5)
+    rgb = rng.integers(0, 256, (13, 21, 3), dtype=np.uint8)          # odd width: row padding
+    cases = {"rgb24.bmp": Image.fromarray(rgb, "RGB")}
+    pal = Image.fromarray(rng.integers(0, 256, (9, 17), dtype=np.uint8), "L").convert("P")
+    cases["pal8.bmp"] = pal
+    cases["bw1.bmp"] = Image.fromarray((rng.integers(0, 2, (7, 11)) * 255).astype(np.uint8), "L").convert("1")
+    out = []
+    for name, im in cases.items():
+        p = tmp_path / name
+        im.save(p)
+        out.append((str(p), np.asarray(im.convert("RGBA"))))
+    return out
+
+
+def test_bmp_decoder_matches_pil(tmp_path):
+    """rtbvh_texture_load_bmp returns the file's rows in storage order (bottom-up), as
+    DevIL does without IL_ORIGIN_SET (Image.cpp:48-49): PIL's top-down image flipped."""
+    from raytracebvh_amd.scene import load_texture
+    for path, want in _bmp_cases(tmp_path):
+        got = load_texture(path)
+        np.testing.assert_array_equal(got, want[::-1], err_msg=path)
+
+
+def test_bmp_decoder_on_reference_textures():
+    """The reference's own texture files (Obj/*.bmp): 8-bit paletted and 24-bit."""
+    from raytracebvh_amd.scene import load_texture
+    from PIL import Image
+    obj = os.path.join("/root/reference", "Obj")
+    if not os.path.isdir(obj):
+        pytest.skip("reference tree not present")
+    for name in ("Balls.bmp", "Map__1_Composite.bmp"):
+        got = load_texture(os.path.join(obj, name))
+        want = np.asarray(Image.open(os.path.join(obj, name)).convert("RGBA"))
+        np.testing.assert_array_equal(got, want[::-1], err_msg=name)
+
+
+def test_srgb_table_and_sampler_properties():
+    from raytracebvh_amd.scene import srgb_table
+    tab = srgb_table()
+    c = np.arange(256) / 255.0
+    ref = np.where(c <= 0.04045, c / 12.92, ((c + 0.055) / 1.055) ** 2.4).astype(np.float32)
+    np.testing.assert_array_equal(tab, ref)
+    assert tab[0] == 0 and tab[255] == 1 and (np.diff(tab) > 0).all()
+    rng = np.random.default_rng(9)
+    tex = rng.integers(0, 256, (5, 7, 4), dtype=np.uint8)
+    H, W = tex.shape[:2]
+    lin = np.concatenate([tab[tex[..., :3]], (tex[..., 3:4].astype(np.float32) / np.float32(255))], -1)
+    for y in range(H):          # texel centres return the decoded texel exactly
+        for x in range(W):
+            u, v = np.float32((x + 0.5) / W), np.float32((y + 0.5) / H)
+            np.testing.assert_array_equal(orc.sample_texture(tex, u, v), lin[y, x])
+    for u, v in [(0.125, 0.75), (0.5, 0.5), (0.9375, 0.0625)]:   # wrap: period 1 (dyadic: exact in f32)
+        np.testing.assert_array_equal(orc.sample_texture(tex, u, v), orc.sample_texture(tex, u + 2.0, v - 3.0))
+    # halfway between two texel centres along x: the mean of the two (lerp at 0.5)
+    u, v = np.float32(1.0 / W), np.float32(0.5 / H)
+    np.testing.assert_allclose(orc.sample_texture(tex, u, v), (lin[0, 0] + lin[0, 1]) / 2, rtol=1e-6)
