@@ -196,6 +196,15 @@ rtbvh_status rtbvh_synchronize(rtbvh_ctx* ctx);
 rtbvh_status rtbvh_read_framebuffer(rtbvh_ctx* ctx, float* rgba);
 /* Final reflectRay[].intensity per pixel (W*H floats). */
 rtbvh_status rtbvh_read_intensity(rtbvh_ctx* ctx, float* intensity);
+/* What the presentation pass shows (RayTraceBVHPS.hlsl:13-16 into the R8G8B8A8_UNORM swap
+ * chain, Graphics.cpp:163): screen row y (top = 0) is framebuffer row H-1-y (the shader's
+ * index at pixel centres), each channel floor(saturate(c) * 255 + 0.5).  W*H*4 bytes, of
+ * the last full-frame trace (not of a band trace). */
+rtbvh_status rtbvh_present(rtbvh_ctx* ctx, uint8_t* rgba8);
+/* SaveBMP (SaveBMP.cpp:3-62): 24-bit BI_RGB file, 0x0ec4 pixels per metre, rows bottom-up;
+ * `rgba8` is a presented image (top row first).  Rows are padded to 4 bytes as BMP
+ * requires (the reference writes them unpadded; identical when 3*W is a multiple of 4). */
+rtbvh_status rtbvh_save_bmp(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height);
 /* Device pointer of the W*H*4-float framebuffer (valid until the next trace/destroy). */
 const float* rtbvh_framebuffer_device(rtbvh_ctx* ctx);
 /* BVHTree UAV u0 in the reference layout (2n-1 nodes, see rtbvh_node). */

@@ -35,6 +35,7 @@ EXPORTS = [
     "rtbvh_scene_num_materials", "rtbvh_scene_num_textures", "rtbvh_scene_vertices", "rtbvh_scene_indices",
     "rtbvh_scene_mat_indices", "rtbvh_scene_materials", "rtbvh_scene_texture_path", "rtbvh_set_scene_obj",
     "rtbvh_camera_reference", "rtbvh_texture_load_bmp", "rtbvh_texture_free", "rtbvh_srgb_table",
+    "rtbvh_present", "rtbvh_save_bmp",
 ]
 
 NODE_DTYPE = np.dtype([("parent", "<u4"), ("child_l", "<u4"), ("child_r", "<u4"), ("code", "<u4"),
@@ -146,6 +147,8 @@ def lib() -> ctypes.CDLL:
         "rtbvh_texture_load_bmp": (i32, [ctypes.c_char_p, vp]),
         "rtbvh_texture_free": (None, [vp]),
         "rtbvh_srgb_table": (None, [vp]),
+        "rtbvh_present": (i32, [vp, vp]),
+        "rtbvh_save_bmp": (i32, [ctypes.c_char_p, vp, u32, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -579,6 +579,25 @@ rtbvh_status rtbvh_read_bvh(rtbvh_ctx* c, rtbvh_node* out, uint32_t capacity) {
     return RTBVH_OK;
 }
 
+rtbvh_status rtbvh_present(rtbvh_ctx* c, uint8_t* rgba8) {
+    if (!c || !rgba8) return RTBVH_ERR_INVALID_ARG;
+    if (!c->traced || c->nranks != 1) return fail(c, RTBVH_ERR_NOT_READY, "present: no full-frame trace yet");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const size_t n = (size_t)c->W * c->H;
+    uint32_t* d = nullptr;
+    HIPC(c, hipMallocAsync((void**)&d, n * 4, c->stream));
+    launch_present(c->d_color, c->W, c->H, d, c->stream);
+    hipError_t e1 = hipGetLastError();
+    hipError_t e2 = hipMemcpyAsync(rgba8, d, n * 4, hipMemcpyDeviceToHost, c->stream);
+    hipError_t e3 = hipFreeAsync(d, c->stream);
+    hipError_t e4 = hipStreamSynchronize(c->stream);
+    HIPC(c, e1);
+    HIPC(c, e2);
+    HIPC(c, e3);
+    HIPC(c, e4);
+    return RTBVH_OK;
+}
+
 rtbvh_status rtbvh_read_wide(rtbvh_ctx* c, uint32_t* out, uint64_t capacity) {
     if (!c || !out) return RTBVH_ERR_INVALID_ARG;
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "no build yet");

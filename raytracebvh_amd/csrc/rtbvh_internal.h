@@ -97,6 +97,8 @@ void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t*
                             uint32_t refill_min, uint32_t chunk, hipStream_t s);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
+// presentation pass (RayTraceBVHPS.hlsl): flipped rows, UNORM8 RGBA
+void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, hipStream_t s);
 // coherence sort keys of a bounce queue: P entries (past *count: key 0xFFFFFFFF)
 void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, uint32_t P, uint32_t* keys,
                         uint32_t* vals, hipStream_t s);

@@ -434,6 +434,35 @@ rtbvh_status rtbvh_texture_load_bmp(const char* path, rtbvh_texture* out) {
     return RTBVH_OK;
 }
 
+rtbvh_status rtbvh_save_bmp(const char* path, const uint8_t* rgba8, uint32_t W, uint32_t H) {
+    if (!path || !rgba8 || W == 0 || H == 0 || W > 65535 || H > 65535) return RTBVH_ERR_INVALID_ARG;
+    const uint32_t stride = (3 * W + 3) & ~3u, size = stride * H;
+    uint8_t hdr[54] = {0};
+    auto put32 = [&](int o, uint32_t v) { hdr[o] = v; hdr[o + 1] = v >> 8; hdr[o + 2] = v >> 16; hdr[o + 3] = v >> 24; };
+    hdr[0] = 'B'; hdr[1] = 'M';                       // bfType 0x4d42
+    put32(2, 54 + size);                              // bfSize
+    put32(10, 0x36);                                  // bfOffBits
+    put32(14, 40);                                    // biSize
+    put32(18, W); put32(22, H);                       // positive height: bottom-up rows
+    hdr[26] = 1; hdr[28] = 24;                        // planes, 24 bpp, BI_RGB
+    put32(34, 0);                                     // biSizeImage 0
+    put32(38, 0x0ec4); put32(42, 0x0ec4);             // pixels per metre (SaveBMP.cpp:26-27)
+    std::ofstream f(path, std::ios::binary);
+    if (!f) return RTBVH_ERR_IO;
+    f.write((const char*)hdr, 54);
+    std::vector<uint8_t> row(stride, 0);
+    for (uint32_t r = 0; r < H; r++) {                // file row r = image row H-1-r
+        const uint8_t* src = rgba8 + (size_t)(H - 1 - r) * W * 4;
+        for (uint32_t x = 0; x < W; x++) {
+            row[3 * x + 0] = src[4 * x + 2];
+            row[3 * x + 1] = src[4 * x + 1];
+            row[3 * x + 2] = src[4 * x + 0];
+        }
+        f.write((const char*)row.data(), stride);
+    }
+    return f ? RTBVH_OK : RTBVH_ERR_IO;
+}
+
 void rtbvh_texture_free(rtbvh_texture* tex) {
     if (!tex) return;
     std::free((void*)tex->rgba8);

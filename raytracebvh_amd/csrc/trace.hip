@@ -1032,6 +1032,17 @@ void launch_bounce_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_co
                        qout_count, (int)emit);
 }
 
+// RayTraceBVHPS.hlsl:13-16 + the R8G8B8A8_UNORM target: screen row y <- framebuffer row H-1-y
+__device__ __forceinline__ uint32_t unorm8(float c) { return (uint32_t)floorf(sat(c) * 255.f + .5f); }
+__global__ __launch_bounds__(BLOCK) void k_present(const float4* __restrict__ color, uint32_t W, uint32_t H,
+                                                   uint32_t* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= (size_t)W * H) return;
+    const uint32_t y = (uint32_t)(i / W), x = (uint32_t)(i % W);
+    const float4 c = color[(size_t)(H - 1 - y) * W + x];
+    out[i] = unorm8(c.x) | unorm8(c.y) << 8 | unorm8(c.z) << 16 | unorm8(c.w) << 24;
+}
+
 template <bool COUNT, int S>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           int mode, float2* hitrec, uint32_t* next, uint32_t refill_min, uint32_t chunk,
@@ -1107,6 +1118,11 @@ void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qi
     else
         hipLaunchKernelGGL((k_bounce_shade<false>), dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a, qin,
                            qin_count, hitrec, qout, qout_count, (int)emit);
+}
+
+void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, hipStream_t s) {
+    const size_t n = (size_t)W * H;
+    if (n) hipLaunchKernelGGL(k_present, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, color, W, H, out);
 }
 
 }  // namespace rtbvh

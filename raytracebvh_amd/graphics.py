@@ -9,6 +9,7 @@ and meanings over librtbvh.so; `Context` is the thin 1:1 wrapper of the C ABI.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -114,6 +115,12 @@ class Context:
         self._check(_L.lib().rtbvh_read_rays(self._h, _L.ptr(refl), _L.ptr(refr)))
         return refl, refr
 
+    def present(self) -> np.ndarray:
+        """The image the pixel shader shows (RayTraceBVHPS.hlsl:13-16): (H, W, 4) uint8, top row first."""
+        out = np.zeros((self.height, self.width, 4), np.uint8)
+        self._check(_L.lib().rtbvh_present(self._h, _L.ptr(out)))
+        return out
+
     def read_intensity(self) -> np.ndarray:
         out = np.zeros((self.height, self.width), np.float32)
         self._check(_L.lib().rtbvh_read_intensity(self._h, _L.ptr(out)))
@@ -209,5 +216,19 @@ class Graphics:
         """reflectRay[].color as (H, W, 4) f32 (the framebuffer of record, RayTraceBVHPS.hlsl:13-16)."""
         return self.ctx.read_framebuffer()
 
+    def onRender(self) -> np.ndarray:  # noqa: N802
+        """Graphics::onRender's frame (the presentation pass) as RGBA8."""
+        return self.ctx.present()
+
+    def save_bmp(self, path: str):
+        """SaveBMP (SaveBMP.cpp:3-62) of the presented frame."""
+        save_bmp(path, self.onRender())
+
     def onDestroy(self):  # noqa: N802
         self.ctx.close()
+
+
+def save_bmp(path: str, rgba8: np.ndarray):
+    """rtbvh_save_bmp: 24-bit BMP of an (H, W, 4) uint8 image, top row first."""
+    img = np.ascontiguousarray(rgba8, dtype=np.uint8)
+    _L.check(_L.lib().rtbvh_save_bmp(os.fsencode(path), _L.ptr(img), img.shape[1], img.shape[0]))

@@ -296,6 +296,20 @@ def test_textured_frames_match_oracle(name, W, H, bounces):
     assert not np.array_equal(white, ofb)
 
 
+def test_present_is_flipped_unorm8_framebuffer():
+    """RayTraceBVHPS.hlsl:13-16 into R8G8B8A8_UNORM: screen row y = framebuffer row H-1-y."""
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"], textures=_textures())
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(640, 360))
+        c.compute_bvh(640, 360, 1)
+        fb = c.read_framebuffer()
+        img = c.present()
+    want = np.floor(np.clip(fb, 0, 1) * np.float32(255) + np.float32(0.5)).astype(np.uint8)[::-1]
+    np.testing.assert_array_equal(img, want)
+
+
 def test_read_rays_needs_records_flag():
     d = load_scene_fixture("Rect")
     s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])

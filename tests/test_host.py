@@ -180,3 +180,18 @@ def test_srgb_table_and_sampler_properties():
     # halfway between two texel centres along x: the mean of the two (lerp at 0.5)
     u, v = np.float32(1.0 / W), np.float32(0.5 / H)
     np.testing.assert_allclose(orc.sample_texture(tex, u, v), (lin[0, 0] + lin[0, 1]) / 2, rtol=1e-6)
+
+
+def test_save_bmp_roundtrip(tmp_path):
+    """rtbvh_save_bmp (SaveBMP.cpp:3-62 layout): PIL reads back the image, padded and unpadded widths."""
+    from PIL import Image
+    rng = np.random.default_rng(11)
+    for W, H in ((5, 3), (8, 4)):
+        img = rng.integers(0, 256, (H, W, 4), dtype=np.uint8)
+        p = str(tmp_path / f"o{W}.bmp")
+        rt.save_bmp(p, img)
+        back = np.asarray(Image.open(p).convert("RGB"))
+        np.testing.assert_array_equal(back, img[..., :3])
+        hdr = open(p, "rb").read(54)
+        assert hdr[:2] == b"BM" and int.from_bytes(hdr[10:14], "little") == 0x36
+        assert int.from_bytes(hdr[38:42], "little") == 0x0EC4 and hdr[28] == 24
