@@ -209,11 +209,12 @@ rtbvh_status rtbvh_save_bmp(const char* path, const uint8_t* rgba8, uint32_t wid
 const float* rtbvh_framebuffer_device(rtbvh_ctx* ctx);
 /* BVHTree UAV u0 in the reference layout (2n-1 nodes, see rtbvh_node). */
 rtbvh_status rtbvh_read_bvh(rtbvh_ctx* ctx, rtbvh_node* out, uint32_t capacity);
-/* Node records in slots (the layout both traversal walks read): 2(n-1) records of 16 u32,
- * record 2p+side = {box of child c's left child (min xyz, max xyz), box of its right child,
- * id_l, id_r, c, 0} for c = child `side` of internal node p; ids: internal k, or
- * 0x80000000|j for sorted leaf j; a leaf child c gives {its box, its box, 0x80000000|c, ~0u,
- * 0x80000000|c, 0}.  (The root's record follows at slot 2(n-1).) */
+/* Node records in slots (the layout every traversal walk reads): 2(n-1) records of 16 u32;
+ * record 2p+side belongs to c = child `side` of internal node p and holds the boxes of
+ * c's children L and R as words {L.min.x, L.min.y, L.max.x, L.max.y, R.min.x, R.min.y,
+ * R.max.x, R.max.y, L.min.z, L.max.z, R.min.z, R.max.z, id_L, id_R, c, 0}; ids: internal k,
+ * or 0x80000000|j for sorted leaf j.  A leaf child c holds {its box as L and as R,
+ * 0x80000000|c, ~0u, 0x80000000|c, 0}.  (The root's record follows at slot 2(n-1).) */
 rtbvh_status rtbvh_read_wide(rtbvh_ctx* ctx, uint32_t* records, uint64_t capacity);
 /* Per-triangle Morton codes in triangle order (MortonCodes.hlsl:104-112). */
 rtbvh_status rtbvh_read_morton(rtbvh_ctx* ctx, uint32_t* codes);

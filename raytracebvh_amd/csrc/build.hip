@@ -248,14 +248,22 @@ __device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
     hi = mk(__uint_as_float((uint32_t)(b >> 32)), __uint_as_float((uint32_t)c), __uint_as_float((uint32_t)(c >> 32)));
 }
 
-// the complete record of node p: its children's boxes (left, right), their ids, p itself
+// the complete record of node p (word layout: rtbvh_device.h "node record"): its
+// children's boxes with each corner's (x, y) as an aligned pair, their ids, p itself
 __device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
                                              uint32_t cr, uint32_t own) {
     float4* d = reinterpret_cast<float4*>(dst);
-    d[0] = make_float4(lmin.x, lmin.y, lmin.z, lmax.x);
-    d[1] = make_float4(lmax.y, lmax.z, rmin.x, rmin.y);
-    d[2] = make_float4(rmin.z, rmax.x, rmax.y, rmax.z);
+    d[0] = make_float4(lmin.x, lmin.y, lmax.x, lmax.y);
+    d[1] = make_float4(rmin.x, rmin.y, rmax.x, rmax.y);
+    d[2] = make_float4(lmin.z, lmax.z, rmin.z, rmax.z);
     d[3] = make_float4(__uint_as_float(cl), __uint_as_float(cr), __uint_as_float(own), 0.f);
+}
+// box of child `side` from a node record: min xyz, max xyz
+__device__ __forceinline__ void record_box(const Inner* r, uint32_t side, float out[6]) {
+    const float* w = reinterpret_cast<const float*>(r);
+    const int b = side ? 4 : 0, z = side ? 10 : 8;
+    out[0] = w[b]; out[1] = w[b + 1]; out[2] = w[z];
+    out[3] = w[b + 2]; out[4] = w[b + 3]; out[5] = w[z + 1];
 }
 __device__ __forceinline__ uint32_t slot_of(uint32_t parent_code, uint32_t T) {
     return parent_code == INVALID ? 2 * T - 2 : parent_code;
@@ -367,7 +375,7 @@ __global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restri
     const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
     if (r >= 2 * T - 1) return;
     RefNode o;
-    const float* box;
+    float box[6];
     uint32_t e;
     if (r < T) {
         e = T == 1 ? INVALID : a.pleaf[r];
@@ -386,11 +394,10 @@ __global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restri
     }
     if (e == INVALID) {
         o.parent = INVALID;
-        box = a.rootbox;
+        for (int k = 0; k < 6; k++) box[k] = a.rootbox[k];
     } else {
         o.parent = (e >> 1) + T;
-        const Inner& pr = a.rec[slot_of(a.pint[e >> 1], T)];   // the parent's record
-        box = (e & 1u) ? pr.rmin : pr.lmin;
+        record_box(a.rec + slot_of(a.pint[e >> 1], T), e & 1u, box);   // from the parent's record
     }
     for (int k = 0; k < 3; k++) { o.bb_min[k] = box[k]; o.bb_max[k] = box[3 + k]; }
     out[r] = o;

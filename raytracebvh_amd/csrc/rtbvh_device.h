@@ -7,8 +7,9 @@
 //   keys/vals u32[T] x2  radix ping-pong (Morton code, triangle id)
 //   leaf   float4[4*T]   64-B leaf records in SORTED order: {v0.xyz, e1.x}, {e1.yz, e2.xy},
 //                        {e2.z, tri, bmin.xy}, {bmin.z, bmax.xyz}; e1 = v1-v0, e2 = v2-v0
-//   rec    Inner[2T-1]   64-B node records in SLOTS: the record of internal node k (the boxes
-//                        and ids of its two children, and k itself) sits at slot
+//   rec    Inner[2T-1]   64-B node records in SLOTS (word layout below, not Inner's field
+//                        names): the record of internal node k (the boxes and ids of its
+//                        two children, and k itself) sits at slot
 //                        pint[k] = 2*parent + side, the root's at slot 2T-2; slot pleaf[j]
 //                        holds a pseudo-record {box_j, box_j, LEAF_BIT|j, INVALID} for leaf j.
 //                        So the records of two siblings share one 128-B line: the binary
@@ -18,6 +19,9 @@
 //                        box hand-off of refit nodes that span workgroups
 //   pleaf  u32[T], pint u32[T-1]   parent<<1 | side (side 0 = left child)
 // Node ids: internal k -> k, leaf j -> LEAF_BIT | j.
+// Node record words (so that each corner's (x, y) is an aligned pair for packed fp32):
+//   0-1 left.min.xy  2-3 left.max.xy  4-5 right.min.xy  6-7 right.max.xy
+//   8 left.min.z  9 left.max.z  10 right.min.z  11 right.max.z  12 id_l  13 id_r  14 own  15 0
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -30,6 +30,9 @@ constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
 
 struct Counts { uint32_t internal, leaf, overflow; };
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
 // Node records live in SLOTS (rtbvh_device.h): the binary walks keep slots on their
 // stacks.  The record of internal node k holds k's own index, so its internal
 // children's records are at slots 2k and 2k+1; a leaf child is LEAF_BIT | j.
@@ -49,6 +52,7 @@ __device__ __forceinline__ void pin(float4& a) {
     a = make_float4(x, y, z, w);
 }
 __device__ __forceinline__ void pin(float& a) { asm volatile("" : "+v"(a)); }
+__device__ __forceinline__ void pin(v4f& a) { asm volatile("" : "+v"(a)); }
 
 // rayTriangleCollision, RayTraceTraversal.hlsl:41-86, with edge1/edge2 precomputed
 // by the build (identical floats: the same single subtraction)
@@ -76,6 +80,21 @@ __device__ __forceinline__ bool ray_box(f3 o, f3 inv, float bx0, float by0, floa
     const float tx1 = (bx1 - o.x) * inv.x, ty1 = (by1 - o.y) * inv.y, tz1 = (bz1 - o.z) * inv.z;
     const float mn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
     const float mx = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    tmin = mn;
+    return 0 <= mx && mn <= mx && (!hit || mn <= best);
+}
+
+// ray_box on a node record's layout (rtbvh_device.h): the (x, y) of a box corner is an
+// aligned register pair, so the x and y slabs run as packed fp32 (v_pk_add_f32 /
+// v_pk_mul_f32: two IEEE operations per instruction, the roundings of the scalar form,
+// no contraction under -ffp-contract=off) -- the traversal kernels are VALU-issue-bound.
+__device__ __forceinline__ bool ray_box_xy(f3 o, f3 inv, f2v lo, f2v hi, float lz, float hz, bool hit, float best,
+                                           float& tmin) {
+    const f2v oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
+    const f2v t0 = (lo - oxy) * ixy, t1 = (hi - oxy) * ixy;
+    const float tz0 = (lz - o.z) * inv.z, tz1 = (hz - o.z) * inv.z;
+    const float mn = fmaxf(fmaxf(fminf(t0.x, t1.x), fminf(t0.y, t1.y)), fminf(tz0, tz1));
+    const float mx = fminf(fminf(fmaxf(t0.x, t1.x), fmaxf(t0.y, t1.y)), fmaxf(tz0, tz1));
     tmin = mn;
     return 0 <= mx && mn <= mx && (!hit || mn <= best);
 }
@@ -116,13 +135,13 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
             continue;
         }
         if (COUNT) c.internal++;
-        const float4* r = reinterpret_cast<const float4*>(inner + node);
-        const float4 q0 = r[0], q1 = r[1], q2 = r[2];
+        const v4f* r = reinterpret_cast<const v4f*>(inner + node);
+        const v4f q0 = r[0], q1 = r[1], q2 = r[2];
         const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
         const uint32_t cl = child_slot(q3.x, q3.z, 0), cr = child_slot(q3.y, q3.z, 1);
         float tl, tr;
-        const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
-        const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
+        const bool lh = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, tl);
+        const bool rh = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, tr);
         if (!lh && !rh) {
             node = top;                                 // pop
             if (--sp >= 0) top = stack[sp];
@@ -177,13 +196,13 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
             continue;
         }
         if (COUNT) c.internal++;
-        const float4* r = reinterpret_cast<const float4*>(inner + node);
-        const float4 q0 = r[0], q1 = r[1], q2 = r[2];
+        const v4f* r = reinterpret_cast<const v4f*>(inner + node);
+        const v4f q0 = r[0], q1 = r[1], q2 = r[2];
         const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
         const uint32_t cl = child_slot(q3.x, q3.z, 0), cr = child_slot(q3.y, q3.z, 1);
         float tl, tr;
-        const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
-        const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
+        const bool lh = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, tl);
+        const bool rh = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, tr);
         if (!lh && !rh) {
             node = stack[sp--];
         } else {
@@ -208,7 +227,6 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
 // order, and nothing changes its state in between), so results and per-lane visit
 // counts are identical to the per-lane DFS.  In nearest-first mode the wave takes
 // the child most of its lanes see first.
-typedef float v4f __attribute__((ext_vector_type(4)));
 typedef const v4f __attribute__((address_space(4))) cv4f;
 
 typedef float v16f __attribute__((ext_vector_type(16)));
@@ -260,8 +278,8 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
             float tl = 0.f, tr = 0.f;
             if (mask & lanebit) {
                 if (COUNT) c.internal++;
-                lh = ray_box(o, inv, q[0], q[1], q[2], q[3], q[4], q[5], hit, best, tl);
-                rh = ray_box(o, inv, q[6], q[7], q[8], q[9], q[10], q[11], hit, best, tr);
+                lh = ray_box_xy(o, inv, q.s01, q.s23, q[8], q[9], hit, best, tl);
+                rh = ray_box_xy(o, inv, q.s45, q.s67, q[10], q[11], hit, best, tr);
             }
             const uint64_t ml = __ballot(lh), mr = __ballot(rh);
             if ((ml | mr) == 0) {
@@ -356,10 +374,10 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             float t[4] = {0.f, 0.f, 0.f, 0.f};
             if (mask & lanebit) {
                 if (COUNT) c.internal++;
-                h[0] = ray_box(o, inv, A[0], A[1], A[2], A[3], A[4], A[5], hit, best, t[0]);
-                h[1] = ray_box(o, inv, A[6], A[7], A[8], A[9], A[10], A[11], hit, best, t[1]) & (id[1] != INVALID);
-                h[2] = ray_box(o, inv, B[0], B[1], B[2], B[3], B[4], B[5], hit, best, t[2]);
-                h[3] = ray_box(o, inv, B[6], B[7], B[8], B[9], B[10], B[11], hit, best, t[3]) & (id[3] != INVALID);
+                h[0] = ray_box_xy(o, inv, A.s01, A.s23, A[8], A[9], hit, best, t[0]);
+                h[1] = ray_box_xy(o, inv, A.s45, A.s67, A[10], A[11], hit, best, t[1]) & (id[1] != INVALID);
+                h[2] = ray_box_xy(o, inv, B.s01, B.s23, B[8], B[9], hit, best, t[2]);
+                h[3] = ray_box_xy(o, inv, B.s45, B.s67, B[10], B[11], hit, best, t[3]) & (id[3] != INVALID);
             }
             uint64_t m[4];
 #pragma unroll
@@ -812,10 +830,10 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         // (leaf and child-pair records are both 64-B aligned records of 64 B; the
         // 4-wide record pair adds a second 64 B for internal lanes)
         const bool isleaf = (node & LEAF_BIT) != 0;
-        const float4* rr = isleaf ? leaf + 4 * (size_t)(node & ~LEAF_BIT)
-                                  : reinterpret_cast<const float4*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
-        float4 q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
-        float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f), q5 = q4, q6 = q4, q7 = q4;
+        const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(node & ~LEAF_BIT))
+                               : reinterpret_cast<const v4f*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
+        v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
+        v4f q4 = {0.f, 0.f, 0.f, 0.f}, q5 = q4, q6 = q4, q7 = q4;
         if (WIDE && !isleaf) {
             q4 = rr[4]; q5 = rr[5]; q6 = rr[6]; q7 = rr[7];
         }
@@ -826,7 +844,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             done = true;
         } else if (isleaf) {
             const uint32_t j = node & ~LEAF_BIT;
-            const float4 la = q0, lb = q1;
+            const v4f la = q0, lb = q1;
             const float e2z = q2.x;
             if (COUNT) c.leaf++;
             const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
@@ -844,14 +862,14 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             }
         } else if (WIDE) {
             if (COUNT) c.internal++;
-            const float4 a0 = q0, a1 = q1, a2 = q2, b0 = q4, b1 = q5, b2 = q6;
+            // record pair: q0..q3 = the record of the left child, q4..q7 of the right one
             const uint4 a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
             const uint4 b3 = make_uint4(__float_as_uint(q7.x), __float_as_uint(q7.y), 0u, 0u);
             float t0, t1, t2, t3;
-            const bool h0 = ray_box(o, inv, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, hit, best, t0);
-            const bool h1 = ray_box(o, inv, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, hit, best, t1) & (a3.y != INVALID);
-            const bool h2 = ray_box(o, inv, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, hit, best, t2);
-            const bool h3 = ray_box(o, inv, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, hit, best, t3) & (b3.y != INVALID);
+            const bool h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, t0);
+            const bool h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, t1) & (a3.y != INVALID);
+            const bool h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, hit, best, t2);
+            const bool h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, hit, best, t3) & (b3.y != INVALID);
             const float INF = __builtin_inff();
             float k0 = h0 ? t0 : INF, k1 = h1 ? t1 : INF, k2 = h2 ? t2 : INF, k3 = h3 ? t3 : INF;
             uint32_t i0 = h0 ? a3.x : INVALID, i1 = h1 ? a3.y : INVALID, i2 = h2 ? b3.x : INVALID,
@@ -876,8 +894,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             const uint32_t own = __float_as_uint(q3.z);
             const uint32_t cl = child_slot(__float_as_uint(q3.x), own, 0), cr = child_slot(__float_as_uint(q3.y), own, 1);
             float tl, tr;
-            const bool lh = ray_box(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hit, best, tl);
-            const bool rh = ray_box(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hit, best, tr);
+            const bool lh = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, tl);
+            const bool rh = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, tr);
             if (!lh && !rh) {
                 node = top;                             // pop
                 spop_top();

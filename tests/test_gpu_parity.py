@@ -382,22 +382,28 @@ def test_wide_view_records_match_binary_tree():
     assert w4.shape == (2 * (T - 1), 16)
     f = w4.view(np.float32)
     par = nodes["parent"]
+
+    def box(rec, side):   # (min xyz, max xyz) of child `side` in the record word layout
+        b, z = (4, 10) if side else (0, 8)
+        return np.array([rec[b], rec[b + 1], rec[z]]), np.array([rec[b + 2], rec[b + 3], rec[z + 1]])
+
     for k in (x for x in range(2 * T - 1) if x != T):   # every node but the root (reference layout: root = T)
         e = par[k] - T                       # parent internal index
         side = 0 if nodes["child_l"][par[k]] == k else 1
-        rec = w4[2 * e + side]
+        rec, fr = w4[2 * e + side], f[2 * e + side]
         if k < T:   # leaf
             assert rec[12] == (0x80000000 | k) and rec[13] == 0xFFFFFFFF and rec[14] == (0x80000000 | k)
-            np.testing.assert_array_equal(f[2 * e + side][0:3], nodes["bb_min"][k])
-            np.testing.assert_array_equal(f[2 * e + side][3:6], nodes["bb_max"][k])
+            lo, hi = box(fr, 0)
+            np.testing.assert_array_equal(lo, nodes["bb_min"][k])
+            np.testing.assert_array_equal(hi, nodes["bb_max"][k])
         else:
             cl, cr = nodes["child_l"][k], nodes["child_r"][k]
             ids = [(0x80000000 | x) if x < T else x - T for x in (cl, cr)]
             assert list(rec[12:15]) == ids + [k - T]
-            np.testing.assert_array_equal(f[2 * e + side][0:3], nodes["bb_min"][cl])
-            np.testing.assert_array_equal(f[2 * e + side][3:6], nodes["bb_max"][cl])
-            np.testing.assert_array_equal(f[2 * e + side][6:9], nodes["bb_min"][cr])
-            np.testing.assert_array_equal(f[2 * e + side][9:12], nodes["bb_max"][cr])
+            for sd, ch in ((0, cl), (1, cr)):
+                lo, hi = box(fr, sd)
+                np.testing.assert_array_equal(lo, nodes["bb_min"][ch])
+                np.testing.assert_array_equal(hi, nodes["bb_max"][ch])
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
