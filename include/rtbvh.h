@@ -145,6 +145,10 @@ typedef struct {
     float ms_build, ms_trace;
     float ms_stage[8];   /* bounds, morton, sort, leaf+karras, refit, primary, bounce (all passes),
                             first bounce pass's traversal kernel (RTBVH_FLAG_REFILL_BOUNCE) */
+    /* RTBVH_FLAG_COUNT_VISITS with RTBVH_FLAG_REFILL_BOUNCE: wave iterations of the bounce
+     * traversal, those with both a leaf lane and an internal-node lane, and active lanes
+     * summed over iterations (lane utilisation = active_lanes / (64 * wave_steps)) */
+    uint64_t trav_wave_steps, trav_mixed_steps, trav_active_lanes;
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 

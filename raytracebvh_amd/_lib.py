@@ -64,7 +64,8 @@ class Stats(ctypes.Structure):
                 ("hits", ctypes.c_uint64 * 2), ("textured_hits", ctypes.c_uint64),
                 ("stack_overflows", ctypes.c_uint64), ("timed_builds", ctypes.c_uint32),
                 ("timed_traces", ctypes.c_uint32), ("ms_build", ctypes.c_float), ("ms_trace", ctypes.c_float),
-                ("ms_stage", ctypes.c_float * 8)]
+                ("ms_stage", ctypes.c_float * 8), ("trav_wave_steps", ctypes.c_uint64),
+                ("trav_mixed_steps", ctypes.c_uint64), ("trav_active_lanes", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         d = {}

@@ -235,10 +235,13 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     // ... and of the refill policy (idle lanes that trigger it, rays per atomic claim):
     // 5 -> (16, none), 6 -> (8, 128), 7 -> (16, 128), 8 -> (8, 256), 9 -> (16, 64), 10 -> (4, 128);
     // default (32, none)
-    const uint32_t refill_min = vsel == 5 ? 16 : vsel == 6 ? 8 : vsel == 7 ? 16 : vsel == 8 ? 8 : vsel == 9 ? 16
-                              : vsel == 10 ? 4 : 0;
-    const uint32_t chunk = vsel == 6 || vsel == 7 || vsel == 10 ? 128 : vsel == 8 ? 256 : vsel == 9 ? 64 : 0;
-    const int bmode = wide ? 2 : (variant == 1 ? 1 : 0);
+    const uint32_t refill_min = vsel == 8 ? 8 : vsel == 9 ? 16 : vsel == 10 ? 4 : 0;
+    uint32_t chunk = vsel == 10 ? 128 : vsel == 8 ? 256 : vsel == 9 ? 64 : 0;
+    if (vsel == 13) chunk = 22u << 24;   // A/B: +22 KB LDS per block -> 4 blocks (4 waves/SIMD) per CU
+    if (vsel == 14) chunk = 9u << 24;    // A/B: +9 KB -> 6 blocks per CU
+    // A/B of postponed leaves in the 4-wide bounce walk: variant 15 -> batch 16, 2 -> ... (see below)
+    const uint32_t leaf_batch = vsel == 15 ? 16 : vsel == 5 ? 8 : vsel == 6 ? 24 : vsel == 7 ? 32 : 16;
+    const int bmode = wide ? ((vsel == 15 || (vsel >= 5 && vsel <= 7)) ? 3 : 2) : (variant == 1 ? 1 : 0);
     if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1)
         pvariant = wide ? 5 : (variant == 1 ? 4 : 3);
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
@@ -264,7 +267,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (refill) {
             if (timing && b == 0) HIPC(c, hipEventRecord(ev[3], s));
             launch_bounce_traverse(a, c->d_q[b & 1], &c->d_qcount[b], perm, count, bmode, c->d_hit,
-                                   &c->d_qcount[16 + b], lds_stack, refill_min, chunk, s);
+                                   &c->d_qcount[16 + b], lds_stack, refill_min, chunk, leaf_batch, s);
             if (timing && b == 0) HIPC(c, hipEventRecord(ev[4], s));
             launch_bounce_shade(a, c->d_q[b & 1], &c->d_qcount[b], c->d_hit, c->d_q[(b + 1) & 1],
                                 &c->d_qcount[b + 1], count, b + 1 < bounces, P, s);
@@ -688,6 +691,9 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         }
         out->stack_overflows = cnt[8];
         out->textured_hits = cnt[9];
+        out->trav_wave_steps = cnt[10];
+        out->trav_mixed_steps = cnt[11];
+        out->trav_active_lanes = cnt[12];
     }
     return RTBVH_OK;
 }

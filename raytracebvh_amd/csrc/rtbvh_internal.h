@@ -89,12 +89,13 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
                    uint32_t* qout_count, bool count, bool emit, int variant, hipStream_t s);
 // bounce pass as persistent refill traversal (hit records) + shading kernel; `next` is a
-// zeroed work counter; mode 0 reference order, 1 nearest-first, 2 nearest-first on inner4;
+// zeroed work counter; mode 0 reference order, 1 nearest-first, 2 nearest-first 4-wide,
+// 3 = 2 with postponed leaves (leaf_batch parked leaves start a leaf phase);
 // lds_stack = stack entries kept in LDS (0, 8, 16, 20); refill_min = idle lanes that trigger a
 // refill (0: default); chunk = rays one work-counter atomic claims for the wave (0: as many as idle)
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
-                            uint32_t refill_min, uint32_t chunk, hipStream_t s);
+                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, hipStream_t s);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
 // presentation pass (RayTraceBVHPS.hlsl): flipped rows, UNORM8 RGBA

@@ -741,13 +741,19 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          uint32_t refill_min, uint32_t chunk) {
-    constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
+                                                          uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch) {
+    // MODE 3 = MODE 2 with postponed leaves: a lane that reaches a leaf parks it (one per
+    // lane) and keeps walking; leaf tests run only in "leaf phases" -- when leaf_batch
+    // lanes hold a parked leaf, or a lane cannot go on without testing its leaf.  Census
+    // (C5): 90% of wave iterations held both leaf and internal lanes, so the triangle
+    // test's VALU ran in nearly every iteration for ~6 of 44 lanes.  The kept answer is
+    // the (t, leaf) minimum over every leaf whose box was hit, as in MODE 2.
+    constexpr bool NEAREST = MODE >= 1, WIDE = MODE >= 2, POSTPONE = MODE == 3;
     const uint32_t n = *qin_count;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0};
     bool has = false, hit = false;
-    uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
+    uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0, pend = INVALID;
     int sp = 0;
     float best = 0.f;
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
@@ -777,6 +783,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     // global counter (chunks lost to the plain threshold in the A/B above: the tail
     // of the last claimed chunks outweighs the saved atomics)
     uint32_t cnext = 0, cend = 0;
+    unsigned long long wsteps = 0, mixed = 0, active_lanes = 0;
     while (true) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -807,6 +814,11 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                     sp = 0;
                     top = INVALID;
                     node = WIDE ? ((T == 1) ? LEAF_BIT : 0u) : root_slot(T);
+                    pend = INVALID;
+                    if (POSTPONE && T == 1) {   // a one-leaf tree: the leaf is parked, no node
+                        pend = LEAF_BIT;
+                        node = INVALID;
+                    }
                     guard = 2 * T + 2;
                 }
             }
@@ -823,14 +835,29 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         // every refill either hands out a ray or moves toward `drained`, so a wave with no
         // ray left loops back to refill until the queue is drained
         if (__ballot(has) == 0 && drained) break;
+        if (COUNT) {   // wave-level divergence census (stats trav_*; all lanes converged here)
+            const uint64_t act = __ballot(has);
+            const uint64_t lf = __ballot(has && (node & LEAF_BIT) != 0);
+            wsteps++;
+            active_lanes += (uint32_t)__popcll(act);
+            mixed += (lf != 0 && lf != act);
+        }
+        bool do_leaf = false;   // POSTPONE: this lane tests its parked leaf in this iteration
+        if (POSTPONE) {         // wave-uniform phase choice (all lanes converged here)
+            const bool blocked = has && ((node & LEAF_BIT) != 0 || (node == INVALID && pend != INVALID));
+            const uint64_t bm = __ballot(blocked);
+            const uint32_t np = (uint32_t)__popcll(__ballot(has && pend != INVALID));
+            do_leaf = has && pend != INVALID && (bm != 0 || np >= leaf_batch);
+        }
         if (!has) continue;
         bool done = false;
         // one fetch for every active lane, leaf or internal, before the branch: a wave
         // holding both kinds would otherwise wait for two dependent round trips
         // (leaf and child-pair records are both 64-B aligned records of 64 B; the
         // 4-wide record pair adds a second 64 B for internal lanes)
-        const bool isleaf = (node & LEAF_BIT) != 0;
-        const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(node & ~LEAF_BIT))
+        const bool isleaf = POSTPONE ? do_leaf : (node & LEAF_BIT) != 0;
+        const uint32_t lid = POSTPONE ? pend : node;
+        const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(lid & ~LEAF_BIT))
                                : reinterpret_cast<const v4f*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
         v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
         v4f q4 = {0.f, 0.f, 0.f, 0.f}, q5 = q4, q6 = q4, q7 = q4;
@@ -843,7 +870,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             c.overflow++;
             done = true;
         } else if (isleaf) {
-            const uint32_t j = node & ~LEAF_BIT;
+            const uint32_t j = lid & ~LEAF_BIT;
             const v4f la = q0, lb = q1;
             const float e2z = q2.x;
             if (COUNT) c.leaf++;
@@ -853,7 +880,13 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 bl = j;
                 hit = true;
             }
-            if (WIDE) {
+            if (POSTPONE) {
+                pend = INVALID;
+                if (node & LEAF_BIT) {   // the leaf that blocked this lane is parked now
+                    pend = node;
+                    node = INVALID;
+                }
+            } else if (WIDE) {
                 node = INVALID;   // pop below
             } else {
                 node = top;                             // pop
@@ -881,6 +914,10 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             sort2(k1, i1, k3, i3);
             sort2(k1, i1, k2, i2);
             node = i0;   // nearest (INVALID when no child is hit -> pop below)
+            if (POSTPONE && (i0 & LEAF_BIT) && i0 != INVALID && pend == INVALID) {
+                pend = i0;   // park it and walk on
+                node = INVALID;
+            }
             if (sp + 3 > STACK4) {
                 c.overflow++;
                 done = true;
@@ -923,11 +960,15 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 --sp;
                 const uint2 e = sp < SW ? s_wstk[sp][tid] : wstack[sp - SW];
                 if (!hit || __uint_as_float(e.y) <= best) {
+                    if (POSTPONE && (e.x & LEAF_BIT) && pend == INVALID) {
+                        pend = e.x;   // park a popped leaf too, and keep popping for a node
+                        continue;
+                    }
                     node = e.x;
                     break;
                 }
             }
-            done = node == INVALID;
+            done = node == INVALID && (!POSTPONE || pend == INVALID);
         }
         if (done) {
             hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
@@ -944,6 +985,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             if (COUNT) {
                 atomicAdd(&counters[5], v[0]);
                 atomicAdd(&counters[6], v[1]);
+                atomicAdd(&counters[10], wsteps);
+                atomicAdd(&counters[11], mixed);
+                atomicAdd(&counters[12], active_lanes);
             }
             if (v[2]) atomicAdd(&counters[8], v[2]);
         }
@@ -1064,17 +1108,23 @@ __global__ __launch_bounds__(BLOCK) void k_present(const float4* __restrict__ co
 template <bool COUNT, int S>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           int mode, float2* hitrec, uint32_t* next, uint32_t refill_min, uint32_t chunk,
-                          hipStream_t s) {
+                          uint32_t leaf_batch, hipStream_t s) {
     const uint32_t blocks = 2048;   // persistent: 8 waves/SIMD x 1024 SIMDs / 4 waves per block
-    if (mode == 2)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), 0, s, a.inner4, a.leaf, a.T, qin,
-                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk);
+    const uint32_t extra_lds = (chunk >> 24) * 1024u;   // A/B only: dynamic LDS (KB in the top byte)
+    chunk &= (1u << 24) - 1;                            // that caps the resident blocks per CU
+    if (mode == 3)
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 3, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s,
+                           a.inner4, a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk,
+                           leaf_batch);
+    else if (mode == 2)
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s, a.inner4, a.leaf, a.T, qin,
+                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
     else if (mode == 1)
         hipLaunchKernelGGL((k_bounce_trav<COUNT, 1, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T, qin,
-                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk);
+                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
     else
         hipLaunchKernelGGL((k_bounce_trav<COUNT, 0, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T,
-                           qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk);
+                           qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
 }
 
 }  // namespace
@@ -1113,11 +1163,11 @@ void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, 
 
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
-                            uint32_t refill_min, uint32_t chunk, hipStream_t s) {
+                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, hipStream_t s) {
     if (refill_min == 0) refill_min = REFILL_MIN;
 #define RTBVH_TRAV(S)                                                                                        \
-    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, s) \
-           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, s))
+    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, s) \
+           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, s))
     switch (lds_stack) {
         case 0: RTBVH_TRAV(0); break;
         case 8: RTBVH_TRAV(8); break;

@@ -40,6 +40,18 @@ def main():
         variants = [("wide refill32", base), ("refill16", base | 5 << V), ("thr8 chunk128", base | 6 << V), ("thr16 chunk128", base | 7 << V),
                     ("thr8 chunk256", base | 8 << V), ("thr16 chunk64", base | 9 << V), ("thr4 chunk128", base | 10 << V),
                     ("binary nearest thr8 chunk128", base & ~rt.FLAG_WIDE_BVH | 6 << V)]
+    if os.environ.get("AB_SET") == "occupancy":
+        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+        V = rt.FLAG_VARIANT_SHIFT
+        variants = [("8 waves/SIMD", base), ("6 waves/SIMD", base | 14 << V), ("4 waves/SIMD", base | 13 << V)]
+    if os.environ.get("AB_SET") == "sort":
+        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+        variants = [("wide", base), ("wide + bounce sort", base | rt.FLAG_SORT_BOUNCE)]
+    if os.environ.get("AB_SET") == "postpone":
+        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+        V = rt.FLAG_VARIANT_SHIFT
+        variants = [("wide", base), ("postpone 8", base | 5 << V), ("postpone 16", base | 15 << V),
+                    ("postpone 24", base | 6 << V), ("postpone 32", base | 7 << V)]
     if os.environ.get("AB_SET") == "wide":
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
         variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),

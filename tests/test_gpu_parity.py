@@ -203,7 +203,9 @@ TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest":
                "refill+sort": rt.FLAG_REFILL_BOUNCE | rt.FLAG_SORT_BOUNCE,
                "nearest+packet+refill": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE,
                "nearest+packet+wide": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
-               "packet+wide": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH}
+               "packet+wide": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
+               "wide+postponed-leaves (A/B variant 15)": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
+               | 15 << rt.FLAG_VARIANT_SHIFT}
 
 
 def _trace_both(s, W, H, bounces, rows=None, flags=0):
@@ -319,6 +321,34 @@ def test_read_rays_needs_records_flag():
         c.compute_bvh(64, 64, 1)
         with pytest.raises(RuntimeError, match="REFRACT_RECORDS"):
             c.read_rays()
+
+
+def _tiny_scene(ntris):
+    """ntris big triangles facing the camera, one behind the other (z = 0, 5, 10)."""
+    verts, idx = [], []
+    for k in range(ntris):
+        z = 5.0 * k
+        for x, y in ((-20.0 - k, -15.0), (20.0, -15.0 - k), (0.0, 18.0 + k)):
+            verts.append([x, y, z, 0.0, 0.0, -1.0, 0.5, 0.5])
+        idx += [3 * k, 3 * k + 1, 3 * k + 2]
+    mat = np.zeros(1, dtype=rt.MATERIAL_DTYPE)
+    mat["diffuse"] = [0.6, 0.5, 0.4, 1.0]
+    mat["specular"] = [1.0, 1.0, 1.0, 1.0]
+    mat["shininess"] = 400.0
+    mat["alpha"] = 1.0
+    mat["tex_num"] = -1
+    return rt.Scene(np.array(verts, np.float32), np.array(idx, np.uint32), np.zeros(ntris, np.uint32), mat)
+
+
+@pytest.mark.parametrize("ntris", [1, 2, 3])
+@pytest.mark.parametrize("mode", list(TRACE_MODES))
+def test_trace_tiny_scenes(ntris, mode):
+    """One-, two- and three-triangle trees (a leaf root, a root with two leaves, ...) in every mode."""
+    s = _tiny_scene(ntris)
+    fb, inten, st, ofb, oint, ost = _trace_both(s, 160, 90, 2, flags=TRACE_MODES[mode])
+    assert np.array_equal(fb, ofb)
+    np.testing.assert_array_equal(inten, oint)
+    assert ost["hits"] > 0 and st["stack_overflows"] == 0
 
 
 @pytest.mark.parametrize("mode", list(TRACE_MODES))
