@@ -250,13 +250,23 @@ __device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
 
 // the complete record of node p (word layout: rtbvh_device.h "node record"): its
 // children's boxes with each corner's (x, y) as an aligned pair, their ids, p itself
+// Word 15 bit s: child s's box needs the general slab test in the axis-parallel
+// primary walk (trace.hip traverse_packet4 AXIS): a non-finite corner, no interior in x
+// or y (min >= max), min.z > max.z, or max.z < 0.  Every other box takes the exact
+// compare-only form of ray_box_xy for rays along +z from z = 0.
+__device__ __forceinline__ uint32_t general_box(f3 lo, f3 hi) {
+    const bool fin = isfinite(lo.x) && isfinite(lo.y) && isfinite(lo.z) && isfinite(hi.x) && isfinite(hi.y) &&
+                     isfinite(hi.z);
+    return fin && lo.x < hi.x && lo.y < hi.y && lo.z <= hi.z && 0.f <= hi.z ? 0u : 1u;
+}
 __device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
                                              uint32_t cr, uint32_t own) {
     float4* d = reinterpret_cast<float4*>(dst);
+    const uint32_t gen = general_box(lmin, lmax) | general_box(rmin, rmax) << 1;
     d[0] = make_float4(lmin.x, lmin.y, lmax.x, lmax.y);
     d[1] = make_float4(rmin.x, rmin.y, rmax.x, rmax.y);
     d[2] = make_float4(lmin.z, lmax.z, rmin.z, rmax.z);
-    d[3] = make_float4(__uint_as_float(cl), __uint_as_float(cr), __uint_as_float(own), 0.f);
+    d[3] = make_float4(__uint_as_float(cl), __uint_as_float(cr), __uint_as_float(own), __uint_as_float(gen));
 }
 // box of child `side` from a node record: min xyz, max xyz
 __device__ __forceinline__ void record_box(const Inner* r, uint32_t side, float out[6]) {

@@ -21,7 +21,9 @@
 // Node ids: internal k -> k, leaf j -> LEAF_BIT | j.
 // Node record words (so that each corner's (x, y) is an aligned pair for packed fp32):
 //   0-1 left.min.xy  2-3 left.max.xy  4-5 right.min.xy  6-7 right.max.xy
-//   8 left.min.z  9 left.max.z  10 right.min.z  11 right.max.z  12 id_l  13 id_r  14 own  15 0
+//   8 left.min.z  9 left.max.z  10 right.min.z  11 right.max.z  12 id_l  13 id_r  14 own
+//   15 bit s: child s's box needs the general slab test for axis-parallel primary rays
+//      (non-finite corner, min >= max in x or y, min.z > max.z or max.z < 0; build.hip)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -22,6 +22,9 @@
 // scratch stack whose top lives in a register.
 #include "rtbvh_internal.h"
 
+// v_writelane_b32 (see writelane below)
+__device__ uint32_t amdgcn_writelane(uint32_t x, uint32_t lane, uint32_t v) __asm("llvm.amdgcn.writelane.i32");
+
 namespace rtbvh {
 namespace {
 
@@ -326,6 +329,11 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
     return hit;
 }
 
+// v[lane] = x for wave-uniform x and lane: v_writelane_b32 through the LLVM intrinsic
+// (this clang has no __builtin_amdgcn_writelane; declared above the namespace); the
+// compiler puts the lane in M0
+__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x, int lane) { v = amdgcn_writelane(x, lane, v); }
+
 // ---- wave-packet traversal on the 4-wide view (primary rays) -------------------
 // As traverse_packet, but one step reads the 128-B record pair inner4[2p], inner4[2p+1]
 // (two s_load_dwordx16 of one line): the boxes of p's four grandchildren.  Children
@@ -334,7 +342,21 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
 // front-to-back order (box zmin: primary rays run along +z) made the per-lane visits
 // 6% fewer but lost the compiler's wave-uniform tracking of the node id and ran 1.6x
 // slower, so there is one order.
-template <bool COUNT>
+//
+// AXIS: the rays run along d = (0, 0, 1) from z = 0 (k_primary), so inv = (inf, inf, 1)
+// and each x/y slab of ray_box_xy yields [-inf, inf] (or NaNs that fminf/fmaxf drop)
+// exactly when min < o < max, and an empty slab otherwise.  For a box whose record bit
+// (word 15, build.hip general_box) is clear -- finite corners, min < max in x and y,
+// min.z <= max.z, 0 <= max.z -- the test is therefore exactly
+//     min.x < o.x < max.x  &&  min.y < o.y < max.y  &&  (!hit || min.z <= best)
+// (denormals are kept, so min < o has the sign of min - o): five compares instead of
+// ~17 VALU operations.  A node with any bit set takes the general test.
+// AXIS 2 (default): o - min and max - o as packed differences and min(...) > 0 (a rounded
+// difference of finite floats is > 0 exactly when the exact one is): 6 VALU + 2 lane-mask
+// ANDs per box.  AXIS 1 (A/B): five v_cmp ANDed as lane masks, 5 VALU + 5 SALU per box --
+// 11% slower (C5 primary 2.96 vs 2.67 ms): the loop's lane-mask and stack work already
+// loads the CU's one scalar unit.  AXIS 0 (A/B): the general test everywhere, 3.13 ms.
+template <bool COUNT, int AX, bool LANESTACK>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
                                                  uint32_t T, f3 o, f3 d, f3 inv, bool valid, float& best,
                                                  uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*STACK4] */) {
@@ -347,6 +369,12 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
     int sp = 0;
     uint32_t node = (T == 1) ? LEAF_BIT : 0u;
     if (mask == 0) return false;
+    float bound = INFINITY;   // AXIS: best once hit, +inf before (min.z <= bound == !hit || min.z <= best)
+    // LANESTACK (A/B): entry i < 64 of the wave-uniform stack in lane i of three VGPRs
+    // (v_writelane / v_readlane at the scalar index sp: no LDS round trip on a pop), deeper
+    // entries in LDS.  Measured 3% slower than the LDS stack (the sp < 64 branches and phi
+    // copies cost more than the LDS latency, which the other waves hide).
+    uint32_t ls_n = 0, ls_lo = 0, ls_hi = 0;
     uint32_t guard = 2 * T + 2;
     while (true) {
         if (--guard == 0) { c.overflow++; break; }
@@ -360,6 +388,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
                 const float t = ray_triangle(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]));
                 if (t != -1.f && (!hit || t < best || (t == best && j < best_leaf))) {
                     best = t;
+                    bound = t;
                     best_leaf = j;
                     hit = true;
                 }
@@ -370,18 +399,47 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             const v16f B = sload16(inner4 + 2 * (size_t)node + 1);
             uint32_t id[4] = {__float_as_uint(A[12]), __float_as_uint(A[13]), __float_as_uint(B[12]),
                               __float_as_uint(B[13])};
-            bool h[4] = {false, false, false, false};
-            float t[4] = {0.f, 0.f, 0.f, 0.f};
-            if (mask & lanebit) {
-                if (COUNT) c.internal++;
-                h[0] = ray_box_xy(o, inv, A.s01, A.s23, A[8], A[9], hit, best, t[0]);
-                h[1] = ray_box_xy(o, inv, A.s45, A.s67, A[10], A[11], hit, best, t[1]) & (id[1] != INVALID);
-                h[2] = ray_box_xy(o, inv, B.s01, B.s23, B[8], B[9], hit, best, t[2]);
-                h[3] = ray_box_xy(o, inv, B.s45, B.s67, B[10], B[11], hit, best, t[3]) & (id[3] != INVALID);
-            }
+            if (COUNT && (mask & lanebit)) c.internal++;
             uint64_t m[4];
+            if (AX == 2 && (__float_as_uint(A[15]) | __float_as_uint(B[15])) == 0) {   // wave-uniform
+                const f2v oxy = {o.x, o.y};
+                const auto lanes = [&](f2v lo, f2v hi, float lz) {
+                    const f2v d0 = oxy - lo, d1 = hi - oxy;
+                    const float m = fminf(fminf(d0.x, d0.y), fminf(d1.x, d1.y));
+                    return __builtin_amdgcn_ballot_w64(m > 0.f) & __builtin_amdgcn_ballot_w64(lz <= bound);
+                };
+                m[0] = lanes(A.s01, A.s23, A[8]) & mask;
+                m[1] = lanes(A.s45, A.s67, A[10]) & mask;
+                m[2] = lanes(B.s01, B.s23, B[8]) & mask;
+                m[3] = lanes(B.s45, B.s67, B[10]) & mask;
+                if (id[1] == INVALID) m[1] = 0;
+                if (id[3] == INVALID) m[3] = 0;
+            } else if (AX == 1 && (__float_as_uint(A[15]) | __float_as_uint(B[15])) == 0) {   // wave-uniform
+                // one ballot per compare: each lowers to the v_cmp's own lane mask (an && chain
+                // would be materialised as a bool and compared again)
+                const auto lanes = [&](f2v lo, f2v hi, float lz) {
+                    return __builtin_amdgcn_ballot_w64(lo.x < o.x) & __builtin_amdgcn_ballot_w64(o.x < hi.x) &
+                           __builtin_amdgcn_ballot_w64(lo.y < o.y) & __builtin_amdgcn_ballot_w64(o.y < hi.y) &
+                           __builtin_amdgcn_ballot_w64(lz <= bound);
+                };
+                m[0] = lanes(A.s01, A.s23, A[8]) & mask;
+                m[1] = lanes(A.s45, A.s67, A[10]) & mask;
+                m[2] = lanes(B.s01, B.s23, B[8]) & mask;
+                m[3] = lanes(B.s45, B.s67, B[10]) & mask;
+                if (id[1] == INVALID) m[1] = 0;
+                if (id[3] == INVALID) m[3] = 0;
+            } else {
+                bool h[4] = {false, false, false, false};
+                float t[4] = {0.f, 0.f, 0.f, 0.f};
+                if (mask & lanebit) {
+                    h[0] = ray_box_xy(o, inv, A.s01, A.s23, A[8], A[9], hit, best, t[0]);
+                    h[1] = ray_box_xy(o, inv, A.s45, A.s67, A[10], A[11], hit, best, t[1]) & (id[1] != INVALID);
+                    h[2] = ray_box_xy(o, inv, B.s01, B.s23, B[8], B[9], hit, best, t[2]);
+                    h[3] = ray_box_xy(o, inv, B.s45, B.s67, B[10], B[11], hit, best, t[3]) & (id[3] != INVALID);
+                }
 #pragma unroll
-            for (int k = 0; k < 4; k++) m[k] = __ballot(h[k]);
+                for (int k = 0; k < 4; k++) m[k] = __ballot(h[k]);
+            }
             // children left to right (compile-time indices only: no private arrays)
             const uint32_t* oi = id;
             const uint64_t* om = m;
@@ -395,7 +453,11 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
 #pragma unroll
                 for (int k = 3; k >= 1; --k) {   // push the later children, farthest first
                     if (k > first && om[k]) {
-                        if (lane == 0) {
+                        if (LANESTACK && sp < 64) {
+                            writelane(ls_n, oi[k], sp);
+                            writelane(ls_lo, (uint32_t)om[k], sp);
+                            writelane(ls_hi, (uint32_t)(om[k] >> 32), sp);
+                        } else if (lane == 0) {
                             s_st[3 * sp] = oi[k];
                             s_st[3 * sp + 1] = (uint32_t)om[k];
                             s_st[3 * sp + 2] = (uint32_t)(om[k] >> 32);
@@ -410,9 +472,16 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
         if (pop) {
             if (sp == 0) break;
             --sp;
-            node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
-            const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
-            const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
+            uint32_t lo, hi;
+            if (LANESTACK && sp < 64) {
+                node = __builtin_amdgcn_readlane(ls_n, sp);
+                lo = __builtin_amdgcn_readlane(ls_lo, sp);
+                hi = __builtin_amdgcn_readlane(ls_hi, sp);
+            } else {
+                node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
+                lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
+                hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
+            }
             mask = ((uint64_t)hi << 32) | lo;
         }
     }
@@ -425,8 +494,10 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
 // 5 = 4-wide packets (left-to-right order, (t, leaf) minimum)
 template <int V> struct TV {
     static constexpr bool NEAREST = (V == 1 || V == 4);
-    static constexpr bool PACKET = (V == 3 || V == 4 || V == 5);
-    static constexpr bool WIDE = (V == 5);
+    static constexpr bool PACKET = (V == 3 || V == 4 || V >= 5);
+    static constexpr bool WIDE = (V >= 5);
+    static constexpr int AXIS = (V == 5 || V == 8) ? 2 : V == 7 ? 1 : 0;   // 6, 7: A/B forms of 5's box test
+    static constexpr bool LANESTACK = V == 8;   // 8: A/B, stack in VGPR lanes (C5 primary 2.73 vs 2.66 ms)
     static constexpr int OCC = (V == 2) ? 1 : 8;   // 8 waves/SIMD => <= 64 VGPRs (A/B: -25% bounce time)
 };
 
@@ -603,7 +674,7 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
     uint32_t bl = 0;
     bool phit = false;
     if (TV<V>::WIDE)     // whole wave, before any divergence
-        phit = traverse_packet4<COUNT>(a.inner4, a.leaf, a.T, o, d, inv, valid, best, bl, c,
+        phit = traverse_packet4<COUNT, TV<V>::AXIS, TV<V>::LANESTACK>(a.inner4, a.leaf, a.T, o, d, inv, valid, best, bl, c,
                                                        s_pst + w * PST);
     else if (TV<V>::PACKET)
         phit = traverse_packet<COUNT, TV<V>::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, best, bl, c,
@@ -1145,7 +1216,10 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
     if (my_bands == 0 || a.W == 0) return;
     dim3 grid((a.W + 31) / 32, my_bands);
 #define RTBVH_PRIM(C, V) launch_primary_t<C, V>(a, q, qcount, emit, grid, s)
-    RTBVH_VARIANTS(RTBVH_PRIM)
+    if (variant == 6) count ? RTBVH_PRIM(true, 6) : RTBVH_PRIM(false, 6);
+    else if (variant == 7) count ? RTBVH_PRIM(true, 7) : RTBVH_PRIM(false, 7);
+    else if (variant == 8) count ? RTBVH_PRIM(true, 8) : RTBVH_PRIM(false, 8);
+    else RTBVH_VARIANTS(RTBVH_PRIM)
 #undef RTBVH_PRIM
 }
 

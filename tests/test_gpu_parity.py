@@ -204,6 +204,12 @@ TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest":
                "nearest+packet+refill": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE,
                "nearest+packet+wide": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
                "packet+wide": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
+               "packet+wide, general primary box test (A/B variant 11)":
+                   rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 11 << rt.FLAG_VARIANT_SHIFT,
+               "packet+wide, compare-form primary box test (A/B variant 12)":
+                   rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 12 << rt.FLAG_VARIANT_SHIFT,
+               "packet+wide, VGPR-lane packet stack (A/B variant 16)":
+                   rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 16 << rt.FLAG_VARIANT_SHIFT,
                "wide+postponed-leaves (A/B variant 15)": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
                | 15 << rt.FLAG_VARIANT_SHIFT}
 
@@ -426,14 +432,69 @@ def test_wide_view_records_match_binary_tree():
             lo, hi = box(fr, 0)
             np.testing.assert_array_equal(lo, nodes["bb_min"][k])
             np.testing.assert_array_equal(hi, nodes["bb_max"][k])
+            assert rec[15] == 3 * _general_box(lo, hi)
         else:
             cl, cr = nodes["child_l"][k], nodes["child_r"][k]
             ids = [(0x80000000 | x) if x < T else x - T for x in (cl, cr)]
             assert list(rec[12:15]) == ids + [k - T]
+            gen = 0
             for sd, ch in ((0, cl), (1, cr)):
                 lo, hi = box(fr, sd)
                 np.testing.assert_array_equal(lo, nodes["bb_min"][ch])
                 np.testing.assert_array_equal(hi, nodes["bb_max"][ch])
+                gen |= _general_box(lo, hi) << sd
+            assert rec[15] == gen
+
+
+def _general_box(lo, hi):
+    """Record word 15's bit (rtbvh_device.h): the box needs the general primary slab test."""
+    fin = np.all(np.isfinite(lo)) and np.all(np.isfinite(hi))
+    return 0 if fin and lo[0] < hi[0] and lo[1] < hi[1] and lo[2] <= hi[2] and 0 <= hi[2] else 1
+
+
+def _general_box_scene(seed=11):
+    """A synthetic scene plus triangles whose boxes take the general primary slab test:
+    triangles in planes x = const (clip x = x * M0 exactly for the reference camera, so
+    their boxes are flat in x), single-point triangles (flat in x and y), and triangles
+    behind the eye (max.z < 0 in clip space)."""
+    base = rt.synthetic(3000, seed=seed, half_extent=(30, 30, 20))
+    rng = np.random.default_rng(seed)
+    extra = []
+    for _ in range(300):   # x = const
+        x = rng.uniform(-25, 25)
+        p = np.stack([np.full(3, x), rng.uniform(-25, 25, 3), rng.uniform(-20, 20, 3)], 1)
+        extra.append(p)
+    for _ in range(150):   # points
+        extra.append(np.repeat(rng.uniform(-25, 25, (1, 3)), 3, 0))
+    for _ in range(300):   # behind the eye (z = -100)
+        extra.append(np.stack([rng.uniform(-40, 40, 3), rng.uniform(-40, 40, 3), rng.uniform(-160, -101, 3)], 1))
+    pos = np.concatenate(extra).astype(np.float32)
+    v = np.zeros((len(pos), 8), np.float32)
+    v[:, :3] = pos
+    v[:, 5] = -1.0
+    V0 = len(base.vertices)
+    verts = np.concatenate([base.vertices, v])
+    idx = np.concatenate([base.indices, V0 + np.arange(len(pos), dtype=np.uint32)])
+    mats = np.concatenate([base.mat_indices, np.zeros(len(pos) // 3, np.uint32)])
+    return rt.Scene(verts, idx, mats, base.materials)
+
+
+@pytest.mark.parametrize("mode", ["packet+wide", "nearest+packet+wide",
+                                  "packet+wide, compare-form primary box test (A/B variant 12)"])
+def test_primary_general_boxes(mode):
+    """Flat and behind-the-eye boxes (record word 15 set) in the axis-parallel primary walk:
+    frames identical to the oracle's, and the record bits as the tree's boxes say."""
+    s = _general_box_scene()
+    fb, inten, st, ofb, oint, ost = _trace_both(s, 320, 240, 1, flags=TRACE_MODES[mode])
+    assert np.array_equal(fb, ofb)
+    np.testing.assert_array_equal(inten, oint)
+    assert ost["hits"] > 0
+    with rt.Context(device=0, flags=rt.FLAG_WIDE_BVH) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(320, 240))
+        c.build()
+        w4 = c.read_wide()
+    assert np.count_nonzero(w4[:, 15]) > 100   # the general path is taken
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
