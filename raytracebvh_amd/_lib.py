@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librtbvh.so")
+# RTBVH_LIB: an A/B build of the same library (raytracebvh_amd/csrc/Makefile OUT=...)
+LIB_PATH = os.environ.get("RTBVH_LIB") or os.path.join(HERE, "librtbvh.so")
 
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_OOM, ERR_NOT_READY, ERR_STACK_OVERFLOW, ERR_IO, ERR_NO_DEVICE = range(8)
 MORTON_CPUTESTS, MORTON_HLSL = 0, 1

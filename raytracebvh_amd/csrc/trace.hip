@@ -855,6 +855,10 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     // of the last claimed chunks outweighs the saved atomics)
     uint32_t cnext = 0, cend = 0;
     unsigned long long wsteps = 0, mixed = 0, active_lanes = 0;
+    // second half of a 4-wide record pair, loop-carried: a leaf lane skips its load and
+    // keeps the previous values (a per-iteration zero would cost 16 v_mov every iteration;
+    // loading the other half of the leaf's line on leaf lanes cost +2% in TA work)
+    v4f q4 = {0.f, 0.f, 0.f, 0.f}, q5 = q4, q6 = q4, q7 = q4;
     while (true) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -931,8 +935,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(lid & ~LEAF_BIT))
                                : reinterpret_cast<const v4f*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
         v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
-        v4f q4 = {0.f, 0.f, 0.f, 0.f}, q5 = q4, q6 = q4, q7 = q4;
-        if (WIDE && !isleaf) {
+        if (WIDE && !isleaf) {   // the right child's record (leaf lanes keep stale q4..q7)
             q4 = rr[4]; q5 = rr[5]; q6 = rr[6]; q7 = rr[7];
         }
         pin(q0); pin(q1); pin(q2); pin(q3);

@@ -52,6 +52,9 @@ def main():
         V = rt.FLAG_VARIANT_SHIFT
         variants = [("wide", base), ("postpone 8", base | 5 << V), ("postpone 16", base | 15 << V),
                     ("postpone 24", base | 6 << V), ("postpone 32", base | 7 << V)]
+    if os.environ.get("AB_SET") == "base":   # the bench's mode only (A/B of two builds via RTBVH_LIB)
+        variants = [("nearest-first-wide", rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST
+                     | rt.FLAG_WIDE_BVH)]
     if os.environ.get("AB_SET") == "axis":   # primary box test for axis-parallel rays
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
         V = rt.FLAG_VARIANT_SHIFT
