@@ -243,7 +243,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t leaf_batch = vsel == 15 ? 16 : vsel == 5 ? 8 : vsel == 6 ? 24 : vsel == 7 ? 32 : 16;
     const int bmode = wide ? ((vsel == 15 || (vsel >= 5 && vsel <= 7)) ? 3 : 2) : (variant == 1 ? 1 : 0);
     if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1)
-        pvariant = wide ? (vsel == 11 ? 6 : vsel == 12 ? 7 : vsel == 16 ? 8 : 5) : (variant == 1 ? 4 : 3);
+        pvariant = wide ? (vsel == 11 ? 6 : vsel == 12 ? 7 : 5) : (variant == 1 ? 4 : 3);
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
     if (records) {
         if (c->cap_rec < P) {

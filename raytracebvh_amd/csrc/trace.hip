@@ -22,9 +22,6 @@
 // scratch stack whose top lives in a register.
 #include "rtbvh_internal.h"
 
-// v_writelane_b32 (see writelane below)
-__device__ uint32_t amdgcn_writelane(uint32_t x, uint32_t lane, uint32_t v) __asm("llvm.amdgcn.writelane.i32");
-
 namespace rtbvh {
 namespace {
 
@@ -329,11 +326,6 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
     return hit;
 }
 
-// v[lane] = x for wave-uniform x and lane: v_writelane_b32 through the LLVM intrinsic
-// (this clang has no __builtin_amdgcn_writelane; declared above the namespace); the
-// compiler puts the lane in M0
-__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x, int lane) { v = amdgcn_writelane(x, lane, v); }
-
 // ---- wave-packet traversal on the 4-wide view (primary rays) -------------------
 // As traverse_packet, but one step reads the 128-B record pair inner4[2p], inner4[2p+1]
 // (two s_load_dwordx16 of one line): the boxes of p's four grandchildren.  Children
@@ -356,7 +348,7 @@ __device__ __forceinline__ void writelane(uint32_t& v, uint32_t x, int lane) { v
 // ANDs per box.  AXIS 1 (A/B): five v_cmp ANDed as lane masks, 5 VALU + 5 SALU per box --
 // 11% slower (C5 primary 2.96 vs 2.67 ms): the loop's lane-mask and stack work already
 // loads the CU's one scalar unit.  AXIS 0 (A/B): the general test everywhere, 3.13 ms.
-template <bool COUNT, int AX, bool LANESTACK>
+template <bool COUNT, int AX>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
                                                  uint32_t T, f3 o, f3 d, f3 inv, bool valid, float& best,
                                                  uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*STACK4] */) {
@@ -370,11 +362,11 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
     uint32_t node = (T == 1) ? LEAF_BIT : 0u;
     if (mask == 0) return false;
     float bound = INFINITY;   // AXIS: best once hit, +inf before (min.z <= bound == !hit || min.z <= best)
-    // LANESTACK (A/B): entry i < 64 of the wave-uniform stack in lane i of three VGPRs
-    // (v_writelane / v_readlane at the scalar index sp: no LDS round trip on a pop), deeper
-    // entries in LDS.  Measured 3% slower than the LDS stack (the sp < 64 branches and phi
-    // copies cost more than the LDS latency, which the other waves hide).
-    uint32_t ls_n = 0, ls_lo = 0, ls_hi = 0;
+    // The stack is lane 0's LDS words, one lane-0 region per push.  Measured against it
+    // (C5 primary, A/B, since removed): the stack in VGPR lanes (v_writelane/v_readlane at
+    // the scalar index sp, LDS beyond 64 entries) +3%; all lanes storing the same words (no
+    // exec region) and branch-free pushes at a running top 0% and +3%; one lane-0 region
+    // for all pushes of a node +26% (the compiler moved the walk state out of SGPRs).
     uint32_t guard = 2 * T + 2;
     while (true) {
         if (--guard == 0) { c.overflow++; break; }
@@ -453,11 +445,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
 #pragma unroll
                 for (int k = 3; k >= 1; --k) {   // push the later children, farthest first
                     if (k > first && om[k]) {
-                        if (LANESTACK && sp < 64) {
-                            writelane(ls_n, oi[k], sp);
-                            writelane(ls_lo, (uint32_t)om[k], sp);
-                            writelane(ls_hi, (uint32_t)(om[k] >> 32), sp);
-                        } else if (lane == 0) {
+                        if (lane == 0) {
                             s_st[3 * sp] = oi[k];
                             s_st[3 * sp + 1] = (uint32_t)om[k];
                             s_st[3 * sp + 2] = (uint32_t)(om[k] >> 32);
@@ -472,16 +460,9 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
         if (pop) {
             if (sp == 0) break;
             --sp;
-            uint32_t lo, hi;
-            if (LANESTACK && sp < 64) {
-                node = __builtin_amdgcn_readlane(ls_n, sp);
-                lo = __builtin_amdgcn_readlane(ls_lo, sp);
-                hi = __builtin_amdgcn_readlane(ls_hi, sp);
-            } else {
-                node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
-                lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
-                hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
-            }
+            node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
             mask = ((uint64_t)hi << 32) | lo;
         }
     }
@@ -496,8 +477,7 @@ template <int V> struct TV {
     static constexpr bool NEAREST = (V == 1 || V == 4);
     static constexpr bool PACKET = (V == 3 || V == 4 || V >= 5);
     static constexpr bool WIDE = (V >= 5);
-    static constexpr int AXIS = (V == 5 || V == 8) ? 2 : V == 7 ? 1 : 0;   // 6, 7: A/B forms of 5's box test
-    static constexpr bool LANESTACK = V == 8;   // 8: A/B, stack in VGPR lanes (C5 primary 2.73 vs 2.66 ms)
+    static constexpr int AXIS = V == 5 ? 2 : V == 7 ? 1 : 0;   // 6, 7: A/B forms of 5's box test
     static constexpr int OCC = (V == 2) ? 1 : 8;   // 8 waves/SIMD => <= 64 VGPRs (A/B: -25% bounce time)
 };
 
@@ -674,7 +654,7 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
     uint32_t bl = 0;
     bool phit = false;
     if (TV<V>::WIDE)     // whole wave, before any divergence
-        phit = traverse_packet4<COUNT, TV<V>::AXIS, TV<V>::LANESTACK>(a.inner4, a.leaf, a.T, o, d, inv, valid, best, bl, c,
+        phit = traverse_packet4<COUNT, TV<V>::AXIS>(a.inner4, a.leaf, a.T, o, d, inv, valid, best, bl, c,
                                                        s_pst + w * PST);
     else if (TV<V>::PACKET)
         phit = traverse_packet<COUNT, TV<V>::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, best, bl, c,
@@ -1221,7 +1201,6 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 #define RTBVH_PRIM(C, V) launch_primary_t<C, V>(a, q, qcount, emit, grid, s)
     if (variant == 6) count ? RTBVH_PRIM(true, 6) : RTBVH_PRIM(false, 6);
     else if (variant == 7) count ? RTBVH_PRIM(true, 7) : RTBVH_PRIM(false, 7);
-    else if (variant == 8) count ? RTBVH_PRIM(true, 8) : RTBVH_PRIM(false, 8);
     else RTBVH_VARIANTS(RTBVH_PRIM)
 #undef RTBVH_PRIM
 }

@@ -58,8 +58,7 @@ def main():
     if os.environ.get("AB_SET") == "axis":   # primary box test for axis-parallel rays
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
         V = rt.FLAG_VARIANT_SHIFT
-        variants = [("axis min3", base), ("general", base | 11 << V), ("axis cmp", base | 12 << V),
-                    ("axis min3, lane stack", base | 16 << V)]
+        variants = [("axis min3", base), ("general", base | 11 << V), ("axis cmp", base | 12 << V)]
     if os.environ.get("AB_SET") == "wide":
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
         variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),

@@ -208,8 +208,6 @@ TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest":
                    rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 11 << rt.FLAG_VARIANT_SHIFT,
                "packet+wide, compare-form primary box test (A/B variant 12)":
                    rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 12 << rt.FLAG_VARIANT_SHIFT,
-               "packet+wide, VGPR-lane packet stack (A/B variant 16)":
-                   rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 16 << rt.FLAG_VARIANT_SHIFT,
                "wide+postponed-leaves (A/B variant 15)": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
                | 15 << rt.FLAG_VARIANT_SHIFT}
 
