@@ -250,14 +250,14 @@ __device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
 
 // the complete record of node p (word layout: rtbvh_device.h "node record"): its
 // children's boxes with each corner's (x, y) as an aligned pair, their ids, p itself
-// Word 15 bit s: child s's box needs the general slab test in the axis-parallel
-// primary walk (trace.hip traverse_packet4 AXIS): a non-finite corner, no interior in x
-// or y (min >= max), min.z > max.z, or max.z < 0.  Every other box takes the exact
-// compare-only form of ray_box_xy for rays along +z from z = 0.
+// Word 15 bit s: child s's box needs the general slab test in the axis-parallel primary
+// walk (trace.hip traverse_packet4 AXIS).  Every box with min < max in x and y,
+// min.z <= max.z and 0 <= max.z < inf takes the exact compare-only form of ray_box_xy for
+// rays along +z from z = 0 (NaN fails a compare; infinite x/y corners and min.z give the
+// slab signs the general test gives; max.z = +inf could let the general test report a hit
+// at t = +inf with an empty slab).
 __device__ __forceinline__ uint32_t general_box(f3 lo, f3 hi) {
-    const bool fin = isfinite(lo.x) && isfinite(lo.y) && isfinite(lo.z) && isfinite(hi.x) && isfinite(hi.y) &&
-                     isfinite(hi.z);
-    return fin && lo.x < hi.x && lo.y < hi.y && lo.z <= hi.z && 0.f <= hi.z ? 0u : 1u;
+    return lo.x < hi.x && lo.y < hi.y && lo.z <= hi.z && 0.f <= hi.z && hi.z < INFINITY ? 0u : 1u;
 }
 __device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
                                              uint32_t cr, uint32_t own) {

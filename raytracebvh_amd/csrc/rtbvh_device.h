@@ -23,7 +23,7 @@
 //   0-1 left.min.xy  2-3 left.max.xy  4-5 right.min.xy  6-7 right.max.xy
 //   8 left.min.z  9 left.max.z  10 right.min.z  11 right.max.z  12 id_l  13 id_r  14 own
 //   15 bit s: child s's box needs the general slab test for axis-parallel primary rays
-//      (non-finite corner, min >= max in x or y, min.z > max.z or max.z < 0; build.hip)
+//      (not: min < max in x and y, min.z <= max.z, 0 <= max.z < inf; build.hip general_box)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -338,14 +338,14 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
 // AXIS: the rays run along d = (0, 0, 1) from z = 0 (k_primary), so inv = (inf, inf, 1)
 // and each x/y slab of ray_box_xy yields [-inf, inf] (or NaNs that fminf/fmaxf drop)
 // exactly when min < o < max, and an empty slab otherwise.  For a box whose record bit
-// (word 15, build.hip general_box) is clear -- finite corners, min < max in x and y,
-// min.z <= max.z, 0 <= max.z -- the test is therefore exactly
+// (word 15, build.hip general_box) is clear -- min < max in x and y, min.z <= max.z,
+// 0 <= max.z < inf -- the test is therefore exactly
 //     min.x < o.x < max.x  &&  min.y < o.y < max.y  &&  (!hit || min.z <= best)
 // (denormals are kept, so min < o has the sign of min - o): five compares instead of
 // ~17 VALU operations.  A node with any bit set takes the general test.
 // AXIS 2 (default): o - min and max - o as packed differences and min(...) > 0 (a rounded
-// difference of finite floats is > 0 exactly when the exact one is): 6 VALU + 2 lane-mask
-// ANDs per box.  AXIS 1 (A/B): five v_cmp ANDed as lane masks, 5 VALU + 5 SALU per box --
+// difference of non-NaN floats, infinities included, is > 0 exactly when the exact one
+// is): 6 VALU + 2 lane-mask ANDs per box.  AXIS 1 (A/B): five v_cmp ANDed as lane masks, 5 VALU + 5 SALU per box --
 // 11% slower (C5 primary 2.96 vs 2.67 ms): the loop's lane-mask and stack work already
 // loads the CU's one scalar unit.  AXIS 0 (A/B): the general test everywhere, 3.13 ms.
 template <bool COUNT, int AX>
