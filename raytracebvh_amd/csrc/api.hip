@@ -34,7 +34,8 @@ struct rtbvh_ctx {
     uint32_t *d_codes = nullptr, *d_ids = nullptr, *d_ka = nullptr, *d_va = nullptr, *d_kb = nullptr, *d_vb = nullptr;
     uint32_t* d_sort_scratch = nullptr;
     float4 *d_tclip = nullptr, *d_leaf = nullptr;
-    Inner* d_inner = nullptr;
+    Inner* d_inner = nullptr;                // box hand-off of refit nodes spanning workgroups
+    uint4* d_topo = nullptr;                 // Karras node: child ids + leaf range
     Inner* d_rec = nullptr;                  // node records in slots (rtbvh_device.h), 2T-1
     uint32_t* d_texels = nullptr;            // textures (rtbvh_texture), concatenated RGBA8
     uint4* d_texinfo = nullptr;
@@ -115,6 +116,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_tclip, 3 * n));
     HIPC(c, dalloc(c->d_leaf, 4 * n));
     HIPC(c, dalloc(c->d_inner, ni));
+    HIPC(c, dalloc(c->d_topo, ni));
     HIPC(c, dalloc(c->d_rec, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
@@ -164,6 +166,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.sorted_vals = c->sorted.vals;
     a.leaf = c->d_leaf;
     a.inner = c->d_inner;
+    a.topo = c->d_topo;
     a.rec = c->d_rec;
     a.pleaf = c->d_pleaf;
     a.pint = c->d_pint;
@@ -359,7 +362,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_rec);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);

@@ -155,7 +155,7 @@ __device__ __forceinline__ int delta(const uint32_t* c, int64_t n, uint32_t i, u
 }
 
 template <int MODE>
-__device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t i, Inner* __restrict__ inner,
+__device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t i, uint4* __restrict__ topo,
                             uint32_t* __restrict__ pleaf, uint32_t* __restrict__ pint) {
     const int64_t N = n, I = i;
     const uint32_t ci = c[i];
@@ -180,10 +180,9 @@ __device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t
     const bool left_leaf = (I < bound_start ? I : bound_start) == loc;
     const bool right_leaf = (I > bound_start ? I : bound_start) == loc + 1;
     const uint32_t l = (uint32_t)loc, r = (uint32_t)(loc + 1);
-    inner[i].child_l = left_leaf ? (LEAF_BIT | l) : l;
-    inner[i].child_r = right_leaf ? (LEAF_BIT | r) : r;
-    inner[i].aux0 = (uint32_t)(I < bound_start ? I : bound_start);   // leaf range of node i
-    inner[i].aux1 = (uint32_t)(I > bound_start ? I : bound_start);
+    topo[i] = make_uint4(left_leaf ? (LEAF_BIT | l) : l, right_leaf ? (LEAF_BIT | r) : r,
+                         (uint32_t)(I < bound_start ? I : bound_start),    // leaf range of node i
+                         (uint32_t)(I > bound_start ? I : bound_start));
     if (left_leaf) pleaf[l] = i << 1; else pint[l] = i << 1;
     if (right_leaf) pleaf[r] = (i << 1) | 1u; else pint[r] = (i << 1) | 1u;
 }
@@ -208,7 +207,7 @@ __global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
     dst[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
     dst[2] = make_float4(e2.z, __uint_as_float(t), lo.x, lo.y);
     dst[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
-    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.inner, a.pleaf, a.pint);
+    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
     if (i == 0 && a.T > 1) a.pint[0] = INVALID;   // root (BVHConstructP1.hlsl:186-187)
 }
 
@@ -216,7 +215,7 @@ __global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_karras_only(BuildArgs a) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.inner, a.pleaf, a.pint);
+    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
     if (i == 0 && a.T > 1) a.pint[0] = INVALID;
 }
 
@@ -280,6 +279,7 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t parent_code, uint32_t T) {
 }
 
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __restrict__ inner,
+                                            const uint4* __restrict__ topo,
                                             const uint32_t* __restrict__ pint, uint32_t* __restrict__ cnt,
                                             float* __restrict__ rootbox, Inner* __restrict__ rec, uint32_t T) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
@@ -294,7 +294,7 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
         f3 smin, smax;
         ld_box_sc1(side ? inner[p].lmin : inner[p].rmin, smin, smax);
         e = pint[p];
-        const uint2 ids = *reinterpret_cast<const uint2*>(&inner[p].child_l);
+        const uint4 ids = topo[p];
         if (side) store_record(rec + slot_of(e, T), smin, smax, lo, hi, ids.x, ids.y, p);
         else      store_record(rec + slot_of(e, T), lo, hi, smin, smax, ids.x, ids.y, p);
         // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
@@ -336,10 +336,10 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
     const uint32_t end = base + BLOCK;
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
-        const uint4 q3 = reinterpret_cast<const uint4*>(&a.inner[p])[3];   // ids, leaf range
+        const uint4 q3 = a.topo[p];   // ids, leaf range
         const uint32_t pe = a.pint[p];
         if (!(p >= base && p < end && q3.z >= base && q3.w < end)) {      // leaves the block
-            refit_climb(lo, hi, e, a.inner, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
+            refit_climb(lo, hi, e, a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
             return;
         }
         float* sb = s_box[p - base][side];
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
         for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
         return;
     }
-    refit_climb(lo, hi, a.pleaf[i], a.inner, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
+    refit_climb(lo, hi, a.pleaf[i], a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
 }
 
 // reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restri
     } else {
         const uint32_t k = r - T;
         e = a.pint[k];
-        const uint32_t cl = a.inner[k].child_l, cr = a.inner[k].child_r;
+        const uint32_t cl = a.topo[k].x, cr = a.topo[k].y;
         o.child_l = (cl & LEAF_BIT) ? (cl & ~LEAF_BIT) : T + cl;
         o.child_r = (cr & LEAF_BIT) ? (cr & ~LEAF_BIT) : T + cr;
         o.code = 0;

@@ -15,8 +15,9 @@
 //                        So the records of two siblings share one 128-B line: the binary
 //                        walks step to slot 2k+side, the 4-wide walks read slots 2k, 2k+1
 //                        (the four grandchild boxes of k) in one line.
-//   inner  Inner[T-1]    build scratch indexed by node: Karras ids + leaf range, and the
-//                        box hand-off of refit nodes that span workgroups
+//   topo   uint4[T-1]    build scratch indexed by node: Karras child ids + leaf range
+//   inner  Inner[T-1]    build scratch: the box hand-off of refit nodes that span
+//                        workgroups (only those are touched)
 //   pleaf  u32[T], pint u32[T-1]   parent<<1 | side (side 0 = left child)
 // Node ids: internal k -> k, leaf j -> LEAF_BIT | j.
 // Node record words (so that each corner's (x, y) is an aligned pair for packed fp32):
@@ -39,7 +40,7 @@ struct alignas(64) Inner {
     float lmin[3], lmax[3];
     float rmin[3], rmax[3];
     uint32_t child_l, child_r;
-    uint32_t aux0, aux1;   // rec: aux0 = own node index; scratch: sorted-leaf range [aux0, aux1]
+    uint32_t aux0, aux1;   // rec: aux0 = own node index, aux1 = word 15 (general-box bits)
 };
 static_assert(sizeof(Inner) == 64, "Inner must be one 64-B record");
 

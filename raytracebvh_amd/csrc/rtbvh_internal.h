@@ -45,7 +45,8 @@ struct BuildArgs {
     const uint32_t* sorted_keys;  // [T]
     const uint32_t* sorted_vals;  // [T]
     float4* leaf;             // [4T] 64-B sorted leaf records
-    Inner* inner;             // [T-1] build scratch (Karras ids + ranges, refit hand-off)
+    Inner* inner;             // [T-1] refit hand-off boxes of nodes spanning workgroups (touched for those only)
+    uint4* topo;              // [T-1] Karras node i: child_l, child_r, leaf range [lo, hi] (16 B)
     Inner* rec;               // [2T-1] node records in slots (rtbvh_device.h)
     uint32_t* pleaf;          // [T]
     uint32_t* pint;           // [T-1]
