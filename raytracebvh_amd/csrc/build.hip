@@ -318,9 +318,15 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __r
 __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
     __shared__ uint32_t s_cnt[BLOCK];
     __shared__ float s_box[BLOCK][2][6];
+    __shared__ uint4 s_topo[BLOCK];   // the block's nodes [base, base + BLOCK): ids, leaf range
+    __shared__ uint32_t s_pint[BLOCK];
     const uint32_t base = blockIdx.x * BLOCK;
     const uint32_t i = base + threadIdx.x;
     s_cnt[threadIdx.x] = 0;
+    if (i + 1 < a.T) {   // coalesced, so the in-block climb makes no dependent global loads
+        s_topo[threadIdx.x] = a.topo[i];
+        s_pint[threadIdx.x] = a.pint[i];
+    }
     __syncthreads();
     if (i >= a.T) return;
     const float4* r = a.leaf + 4 * (size_t)i;
@@ -336,9 +342,13 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
     const uint32_t end = base + BLOCK;
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
-        const uint4 q3 = a.topo[p];   // ids, leaf range
-        const uint32_t pe = a.pint[p];
-        if (!(p >= base && p < end && q3.z >= base && q3.w < end)) {      // leaves the block
+        if (!(p >= base && p < end)) {   // leaves the block
+            refit_climb(lo, hi, e, a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
+            return;
+        }
+        const uint4 q3 = s_topo[p - base];   // ids, leaf range
+        const uint32_t pe = s_pint[p - base];
+        if (!(q3.z >= base && q3.w < end)) {   // p's range crosses the block
             refit_climb(lo, hi, e, a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
             return;
         }
