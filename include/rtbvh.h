@@ -37,7 +37,8 @@ typedef enum {
     RTBVH_ERR_NOT_READY = 4,      /* e.g. trace before build, build before set_scene */
     RTBVH_ERR_STACK_OVERFLOW = 5, /* a traversal stack overflowed (never for a clz64 tree) */
     RTBVH_ERR_IO = 6,             /* scene file could not be read / parsed */
-    RTBVH_ERR_NO_DEVICE = 7
+    RTBVH_ERR_NO_DEVICE = 7,
+    RTBVH_ERR_COMM = 8            /* RCCL missing or an RCCL call failed (message has the RCCL error) */
 } rtbvh_status;
 
 /* ---- data layouts (byte-identical to the reference's HLSL structs) -------- */
@@ -193,6 +194,33 @@ rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* ctx, uint32_t width, uint32_t height, 
 rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces,
                                     uint32_t rank, uint32_t nranks, float* dev_out, void* stream);
 uint32_t rtbvh_band_rows(uint32_t height, uint32_t rank, uint32_t nranks);
+/* The frame from the ranks' compact band buffers, all on this device: buffer r (rank r's
+ * rtbvh_trace_band_async output) starts stride_rows * W * 4 floats after buffer r-1
+ * (stride_rows >= rtbvh_band_rows(H, 0, nranks)); writes W*H*4 floats to dev_frame.
+ * Enqueued on `stream` (NULL = the context stream).  rtbvh_trace_tiles uses it on rank 0. */
+rtbvh_status rtbvh_assemble_bands(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t nranks,
+                                  const float* dev_bands, uint32_t stride_rows, float* dev_frame, void* stream);
+
+/* ---- multi-GPU inside the library: one context per rank/GPU ----------
+ * For a C/C++ host with no framework of its own.  RCCL is resolved at run time: the
+ * process's librccl.so.1 if one is loaded (e.g. PyTorch's), else the system's; librtbvh.so
+ * has no link-time RCCL dependency (RTBVH_ERR_COMM if none can be loaded).
+ * rtbvh_comm_unique_id on rank 0, share the bytes with every rank (any channel), then
+ * rtbvh_comm_init on every rank.  `comm` is an ncclComm_t; a host's own communicator
+ * (one rank per GPU, same rank numbering) may be passed to rtbvh_trace_tiles instead. */
+#define RTBVH_COMM_ID_BYTES 128
+rtbvh_status rtbvh_comm_unique_id(uint8_t id[RTBVH_COMM_ID_BYTES]);
+rtbvh_status rtbvh_comm_init(rtbvh_ctx* ctx, uint32_t nranks, uint32_t rank, const uint8_t id[RTBVH_COMM_ID_BYTES],
+                             void** comm);
+rtbvh_status rtbvh_comm_destroy(void* comm);
+/* computeBVH's trace on nranks GPUs: this rank traces its 8-row bands (as
+ * rtbvh_trace_band_async), every rank sends its bands to rank 0 (ncclSend / ncclRecv on the
+ * context stream, one group) and rank 0 assembles the frame.  Collective: every rank calls
+ * it with the same W, H, bounces.  Returns when this rank's part is done; afterwards
+ * rtbvh_read_framebuffer / rtbvh_present on rank 0 give the whole frame (other ranks:
+ * RTBVH_ERR_NOT_READY). */
+rtbvh_status rtbvh_trace_tiles(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces, uint32_t rank,
+                               uint32_t nranks, void* comm);
 rtbvh_status rtbvh_synchronize(rtbvh_ctx* ctx);
 
 /* ---- outputs --------------------------------------------------------------- */

@@ -36,8 +36,10 @@ EXPORTS = [
     "rtbvh_scene_num_materials", "rtbvh_scene_num_textures", "rtbvh_scene_vertices", "rtbvh_scene_indices",
     "rtbvh_scene_mat_indices", "rtbvh_scene_materials", "rtbvh_scene_texture_path", "rtbvh_set_scene_obj",
     "rtbvh_camera_reference", "rtbvh_texture_load_bmp", "rtbvh_texture_free", "rtbvh_srgb_table",
-    "rtbvh_present", "rtbvh_save_bmp",
+    "rtbvh_present", "rtbvh_save_bmp", "rtbvh_assemble_bands", "rtbvh_comm_unique_id", "rtbvh_comm_init",
+    "rtbvh_comm_destroy", "rtbvh_trace_tiles",
 ]
+COMM_ID_BYTES = 128
 
 NODE_DTYPE = np.dtype([("parent", "<u4"), ("child_l", "<u4"), ("child_r", "<u4"), ("code", "<u4"),
                        ("bb_min", "<f4", (3,)), ("bb_max", "<f4", (3,)), ("index", "<u4")])
@@ -117,6 +119,11 @@ def lib() -> ctypes.CDLL:
         "rtbvh_compute_bvh": (i32, [vp, u32, u32, u32]),
         "rtbvh_trace_band_async": (i32, [vp, u32, u32, u32, u32, u32, vp, vp]),
         "rtbvh_band_rows": (u32, [u32, u32, u32]),
+        "rtbvh_assemble_bands": (i32, [vp, u32, u32, u32, vp, u32, vp, vp]),
+        "rtbvh_comm_unique_id": (i32, [vp]),
+        "rtbvh_comm_init": (i32, [vp, u32, u32, vp, ctypes.POINTER(vp)]),
+        "rtbvh_comm_destroy": (i32, [vp]),
+        "rtbvh_trace_tiles": (i32, [vp, u32, u32, u32, u32, u32, vp]),
         "rtbvh_synchronize": (i32, [vp]),
         "rtbvh_read_framebuffer": (i32, [vp, vp]),
         "rtbvh_read_intensity": (i32, [vp, vp]),

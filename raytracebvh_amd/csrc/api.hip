@@ -2,10 +2,14 @@
 // buffers, stream ordering and the host sequence of Graphics::computeBVH
 // (Graphics.cpp:667-831), re-done as one HIP stream of kernels with no per-frame
 // queue/allocator/fence creation and no host round trip inside build or trace.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rtbvh.h"
@@ -34,6 +38,8 @@ struct rtbvh_ctx {
     uint32_t *d_codes = nullptr, *d_ids = nullptr, *d_ka = nullptr, *d_va = nullptr, *d_kb = nullptr, *d_vb = nullptr;
     uint32_t* d_sort_scratch = nullptr;
     float4 *d_tclip = nullptr, *d_leaf = nullptr;
+    float4* d_band = nullptr;                // rtbvh_trace_tiles: this rank's bands; rank 0: all ranks'
+    size_t cap_band = 0;                     //   (float4 capacity)
     Inner* d_inner = nullptr;                // box hand-off of refit nodes spanning workgroups
     uint4* d_topo = nullptr;                 // Karras node: child ids + leaf range
     Inner* d_rec = nullptr;                  // node records in slots (rtbvh_device.h), 2T-1
@@ -61,6 +67,8 @@ struct rtbvh_ctx {
     float2* d_hit = nullptr;                  // per queued bounce ray: (t, leaf | INVALID)
     unsigned long long* d_counters = nullptr; // [8]
     bool traced = false;
+    bool frame_here = false;                 // d_color holds the last trace's whole frame
+    bool intensity_here = false;             // d_intensity holds its intensities
 
     // hipEvent rings: per build 6 events (before bounds, after bounds/morton/sort/karras/refit),
     // per trace 3 (before primary, after primary, after bounces)
@@ -201,6 +209,49 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     return a;
 }
 
+// RCCL, resolved at run time: the process's librccl.so.1 if one is already loaded (e.g.
+// PyTorch's; dlopen by SONAME returns it), else the system's.  No link-time dependency.
+struct Rccl {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+const Rccl& rccl() {
+    static const Rccl lib = [] {
+        Rccl r;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            r.err = std::string("RCCL not available: ") + (e ? e : "dlopen(librccl.so.1) failed");
+            return r;
+        }
+        bool all = true;
+        auto sym = [&](auto& f, const char* name) {
+            f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+            if (!f) all = false;
+        };
+        sym(r.GetUniqueId, "ncclGetUniqueId");
+        sym(r.CommInitRank, "ncclCommInitRank");
+        sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.Send, "ncclSend");
+        sym(r.Recv, "ncclRecv");
+        sym(r.GroupStart, "ncclGroupStart");
+        sym(r.GroupEnd, "ncclGroupEnd");
+        sym(r.GetErrorString, "ncclGetErrorString");
+        r.ok = all;
+        if (!all) r.err = "RCCL: librccl.so.1 lacks a required symbol";
+        return r;
+    }();
+    return lib;
+}
+
 rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(c, RTBVH_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -289,6 +340,8 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     c->rank = rank;
     c->nranks = nranks;
     c->traced = true;
+    c->frame_here = color == c->d_color && nranks == 1;
+    c->intensity_here = c->frame_here && inten != nullptr;
     return check_launch(c, "trace kernels");
 }
 
@@ -363,6 +416,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec);
+    dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
@@ -541,6 +595,94 @@ rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32
     return RTBVH_OK;
 }
 
+rtbvh_status rtbvh_assemble_bands(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t nranks, const float* dev_bands,
+                                  uint32_t stride_rows, float* dev_frame, void* stream) {
+    if (!c || !dev_bands || !dev_frame || W == 0 || H == 0 || nranks == 0 ||
+        stride_rows < rtbvh_band_rows(H, 0, nranks))
+        return RTBVH_ERR_INVALID_ARG;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    launch_assemble((const float4*)dev_bands, stride_rows, W, H, nranks, (float4*)dev_frame,
+                    stream ? (hipStream_t)stream : c->stream);
+    return check_launch(c, "assemble bands");
+}
+
+rtbvh_status rtbvh_comm_unique_id(uint8_t id[RTBVH_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == RTBVH_COMM_ID_BYTES, "ncclUniqueId is 128 B");
+    if (!id) return RTBVH_ERR_INVALID_ARG;
+    const Rccl& r = rccl();
+    if (!r.ok) return fail(nullptr, RTBVH_ERR_COMM, r.err);
+    ncclUniqueId u;
+    const ncclResult_t e = r.GetUniqueId(&u);
+    if (e != ncclSuccess) return fail(nullptr, RTBVH_ERR_COMM, std::string("ncclGetUniqueId: ") + r.GetErrorString(e));
+    memcpy(id, &u, sizeof(u));
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_comm_init(rtbvh_ctx* c, uint32_t nranks, uint32_t rank, const uint8_t id[RTBVH_COMM_ID_BYTES],
+                             void** comm) {
+    if (!c || !id || !comm || nranks == 0 || rank >= nranks) return RTBVH_ERR_INVALID_ARG;
+    const Rccl& r = rccl();
+    if (!r.ok) return fail(c, RTBVH_ERR_COMM, r.err);
+    HIPC(c, hipSetDevice(c->cfg.device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t cm = nullptr;
+    const ncclResult_t e = r.CommInitRank(&cm, (int)nranks, u, (int)rank);
+    if (e != ncclSuccess) return fail(c, RTBVH_ERR_COMM, std::string("ncclCommInitRank: ") + r.GetErrorString(e));
+    *comm = cm;
+    return RTBVH_OK;
+}
+
+rtbvh_status rtbvh_comm_destroy(void* comm) {
+    if (!comm) return RTBVH_ERR_INVALID_ARG;
+    const Rccl& r = rccl();
+    if (!r.ok) return fail(nullptr, RTBVH_ERR_COMM, r.err);
+    const ncclResult_t e = r.CommDestroy((ncclComm_t)comm);
+    if (e != ncclSuccess) return fail(nullptr, RTBVH_ERR_COMM, std::string("ncclCommDestroy: ") + r.GetErrorString(e));
+    return RTBVH_OK;
+}
+
+// bands of 8 rows dealt round-robin; one RCCL group of point-to-point
+// transfers into rank 0 (xGMI is point to point: each rank's shard travels its own link),
+// then the row scatter on rank 0.  Rank 0's buffer holds every rank's bands, rank r at
+// r * rows0 rows (rows0 = rank 0's band rows, the most any rank has).
+rtbvh_status rtbvh_trace_tiles(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank,
+                               uint32_t nranks, void* comm) {
+    if (!c || !comm || W == 0 || H == 0 || nranks == 0 || rank >= nranks) return RTBVH_ERR_INVALID_ARG;
+    const Rccl& r = rccl();
+    if (!r.ok) return fail(c, RTBVH_ERR_COMM, r.err);
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const uint32_t rows0 = rtbvh_band_rows(H, 0, nranks);
+    const size_t need = (size_t)(rank == 0 ? nranks : 1) * rows0 * W;
+    if (c->cap_band < need) {
+        HIPC(c, dalloc(c->d_band, need));
+        c->cap_band = need;
+    }
+    rtbvh_status st = enqueue_trace(c, W, H, bounces, rank, nranks, c->d_band, nullptr, c->stream);
+    if (st) return st;
+    const ncclComm_t cm = (ncclComm_t)comm;
+    ncclResult_t e = r.GroupStart();
+    if (rank != 0) {
+        if (e == ncclSuccess)
+            e = r.Send(c->d_band, (size_t)rtbvh_band_rows(H, rank, nranks) * W * 4, ncclFloat32, 0, cm, c->stream);
+    } else {
+        for (uint32_t q = 1; q < nranks && e == ncclSuccess; q++)
+            e = r.Recv(c->d_band + (size_t)q * rows0 * W, (size_t)rtbvh_band_rows(H, q, nranks) * W * 4, ncclFloat32,
+                       (int)q, cm, c->stream);
+    }
+    const ncclResult_t e2 = r.GroupEnd();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) return fail(c, RTBVH_ERR_COMM, std::string("band gather: ") + r.GetErrorString(e));
+    if (rank == 0) {
+        launch_assemble(c->d_band, rows0, W, H, nranks, c->d_color, c->stream);
+        st = check_launch(c, "assemble bands");
+        if (st) return st;
+    }
+    c->frame_here = rank == 0;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return RTBVH_OK;
+}
+
 rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
     if (!c) return RTBVH_ERR_INVALID_ARG;
     HIPC(c, hipStreamSynchronize(c->stream));
@@ -550,6 +692,7 @@ rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
 rtbvh_status rtbvh_read_framebuffer(rtbvh_ctx* c, float* rgba) {
     if (!c || !rgba) return RTBVH_ERR_INVALID_ARG;
     if (!c->traced) return fail(c, RTBVH_ERR_NOT_READY, "no trace yet");
+    if (!c->frame_here) return fail(c, RTBVH_ERR_NOT_READY, "the last trace was a band trace: the frame is elsewhere");
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(rgba, c->d_color, sizeof(float4) * (size_t)c->W * c->H, hipMemcpyDeviceToHost));
     return RTBVH_OK;
@@ -557,7 +700,7 @@ rtbvh_status rtbvh_read_framebuffer(rtbvh_ctx* c, float* rgba) {
 
 rtbvh_status rtbvh_read_intensity(rtbvh_ctx* c, float* inten) {
     if (!c || !inten) return RTBVH_ERR_INVALID_ARG;
-    if (!c->traced) return fail(c, RTBVH_ERR_NOT_READY, "no trace yet");
+    if (!c->traced || !c->intensity_here) return fail(c, RTBVH_ERR_NOT_READY, "no full-frame trace yet");
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(inten, c->d_intensity, sizeof(float) * (size_t)c->W * c->H, hipMemcpyDeviceToHost));
     return RTBVH_OK;
@@ -587,7 +730,7 @@ rtbvh_status rtbvh_read_bvh(rtbvh_ctx* c, rtbvh_node* out, uint32_t capacity) {
 
 rtbvh_status rtbvh_present(rtbvh_ctx* c, uint8_t* rgba8) {
     if (!c || !rgba8) return RTBVH_ERR_INVALID_ARG;
-    if (!c->traced || c->nranks != 1) return fail(c, RTBVH_ERR_NOT_READY, "present: no full-frame trace yet");
+    if (!c->traced || !c->frame_here) return fail(c, RTBVH_ERR_NOT_READY, "present: no full frame on this context");
     HIPC(c, hipSetDevice(c->cfg.device));
     const size_t n = (size_t)c->W * c->H;
     uint32_t* d = nullptr;

@@ -99,6 +99,9 @@ void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t*
                             uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, hipStream_t s);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
+// frame from per-rank compact band buffers (stride_rows rows apart), see rtbvh_assemble_bands
+void launch_assemble(const float4* bands, uint32_t stride_rows, uint32_t W, uint32_t H, uint32_t nranks,
+                     float4* frame, hipStream_t s);
 // presentation pass (RayTraceBVHPS.hlsl): flipped rows, UNORM8 RGBA
 void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, hipStream_t s);
 // coherence sort keys of a bounce queue: P entries (past *count: key 0xFFFFFFFF)

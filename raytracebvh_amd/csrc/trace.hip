@@ -1159,6 +1159,19 @@ __global__ __launch_bounds__(BLOCK) void k_present(const float4* __restrict__ co
     out[i] = unorm8(c.x) | unorm8(c.y) << 8 | unorm8(c.z) << 16 | unorm8(c.w) << 24;
 }
 
+// frame row y of a W x H frame traced as 8-row bands dealt round-robin over nranks: band
+// b = y / 8 is rank b % nranks's (b / nranks)-th band, so it sits at row (b / nranks) * 8 +
+// y % 8 of that rank's compact buffer, buffers stacked stride_rows apart (tiles.py layout)
+__global__ __launch_bounds__(BLOCK) void k_assemble(const float4* __restrict__ bands, uint32_t stride_rows,
+                                                    uint32_t W, uint32_t H, uint32_t nranks,
+                                                    float4* __restrict__ frame) {
+    const size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= (size_t)W * H) return;
+    const uint32_t y = (uint32_t)(i / W), x = (uint32_t)(i % W);
+    const uint32_t b = y >> 3, r = b % nranks, k = (b / nranks) * 8 + (y & 7u);
+    frame[i] = bands[((size_t)r * stride_rows + k) * W + x];
+}
+
 template <bool COUNT, int S>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           int mode, float2* hitrec, uint32_t* next, uint32_t refill_min, uint32_t chunk,
@@ -1242,6 +1255,13 @@ void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qi
     else
         hipLaunchKernelGGL((k_bounce_shade<false>), dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a, qin,
                            qin_count, hitrec, qout, qout_count, (int)emit);
+}
+
+void launch_assemble(const float4* bands, uint32_t stride_rows, uint32_t W, uint32_t H, uint32_t nranks,
+                     float4* frame, hipStream_t s) {
+    const size_t n = (size_t)W * H;
+    hipLaunchKernelGGL(k_assemble, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, bands, stride_rows,
+                       W, H, nranks, frame);
 }
 
 void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, hipStream_t s) {

@@ -97,6 +97,26 @@ class Context:
                                                     ctypes.c_void_p(dev_out_ptr),
                                                     ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def assemble_bands(self, width: int, height: int, nranks: int, dev_bands_ptr: int, stride_rows: int,
+                       dev_frame_ptr: int, stream_ptr: int | None = None):
+        """rtbvh_assemble_bands: the frame from the ranks' compact band buffers (one device)."""
+        self._check(_L.lib().rtbvh_assemble_bands(self._h, width, height, nranks, ctypes.c_void_p(dev_bands_ptr),
+                                                  stride_rows, ctypes.c_void_p(dev_frame_ptr),
+                                                  ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes) -> int:
+        """rtbvh_comm_init: an RCCL communicator (ncclComm_t) for this context's device."""
+        assert len(unique_id) == _L.COMM_ID_BYTES
+        comm = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * _L.COMM_ID_BYTES).from_buffer_copy(unique_id)
+        self._check(_L.lib().rtbvh_comm_init(self._h, nranks, rank, buf, ctypes.byref(comm)))
+        return comm.value
+
+    def trace_tiles(self, width: int, height: int, bounces: int, rank: int, nranks: int, comm: int):
+        """rtbvh_trace_tiles: this rank's bands + the RCCL gather; rank 0 then holds the frame."""
+        self._check(_L.lib().rtbvh_trace_tiles(self._h, width, height, bounces, rank, nranks, ctypes.c_void_p(comm)))
+        self.width, self.height = width, height
+
     def synchronize(self):
         self._check(_L.lib().rtbvh_synchronize(self._h))
 
@@ -226,6 +246,18 @@ class Graphics:
 
     def onDestroy(self):  # noqa: N802
         self.ctx.close()
+
+
+def comm_unique_id() -> bytes:
+    """rtbvh_comm_unique_id: the 128-B RCCL id rank 0 creates and shares with every rank."""
+    buf = (ctypes.c_uint8 * _L.COMM_ID_BYTES)()
+    _L.check(_L.lib().rtbvh_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def comm_destroy(comm: int):
+    """rtbvh_comm_destroy."""
+    _L.check(_L.lib().rtbvh_comm_destroy(ctypes.c_void_p(comm)))
 
 
 def save_bmp(path: str, rgba8: np.ndarray):

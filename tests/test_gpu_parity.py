@@ -519,6 +519,55 @@ def test_band_split_reassembles_full_frame(nranks):
     np.testing.assert_array_equal(frame, full)
 
 
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_assemble_bands_matches_full_frame(nranks):
+    """rtbvh_assemble_bands (rank 0's step of rtbvh_trace_tiles): the ranks' band buffers,
+    stacked as RCCL delivers them, give the full frame; after a band trace the context
+    reports that its framebuffer is not a frame."""
+    import torch
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    W, H = 640, 357
+    with rt.Context(device=0, flags=rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(W, H))
+        c.compute_bvh(W, H, 1)
+        full = c.read_framebuffer()
+        rows0 = rt.lib().rtbvh_band_rows(H, 0, nranks)
+        bands = torch.full((nranks, rows0, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
+        for r in range(nranks):
+            c.trace_band_async(W, H, 1, r, nranks, bands[r].data_ptr())
+        frame = torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0")
+        c.assemble_bands(W, H, nranks, bands.data_ptr(), rows0, frame.data_ptr())
+        c.synchronize()
+        np.testing.assert_array_equal(frame.cpu().numpy(), full)
+        with pytest.raises(rt.RtbvhError) as e:
+            c.read_framebuffer()
+        assert e.value.status == 4
+
+
+def test_trace_tiles_one_rank_matches_trace():
+    """rtbvh_comm_* + rtbvh_trace_tiles through RCCL with one rank (a box has one GPU, and
+    RCCL takes one rank per device): the frame on rank 0 equals rtbvh_trace's.  More ranks
+    reuse the same calls; their assembly is test_assemble_bands_matches_full_frame."""
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    W, H = 640, 357
+    with rt.Context(device=0, flags=rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(W, H))
+        c.compute_bvh(W, H, 1)
+        full = c.read_framebuffer()
+        shown = c.present()
+        comm = c.comm_init(1, 0, rt.comm_unique_id())
+        try:
+            c.trace_tiles(W, H, 1, 0, 1, comm)
+            np.testing.assert_array_equal(c.read_framebuffer(), full)
+            np.testing.assert_array_equal(c.present(), shown)
+        finally:
+            rt.comm_destroy(comm)
+
+
 def test_errors_are_reported():
     with rt.Context(device=0) as c:
         with pytest.raises(rt.RtbvhError) as e:
