@@ -88,6 +88,16 @@ def load_pmc(workload, mode, kernel):
         return None
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(rt, scene, ctx, wl, W, H):
     """Oracle (single-thread C++ restatement of the reference path) on a bounded sample."""
     from oracle import lib as orc
@@ -100,8 +110,23 @@ def cpu_baseline(rt, scene, ctx, wl, W, H):
     dt = time.perf_counter() - t0
     rays = st["primary"] + st["bounce"]
     res = {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-           "sample": f"oracle/liboracle.so orc_trace of every {step}th row of the same frame and BVH "
-                     f"({st['primary']} primary + {st['bounce']} bounce rays, {dt:.1f} s, 1 thread)"}
+           "sample": f"oracle/liboracle.so orc_trace of 1 row in {step} of the same frame and BVH "
+                     f"({st['primary']} primary + {st['bounce']} bounce rays, {dt:.1f} s, 1 thread)",
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
+    # BASELINE.md's all-cores variant: the same code, OpenMP over rows, on this process's CPU
+    # share (OMP_NUM_THREADS, 16 on the GPU boxes), on a 4x larger sample
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    step_all = max(1, step // 4)
+    orc.set_threads(threads)
+    try:
+        t0 = time.perf_counter()
+        _, _, st2 = orc.trace(osc, nodes, wvp, wv, W, H, wl["bounces"], 0, H, step_all)
+        dt2 = time.perf_counter() - t0
+    finally:
+        orc.set_threads(1)
+    res["all_cores"] = {"value": (st2["primary"] + st2["bounce"]) / dt2 / 1e6, "unit": "Mrays/s", "cores": threads,
+                        "sample": f"1 row in {step_all}, {st2['primary']} primary + {st2['bounce']} bounce rays, "
+                                  f"{dt2:.1f} s, OpenMP over rows"}
     # build baseline: reference-faithful 32 x 1-bit split sort + Karras + refit on a 1M-triangle sample
     n_s = 1_000_000
     sub = rt.Scene(scene.vertices[: 3 * n_s], scene.indices[: 3 * n_s], scene.mat_indices[:n_s], scene.materials)

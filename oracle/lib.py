@@ -77,6 +77,7 @@ def lib():
         L.orc_fnv1a64.restype = ctypes.c_uint64
         L.orc_fnv1a64.argtypes = [u32p, ctypes.c_uint64]
         L.orc_num_threads.restype = ctypes.c_int
+        L.orc_set_threads.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
 
@@ -225,6 +226,11 @@ def camera_reference(W, H):
     wv = np.zeros(16, dtype=np.float32)
     lib().orc_camera_reference(W, H, _p(wvp), _p(wv))
     return wvp.reshape(4, 4), wv.reshape(4, 4)
+
+
+def set_threads(n: int) -> None:
+    """Threads trace() uses over rows (default 1; the result does not depend on it)."""
+    lib().orc_set_threads(int(n))
 
 
 def fnv1a64(a: np.ndarray) -> int:

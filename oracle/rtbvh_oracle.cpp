@@ -17,6 +17,10 @@
 #endif
 
 namespace {
+int g_threads = 1;   // orc_trace_ex row parallelism (orc_set_threads)
+}  // namespace
+
+namespace {
 
 inline float fmin_h(float a, float b) { return fminf(a, b); }   // HLSL min: NaN-dropping
 inline float fmax_h(float a, float b) { return fmaxf(a, b); }
@@ -577,10 +581,18 @@ int orc_trace_ex(const orc_scene* s, const orc_node* nodes, uint32_t n, const fl
                  uint32_t row_end, uint32_t row_step, float* rgba, float* intensity_out,
                  uint64_t* counters, float* refl_rec, float* refr_rec) {
     if (n == 0 || row_step == 0) return 1;
-    uint64_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t total[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const float hw = (float)(W >> 1), hh = (float)(H >> 1);
-    uint64_t out_row = 0;
-    for (uint32_t y = row_begin; y < row_end && y < H; y += row_step, out_row++) {
+    const uint32_t last = row_end < H ? row_end : H;
+    const int64_t nrows = row_begin < last ? ((int64_t)last - row_begin + row_step - 1) / row_step : 0;
+    // rows are independent: OpenMP over rows when orc_set_threads(n > 1) (the all-cores CPU
+    // baseline); each thread sums its own counters, merged at the end (same totals)
+#pragma omp parallel num_threads(g_threads)
+    {
+    uint64_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t out_row = 0; out_row < nrows; out_row++) {
+        const uint32_t y = row_begin + (uint32_t)out_row * row_step;
         for (uint32_t x = 0; x < W; x++) {
             Ctx c{s, nodes, n, wvp, wv, 0, 0, 0, 0};
             // RayTraceLaunch.hlsl:23-30
@@ -653,7 +665,13 @@ int orc_trace_ex(const orc_scene* s, const orc_node* nodes, uint32_t n, const fl
             if (c.max_depth > cnt[7]) cnt[7] = c.max_depth;
         }
     }
-    if (counters) for (int k = 0; k < 8; k++) counters[k] = cnt[k];
+#pragma omp critical
+    {
+        for (int k = 0; k < 7; k++) total[k] += cnt[k];
+        if (cnt[7] > total[7]) total[7] = cnt[7];
+    }
+    }
+    if (counters) for (int k = 0; k < 8; k++) counters[k] = total[k];
     return 0;
 }
 
@@ -691,6 +709,8 @@ uint64_t orc_fnv1a64(const void* data, uint64_t nbytes) {
     for (uint64_t i = 0; i < nbytes; i++) { h ^= p[i]; h *= 1099511628211ull; }
     return h;
 }
+
+void orc_set_threads(int n) { g_threads = n > 0 ? n : 1; }
 
 int orc_num_threads(void) {
 #ifdef _OPENMP

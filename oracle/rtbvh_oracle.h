@@ -125,6 +125,8 @@ void orc_sample_texture(const orc_texture* t, float u, float v, float out[4]);
 void orc_camera_reference(uint32_t W, uint32_t H, float wvp[16], float wv[16]);
 uint64_t orc_fnv1a64(const void* data, uint64_t nbytes);
 int orc_num_threads(void);
+/* threads orc_trace / orc_trace_ex use over rows (default 1; results are identical) */
+void orc_set_threads(int n);
 
 #ifdef __cplusplus
 }
