@@ -120,6 +120,8 @@ enum {
     RTBVH_FLAG_WIDE_BVH = 1u << 7,        /* trace: walk the node records 4-wide (a node's four grandchild
                                              boxes share one 128-B line), keeping the lexicographic
                                              (t, leaf) minimum as NEAREST_FIRST does */
+    RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
+                                              build instead of the one-workgroup build (same output) */
     /* bits 8..15: kernel variant for A/B measurement (0 = default, 1 = first version) */
     RTBVH_FLAG_VARIANT_SHIFT = 8
 };

@@ -21,6 +21,7 @@ FLAG_TIMING, FLAG_COUNT_VISITS, FLAG_REFRACT_RECORDS, FLAG_SORT_BOUNCE, FLAG_NEA
 FLAG_PACKET_PRIMARY = 1 << 5
 FLAG_REFILL_BOUNCE = 1 << 6
 FLAG_WIDE_BVH = 1 << 7
+FLAG_MULTI_KERNEL_BUILD = 1 << 16
 FLAG_VARIANT_SHIFT = 8
 
 # every symbol include/rtbvh.h declares (tests check the library exports them all)

@@ -521,6 +521,17 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     BuildArgs a = build_args(c);
     hipEvent_t* ev = c->evb[c->n_builds % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
+    if (c->T <= small_build_max() && !(c->cfg.flags & RTBVH_FLAG_MULTI_KERNEL_BUILD)) {
+        // one workgroup (build.hip k_build_small); its time is reported as stage 0
+        c->sorted = SortResult{c->d_ka, c->d_va};
+        a.sorted_keys = c->d_ka;
+        a.sorted_vals = c->d_va;
+        launch_build_small(a, s);
+        if (timing) for (int k = 1; k <= 5; k++) HIPC(c, hipEventRecord(ev[k], s));
+        if (timing) c->n_builds++;
+        c->built = true;
+        return check_launch(c, "build kernel");
+    }
     if (c->cfg.morton_mode == RTBVH_MORTON_CPUTESTS) {
         launch_bounds(a, s);
     }

@@ -96,10 +96,9 @@ __global__ __launch_bounds__(BLOCK) void k_bounds_final(float* __restrict__ boun
     }
 }
 
-// MortonCodes.hlsl:54-125 (HLSL mode) / ShaderSim/main.cpp:292-301 (CPUTests mode)
-__global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= a.T) return;
+// MortonCodes.hlsl:54-125 (HLSL mode) / ShaderSim/main.cpp:292-301 (CPUTests mode):
+// triangle t's code (also stored in keys/vals) and its clip-space triangle
+__device__ __forceinline__ uint32_t morton_tri(const BuildArgs& a, uint32_t t) {
     const uint32_t i0 = a.idx[3 * (size_t)t], i1 = a.idx[3 * (size_t)t + 1], i2 = a.idx[3 * (size_t)t + 2];
     const float4 q0 = a.opos[i0], q1 = a.opos[i1], q2 = a.opos[i2];
     const f3 p0 = mk(q0.x, q0.y, q0.z), p1 = mk(q1.x, q1.y, q1.z), p2 = mk(q2.x, q2.y, q2.z);
@@ -128,12 +127,23 @@ __global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
     o[0] = make_float4(c0.x, c0.y, c0.z, __uint_as_float(t));
     o[1] = make_float4(c1.x, c1.y, c1.z, 0.f);
     o[2] = make_float4(c2.x, c2.y, c2.z, 0.f);
+    return code;
+}
+__global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < a.T) morton_tri(a, t);
 }
 
 // ---- Karras 2012 (BVHConstructP1.hlsl:61-165) --------------------------------
-__device__ __forceinline__ int delta_clz64(const uint32_t* __restrict__ c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
+// `c` is the sorted code sequence: a pointer, or an accessor c(j) (the one-workgroup build
+// reads the codes from LDS)
+template <class C>
+__device__ __forceinline__ uint32_t code_at(const C& c, int64_t j) { return c[j]; }
+
+template <class C>
+__device__ __forceinline__ int delta_clz64(const C& c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
     if (j < 0 || j >= n) return -1;   // leadingPrefixBounds :78-84
-    const uint32_t cj = c[j];
+    const uint32_t cj = code_at(c, j);
     return ci != cj ? __clz((int)(ci ^ cj)) : 32 + __clz((int)(i ^ (uint32_t)j));
 }
 __device__ __forceinline__ int debruijn_lz(uint32_t data) {   // RadixBVHCombo/main.cpp:136-151
@@ -143,22 +153,23 @@ __device__ __forceinline__ int debruijn_lz(uint32_t data) {   // RadixBVHCombo/m
     data++;
     return data ? tbl[(uint32_t)(data * 0x076be629u) >> 27] : 32;
 }
-__device__ __forceinline__ int delta_cputests(const uint32_t* __restrict__ c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
+template <class C>
+__device__ __forceinline__ int delta_cputests(const C& c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
     if (j < 0 || j >= n) return -1;
-    const uint32_t cj = c[j];
+    const uint32_t cj = code_at(c, j);
     return debruijn_lz(ci == cj ? (i ^ (uint32_t)j) : (ci ^ cj));
 }
 
-template <int MODE>
-__device__ __forceinline__ int delta(const uint32_t* c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
+template <int MODE, class C>
+__device__ __forceinline__ int delta(const C& c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
     return MODE == 0 ? delta_clz64(c, n, i, ci, j) : delta_cputests(c, n, i, ci, j);
 }
 
-template <int MODE>
-__device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t i, uint4* __restrict__ topo,
+template <int MODE, class C>
+__device__ void karras_node(const C& c, uint32_t n, uint32_t i, uint4* __restrict__ topo,
                             uint32_t* __restrict__ pleaf, uint32_t* __restrict__ pint) {
     const int64_t N = n, I = i;
-    const uint32_t ci = c[i];
+    const uint32_t ci = code_at(c, I);
     const int64_t d = delta<MODE>(c, N, i, ci, I + 1) < delta<MODE>(c, N, i, ci, I - 1) ? -1 : 1;
     const int min_lz = delta<MODE>(c, N, i, ci, I - d);
     int64_t bound_len = 2;
@@ -187,13 +198,10 @@ __device__ void karras_node(const uint32_t* __restrict__ c, uint32_t n, uint32_t
     if (right_leaf) pleaf[r] = (i << 1) | 1u; else pint[r] = (i << 1) | 1u;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= a.T) return;
-    // leaf record of sorted position i: gather the clip-space triangle once, store
-    // (v0, e1, e2) for the triangle test (the reference's edge1/edge2, :43-44) and
-    // the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
+// leaf record of sorted position i: gather the clip-space triangle once, store
+// (v0, e1, e2) for the triangle test (the reference's edge1/edge2, :43-44) and
+// the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
+__device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i) {
     const uint32_t t = a.sorted_vals[i];
     const float4* src = a.tclip + 3 * (size_t)t;
     const float4 s0 = src[0], s1 = src[1], s2 = src[2];
@@ -207,6 +215,12 @@ __global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
     dst[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
     dst[2] = make_float4(e2.z, __uint_as_float(t), lo.x, lo.y);
     dst[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
+}
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= a.T) return;
+    leaf_record(a, i);
     if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
     if (i == 0 && a.T > 1) a.pint[0] = INVALID;   // root (BVHConstructP1.hlsl:186-187)
 }
@@ -386,6 +400,143 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
     refit_climb(lo, hi, a.pleaf[i], a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
 }
 
+// ---- small scenes: the whole build in one workgroup ------------------------------
+// The reference's own meshes (Test.obj: 1,952 triangles) rebuild every frame
+// (Graphics.cpp:56), and at that size the multi-kernel build is ~18 dependent launches of
+// almost no work.  One 1024-thread workgroup does it all with the same arithmetic (the
+// mesh box reduction, morton_tri, leaf_record, karras_node, store_record), everything but
+// the outputs resident in LDS (152 KB of the CU's 160):
+//  - the sort is a bitonic network over 64-bit (code << 32 | triangle) keys: a total order
+//    on distinct keys, hence exactly the stable radix sort's (code, triangle) order;
+//  - Karras reads the codes from LDS;
+//  - the refit is k_refit's in-block protocol for every node (LDS boxes and tickets).
+// Outputs land in the multi-kernel build's buffers (the sorted pairs in the sort's A
+// buffers), so every later kernel and export is unchanged.
+constexpr uint32_t SMALL_BLOCK = 1024;
+constexpr uint32_t SMALL_T = 2048;
+
+struct LdsCodes {   // sorted code j = the high word of the sorted 64-bit key
+    const uint64_t* kv;
+    __device__ uint32_t operator[](int64_t j) const { return (uint32_t)(kv[j] >> 32); }
+};
+
+template <int MODE>
+__global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32_t* __restrict__ sk,
+                                                             uint32_t* __restrict__ sv) {
+    __shared__ uint64_t s_kv[SMALL_T];
+    __shared__ uint2 s_ids[SMALL_T];        // node k: child ids
+    __shared__ uint32_t s_pint[SMALL_T];    // node k: parent << 1 | side (INVALID: root)
+    __shared__ uint32_t s_pleaf[SMALL_T];   // leaf j: parent << 1 | side
+    __shared__ float s_box[SMALL_T][2][6];
+    __shared__ uint32_t s_cnt[SMALL_T];
+    __shared__ float s_red[16 * 6];
+    const uint32_t tid = threadIdx.x, T = a.T;
+    for (uint32_t k = tid; k < SMALL_T; k += SMALL_BLOCK) s_cnt[k] = 0;
+    if (a.morton_mode == 0) {   // k_bounds + k_bounds_final as one reduction
+        f3 mn = mk(INFINITY, INFINITY, INFINITY), mx = mk(-INFINITY, -INFINITY, -INFINITY);
+        for (uint32_t i = tid; i < a.V; i += SMALL_BLOCK) {
+            const float4 p = a.opos[i];
+            mn = vmin(mn, mk(p.x, p.y, p.z));
+            mx = vmax(mx, mk(p.x, p.y, p.z));
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            mn.x = fminf(mn.x, __shfl_xor(mn.x, off, 64));
+            mn.y = fminf(mn.y, __shfl_xor(mn.y, off, 64));
+            mn.z = fminf(mn.z, __shfl_xor(mn.z, off, 64));
+            mx.x = fmaxf(mx.x, __shfl_xor(mx.x, off, 64));
+            mx.y = fmaxf(mx.y, __shfl_xor(mx.y, off, 64));
+            mx.z = fmaxf(mx.z, __shfl_xor(mx.z, off, 64));
+        }
+        const uint32_t w = tid >> 6;
+        if ((tid & 63) == 0) {
+            s_red[6 * w + 0] = mn.x; s_red[6 * w + 1] = mn.y; s_red[6 * w + 2] = mn.z;
+            s_red[6 * w + 3] = mx.x; s_red[6 * w + 4] = mx.y; s_red[6 * w + 5] = mx.z;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int k = 1; k < 16; k++) {
+                mn = vmin(mn, mk(s_red[6 * k + 0], s_red[6 * k + 1], s_red[6 * k + 2]));
+                mx = vmax(mx, mk(s_red[6 * k + 3], s_red[6 * k + 4], s_red[6 * k + 5]));
+            }
+            a.bounds[0] = mn.x; a.bounds[1] = mn.y; a.bounds[2] = mn.z;
+            a.bounds[3] = mx.x; a.bounds[4] = mx.y; a.bounds[5] = mx.z;
+        }
+        __syncthreads();   // morton_tri reads the box back (same workgroup: visible)
+    }
+    uint32_t n = 1;
+    while (n < T) n <<= 1;
+    for (uint32_t t = tid; t < n; t += SMALL_BLOCK)
+        s_kv[t] = t < T ? ((uint64_t)morton_tri(a, t) << 32 | t) : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < n; i += SMALL_BLOCK) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = s_kv[i], y = s_kv[l];
+                    if ((x > y) == ((i & k) == 0)) { s_kv[i] = y; s_kv[l] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
+        sk[i] = (uint32_t)(s_kv[i] >> 32);
+        sv[i] = (uint32_t)s_kv[i];
+    }
+    __syncthreads();   // sorted ids (leaf_record) and clip triangles visible to the block
+    const LdsCodes codes{s_kv};
+    for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
+        leaf_record(a, i);
+        if (i + 1 < T) karras_node<MODE>(codes, T, i, a.topo, a.pleaf, a.pint);
+    }
+    if (tid == 0 && T > 1) a.pint[0] = INVALID;
+    __syncthreads();   // links written by other threads: copy them into LDS
+    for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
+        s_pleaf[i] = a.pleaf[i];
+        if (i + 1 < T) {
+            const uint4 q = a.topo[i];
+            s_ids[i] = make_uint2(q.x, q.y);
+            s_pint[i] = a.pint[i];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
+        const float4* r = a.leaf + 4 * (size_t)i;
+        const float4 b0 = r[2], b1 = r[3];
+        f3 lo = mk(b0.z, b0.w, b1.x), hi = mk(b1.y, b1.z, b1.w);
+        if (T == 1) {
+            a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
+            a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+            continue;
+        }
+        uint32_t e = s_pleaf[i];
+        store_record(a.rec + e, lo, hi, lo, hi, LEAF_BIT | i, INVALID, LEAF_BIT | i);
+        for (int level = 0; level < 2 * STACK_SIZE; level++) {   // k_refit's in-block protocol
+            const uint32_t p = e >> 1, side = e & 1u;
+            float* sb = s_box[p][side];
+            sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the LDS box lands before the ticket
+            if (atomicAdd(&s_cnt[p], 1u) == 0) break;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const float* ob = s_box[p][side ^ 1u];
+            const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
+            const uint2 ids = s_ids[p];
+            e = s_pint[p];
+            if (side) store_record(a.rec + slot_of(e, T), smin, smax, lo, hi, ids.x, ids.y, p);
+            else      store_record(a.rec + slot_of(e, T), lo, hi, smin, smax, ids.x, ids.y, p);
+            if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
+            else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
+            if (e == INVALID) {
+                a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
+                a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+                break;
+            }
+        }
+    }
+}
+
 // reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k
 struct RefNode { uint32_t parent, child_l, child_r, code; float bb_min[3], bb_max[3]; uint32_t index; };
 static_assert(sizeof(RefNode) == 44, "44-B Node");
@@ -440,6 +591,13 @@ void launch_morton(const BuildArgs& a, hipStream_t s) {
 void launch_leaf_karras(const BuildArgs& a, hipStream_t s) {
     if (a.delta_mode == 0) hipLaunchKernelGGL(k_leaf_karras<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
     else hipLaunchKernelGGL(k_leaf_karras<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+}
+uint32_t small_build_max() { return SMALL_T; }
+void launch_build_small(const BuildArgs& a, hipStream_t s) {
+    uint32_t* sk = const_cast<uint32_t*>(a.sorted_keys);
+    uint32_t* sv = const_cast<uint32_t*>(a.sorted_vals);
+    if (a.delta_mode == 0) hipLaunchKernelGGL(k_build_small<0>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
+    else hipLaunchKernelGGL(k_build_small<1>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
 }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);

@@ -57,6 +57,10 @@ void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
 void launch_leaf_karras(const BuildArgs& a, hipStream_t s);
 void launch_refit(const BuildArgs& a, hipStream_t s);
+// the whole build in one workgroup for T <= small_build_max() (sorted pairs into
+// a.sorted_keys / a.sorted_vals, which must be writable)
+uint32_t small_build_max();
+void launch_build_small(const BuildArgs& a, hipStream_t s);
 // reference-layout export (44-B Node), 2T-1 entries
 void launch_export(const BuildArgs& a, void* out_nodes, hipStream_t s);
 // Karras + refit from given sorted codes and leaf boxes (n x 6 floats, device)

@@ -10,11 +10,17 @@ import torch  # noqa: F401  (the HIP runtime torch loads; see raytracebvh_amd/_l
 import raytracebvh_amd as rt
 
 iters = int(os.environ.get("ITERS", "20"))
-s = rt.synthetic(10_000_000, seed=0x5EED0004, half_extent=(50.0, 50.0, 50.0))
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+scene_name = os.environ.get("SCENE", "c4")   # c4 | Test | Image_Test | Rect (tests/golden/scenes)
+if scene_name == "c4":
+    s = rt.synthetic(10_000_000, seed=0x5EED0004, half_extent=(50.0, 50.0, 50.0))
+else:
+    s = rt.load_npz(os.path.join(REPO, "tests", "golden", "scenes", scene_name + ".npz"))
+extra = int(os.environ.get("BUILD_FLAGS", "0"), 0)
 wvp, wv = rt.camera_reference(1920, 1080)
 out = []
 for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
-    with rt.Context(device=0, flags=rt.FLAG_TIMING) as c:
+    with rt.Context(device=0, flags=rt.FLAG_TIMING | extra) as c:
         c.set_scene(s)
         c.set_camera(wvp, wv)
         c.build()
@@ -24,5 +30,6 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
         c.synchronize()
         st = c.stats()
     out.append([round(x, 4) for x in st["ms_stage"][:5]])
-print(json.dumps({"lib": os.path.basename(os.environ.get("RTBVH_LIB", "librtbvh.so")), "stages_ms": out,
+print(json.dumps({"lib": os.path.basename(os.environ.get("RTBVH_LIB", "librtbvh.so")), "scene": scene_name,
+                  "flags": extra, "stages_ms": out,
                   "total_ms": [round(sum(x), 4) for x in out]}))

@@ -568,6 +568,34 @@ def test_trace_tiles_one_rank_matches_trace():
             rt.comm_destroy(comm)
 
 
+def _build_outputs(s, flags, morton_mode=0, delta_mode=0):
+    with rt.Context(device=0, flags=flags, morton_mode=morton_mode, delta_mode=delta_mode) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(640, 360))
+        c.build()
+        out = {"nodes": c.read_bvh(), "morton": c.read_morton(), "sorted": c.read_sorted()}
+        if s.num_tris > 1:
+            out["wide"] = c.read_wide()
+    return out
+
+
+@pytest.mark.parametrize("ntris", [1, 2, 3, 57, 1000, 2047, 2048, 2049])
+@pytest.mark.parametrize("modes", [(0, 0), (1, 0), (0, 1)])
+def test_one_workgroup_build_equals_multi_kernel_build(ntris, modes):
+    """Scenes of <= 2048 triangles build in one workgroup (build.hip k_build_small): the
+    exported tree, Morton codes, sorted order and every node record equal the multi-kernel
+    build's, for both Morton modes and both delta modes."""
+    s = rt.synthetic(ntris, seed=ntris, half_extent=(30, 30, 20))
+    a = _build_outputs(s, 0, *modes)
+    b = _build_outputs(s, rt.FLAG_MULTI_KERNEL_BUILD, *modes)
+    np.testing.assert_array_equal(a["nodes"], b["nodes"])
+    np.testing.assert_array_equal(a["morton"], b["morton"])
+    for x, y in zip(a["sorted"], b["sorted"]):
+        np.testing.assert_array_equal(x, y)
+    if "wide" in a:
+        np.testing.assert_array_equal(a["wide"], b["wide"])
+
+
 def test_errors_are_reported():
     with rt.Context(device=0) as c:
         with pytest.raises(rt.RtbvhError) as e:
