@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RTBVH_ABI_VERSION 1
+#define RTBVH_ABI_VERSION 2
 
 typedef enum {
     RTBVH_OK = 0,
@@ -123,7 +123,10 @@ enum {
     RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
                                               build instead of the one-workgroup build (same output) */
     /* bits 8..15: kernel variant for A/B measurement (0 = default, 1 = first version) */
-    RTBVH_FLAG_VARIANT_SHIFT = 8
+    RTBVH_FLAG_VARIANT_SHIFT = 8,
+    /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n
+       independent primary -> bounce kernel chains on n streams (same results) */
+    RTBVH_FLAG_SPLIT_SHIFT = 17
 };
 
 typedef struct {
@@ -152,6 +155,9 @@ typedef struct {
      * traversal, those with both a leaf lane and an internal-node lane, and active lanes
      * summed over iterations (lane utilisation = active_lanes / (64 * wave_steps)) */
     uint64_t trav_wave_steps, trav_mixed_steps, trav_active_lanes;
+    /* ... and the walk length of the bounce rays (loop iterations per ray): the longest,
+     * and a histogram, [k] = rays of floor(log2(iterations)) == k */
+    uint64_t trav_max_steps, trav_steps_log2[32];
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 

@@ -23,6 +23,7 @@ FLAG_REFILL_BOUNCE = 1 << 6
 FLAG_WIDE_BVH = 1 << 7
 FLAG_MULTI_KERNEL_BUILD = 1 << 16
 FLAG_VARIANT_SHIFT = 8
+FLAG_SPLIT_SHIFT = 17   # trace chains: (n << FLAG_SPLIT_SHIFT), 0 = automatic
 
 # every symbol include/rtbvh.h declares (tests check the library exports them all)
 EXPORTS = [
@@ -69,7 +70,8 @@ class Stats(ctypes.Structure):
                 ("stack_overflows", ctypes.c_uint64), ("timed_builds", ctypes.c_uint32),
                 ("timed_traces", ctypes.c_uint32), ("ms_build", ctypes.c_float), ("ms_trace", ctypes.c_float),
                 ("ms_stage", ctypes.c_float * 8), ("trav_wave_steps", ctypes.c_uint64),
-                ("trav_mixed_steps", ctypes.c_uint64), ("trav_active_lanes", ctypes.c_uint64)]
+                ("trav_mixed_steps", ctypes.c_uint64), ("trav_active_lanes", ctypes.c_uint64),
+                ("trav_max_steps", ctypes.c_uint64), ("trav_steps_log2", ctypes.c_uint64 * 32)]
 
     def as_dict(self) -> dict:
         d = {}

@@ -63,9 +63,20 @@ struct rtbvh_ctx {
     RayQ* d_q[2] = {nullptr, nullptr};
     uint32_t *d_bkin = nullptr, *d_bvin = nullptr, *d_bka = nullptr, *d_bva = nullptr, *d_bkb = nullptr,
              *d_bvb = nullptr, *d_bscratch = nullptr;   // bounce coherence sort
-    uint32_t* d_qcount = nullptr;             // [32]: queue counts [0..15], bounce work counters [16..31]
+    uint32_t* d_qcount = nullptr;             // [32 x MAXSPLIT]: per pipeline, queue counts [0..15] and
+                                              //   bounce work counters [16..31]
     float2* d_hit = nullptr;                  // per queued bounce ray: (t, leaf | INVALID)
-    unsigned long long* d_counters = nullptr; // [8]
+    // pipelines 1.. of a split trace (pipeline 0 = d_q / d_hit on the context stream): a
+    // rank's bands dealt over `nsplit` independent primary -> bounce chains on their own
+    // streams, so one chain's kernel tail overlaps the others' work
+    static constexpr uint32_t MAXSPLIT = 4;
+    RayQ* d_qs[MAXSPLIT][2] = {};
+    float2* d_hits[MAXSPLIT] = {};
+    size_t cap_split = 0;                     // rays per pipeline queue
+    hipStream_t sub[MAXSPLIT] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[MAXSPLIT] = {};
+    uint32_t nsplit = 1;                      // pipelines of the last trace
+    unsigned long long* d_counters = nullptr; // [64]: see rtbvh_get_stats
     bool traced = false;
     bool frame_here = false;                 // d_color holds the last trace's whole frame
     bool intensity_here = false;             // d_intensity holds its intensities
@@ -149,9 +160,38 @@ rtbvh_status ensure_trace_capacity(rtbvh_ctx* c, size_t P) {
     HIPC(c, dalloc(c->d_bvb, P));
     HIPC(c, dalloc(c->d_bscratch, sort_scratch_words((uint32_t)P)));
     HIPC(c, dalloc(c->d_hit, P));
-    if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 32));
-    if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 16));
+    if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 32 * rtbvh_ctx::MAXSPLIT));
+    if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 64));
     c->cap_P = P;
+    return RTBVH_OK;
+}
+
+// chains of a trace (enqueue_trace): RTBVH_FLAG_SPLIT_SHIFT bits, 0 = automatic
+uint32_t trace_split(const rtbvh_ctx* c, size_t pixels) {
+    const uint32_t v = (c->cfg.flags >> RTBVH_FLAG_SPLIT_SHIFT) & 7u;
+    (void)pixels;
+    if (v) return v < rtbvh_ctx::MAXSPLIT ? v : rtbvh_ctx::MAXSPLIT;
+    return 1;
+}
+
+rtbvh_status ensure_split_capacity(rtbvh_ctx* c, uint32_t nsplit, size_t rays) {
+    if (nsplit < 2) return RTBVH_OK;
+    const bool grow = rays > c->cap_split;
+    if (grow) {   // every chain's queues hold cap_split rays: drop the smaller ones
+        c->cap_split = rays;
+        for (uint32_t g = nsplit; g < rtbvh_ctx::MAXSPLIT; g++) {
+            dfree(c->d_qs[g][0]); dfree(c->d_qs[g][1]); dfree(c->d_hits[g]);
+        }
+    }
+    for (uint32_t g = 1; g < nsplit; g++) {
+        if (!c->sub[g]) HIPC(c, hipStreamCreateWithFlags(&c->sub[g], hipStreamNonBlocking));
+        if (!c->ev_join[g]) HIPC(c, hipEventCreateWithFlags(&c->ev_join[g], hipEventDisableTiming));
+        if (!c->ev_fork) HIPC(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        if (c->d_qs[g][0] && !grow) continue;
+        HIPC(c, dalloc(c->d_qs[g][0], c->cap_split));
+        HIPC(c, dalloc(c->d_qs[g][1], c->cap_split));
+        HIPC(c, dalloc(c->d_hits[g], c->cap_split));
+    }
     return RTBVH_OK;
 }
 
@@ -202,6 +242,8 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.H = H;
     a.rank = rank;
     a.nranks = nranks;
+    a.band0 = 0;
+    a.bstep = 1;
     memcpy(a.wv.m, c->wv, sizeof(c->wv));
     a.color = color;
     a.intensity = inten;
@@ -269,10 +311,8 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool count = (c->cfg.flags & RTBVH_FLAG_COUNT_VISITS) != 0;
     const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream;
     TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
-    HIPC(c, hipMemsetAsync(c->d_qcount, 0, 32 * sizeof(uint32_t), s));
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), s));
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 64 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
-    if (timing) HIPC(c, hipEventRecord(ev[0], s));
     // kernel variant: 0 reference order, 1 nearest-first, 2 first version (A/B)
     int variant = (c->cfg.flags & RTBVH_FLAG_NEAREST_FIRST) ? 1 : 0;
     const uint32_t vsel = (c->cfg.flags >> RTBVH_FLAG_VARIANT_SHIFT) & 255u;
@@ -309,26 +349,55 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         a.refr_rec = c->d_refr_rec;
     }
     c->rec_P = records ? P : 0;
-    launch_primary(a, c->d_q[0], &c->d_qcount[0], count, bounces > 0, pvariant, s);
-    if (timing) HIPC(c, hipEventRecord(ev[1], s));
-    for (uint32_t b = 0; b < bounces; b++) {
-        const uint32_t* perm = nullptr;
-        if (sort) {
-            launch_bounce_keys(c->d_q[b & 1], &c->d_qcount[b], c->d_rootbox, P, c->d_bkin, c->d_bvin, s);
-            perm = radix_sort_pairs(c->d_bkin, c->d_bvin, c->d_bka, c->d_bva, c->d_bkb, c->d_bvb, P, 30,
-                                    c->d_bscratch, s).vals;
+    // pipelines: the rank's bands dealt round-robin over nsplit primary -> bounce chains
+    // (band k of this rank goes to chain k % nsplit), each with its own queues and work
+    // counters, chain 0 on the context stream, chain g on sub[g]; joined before the end event
+    const uint32_t nbands = (H + 7) / 8;
+    const uint32_t my_bands = rank < nbands ? (nbands - rank + nranks - 1) / nranks : 0;
+    uint32_t nsplit = trace_split(c, (size_t)W * 8 * my_bands);
+    if (sort || my_bands < nsplit) nsplit = 1;   // the coherence sort has one set of buffers
+    const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
+    st = ensure_split_capacity(c, nsplit, Pg);
+    if (st) return st;
+    HIPC(c, hipMemsetAsync(c->d_qcount, 0, 32 * nsplit * sizeof(uint32_t), s));
+    if (timing) HIPC(c, hipEventRecord(ev[0], s));
+    if (nsplit > 1) HIPC(c, hipEventRecord(c->ev_fork, s));
+    for (uint32_t g = 0; g < nsplit; g++) {
+        hipStream_t sg = g ? c->sub[g] : s;
+        if (g) HIPC(c, hipStreamWaitEvent(sg, c->ev_fork, 0));
+        TraceArgs ag = a;
+        ag.band0 = g;
+        ag.bstep = nsplit;
+        RayQ* q[2] = {g ? c->d_qs[g][0] : c->d_q[0], g ? c->d_qs[g][1] : c->d_q[1]};
+        float2* hit = g ? c->d_hits[g] : c->d_hit;
+        uint32_t* qc = c->d_qcount + 32 * g;
+        const bool tg = timing && g == 0;   // stage events: chain 0's kernels
+        launch_primary(ag, q[0], &qc[0], count, bounces > 0, pvariant, sg);
+        if (tg) HIPC(c, hipEventRecord(ev[1], sg));
+        for (uint32_t b = 0; b < bounces; b++) {
+            const uint32_t* perm = nullptr;
+            if (sort) {
+                launch_bounce_keys(q[b & 1], &qc[b], c->d_rootbox, P, c->d_bkin, c->d_bvin, sg);
+                perm = radix_sort_pairs(c->d_bkin, c->d_bvin, c->d_bka, c->d_bva, c->d_bkb, c->d_bvb, P, 30,
+                                        c->d_bscratch, sg).vals;
+            }
+            if (refill) {
+                if (tg && b == 0) HIPC(c, hipEventRecord(ev[3], sg));
+                launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, bmode, hit, &qc[16 + b], lds_stack,
+                                       refill_min, chunk, leaf_batch, sg);
+                if (tg && b == 0) HIPC(c, hipEventRecord(ev[4], sg));
+                launch_bounce_shade(ag, q[b & 1], &qc[b], hit, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
+                                    Pg, sg);
+            } else
+                launch_bounce(ag, q[b & 1], &qc[b], perm, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
+                              variant, sg);
         }
-        if (refill) {
-            if (timing && b == 0) HIPC(c, hipEventRecord(ev[3], s));
-            launch_bounce_traverse(a, c->d_q[b & 1], &c->d_qcount[b], perm, count, bmode, c->d_hit,
-                                   &c->d_qcount[16 + b], lds_stack, refill_min, chunk, leaf_batch, s);
-            if (timing && b == 0) HIPC(c, hipEventRecord(ev[4], s));
-            launch_bounce_shade(a, c->d_q[b & 1], &c->d_qcount[b], c->d_hit, c->d_q[(b + 1) & 1],
-                                &c->d_qcount[b + 1], count, b + 1 < bounces, P, s);
-        } else
-            launch_bounce(a, c->d_q[b & 1], &c->d_qcount[b], perm, c->d_q[(b + 1) & 1], &c->d_qcount[b + 1], count,
-                          b + 1 < bounces, variant, s);
+        if (g) {
+            HIPC(c, hipEventRecord(c->ev_join[g], sg));
+            HIPC(c, hipStreamWaitEvent(s, c->ev_join[g], 0));
+        }
     }
+    c->nsplit = nsplit;
     if (timing) {
         HIPC(c, hipEventRecord(ev[2], s));
         c->evt_trav[c->n_traces % rtbvh_ctx::RING] = refill && bounces > 0;
@@ -413,6 +482,15 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (uint32_t g = 1; g < rtbvh_ctx::MAXSPLIT; g++) {
+        if (c->sub[g]) {
+            (void)hipStreamSynchronize(c->sub[g]);
+            (void)hipStreamDestroy(c->sub[g]);
+        }
+        if (c->ev_join[g]) (void)hipEventDestroy(c->ev_join[g]);
+        dfree(c->d_qs[g][0]); dfree(c->d_qs[g][1]); dfree(c->d_hits[g]);
+    }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec);
@@ -833,13 +911,14 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
     }
     out->timed_traces = nt;
     if (c->traced && c->d_counters) {
-        unsigned long long cnt[16];
-        uint32_t q[16];
+        unsigned long long cnt[64];
+        uint32_t q[32 * rtbvh_ctx::MAXSPLIT];
         HIPC(c, hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
-        HIPC(c, hipMemcpy(q, c->d_qcount, sizeof(q), hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(q, c->d_qcount, sizeof(uint32_t) * 32 * c->nsplit, hipMemcpyDeviceToHost));
         out->primary_rays = (uint64_t)c->W * rtbvh_band_rows(c->H, c->rank, c->nranks);
         uint64_t b = 0;
-        for (uint32_t k = 0; k < c->bounces; k++) b += q[k];
+        for (uint32_t g = 0; g < c->nsplit; g++)
+            for (uint32_t k = 0; k < c->bounces; k++) b += q[32 * g + k];
         out->bounce_rays = b;
         for (int p = 0; p < 2; p++) {
             out->internal_visits[p] = cnt[2 + 3 * p];
@@ -849,6 +928,8 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         out->stack_overflows = cnt[8];
         out->textured_hits = cnt[9];
         out->trav_wave_steps = cnt[10];
+        out->trav_max_steps = cnt[13];
+        for (int k = 0; k < 32; k++) out->trav_steps_log2[k] = cnt[32 + k];
         out->trav_mixed_steps = cnt[11];
         out->trav_active_lanes = cnt[12];
     }

@@ -81,6 +81,7 @@ struct TraceArgs {
     const float* srgb;        // [256] sRGB -> linear (rtbvh_srgb_table)
     uint32_t ntex;
     uint32_t T, W, H, rank, nranks;
+    uint32_t band0, bstep;    // this launch traces the rank's bands band0, band0 + bstep, ... (trace chains)
     Mat4 wv;
     float4* color;            // output pixels (compacted band rows when nranks > 1)
     float* intensity;         // optional, same indexing as color

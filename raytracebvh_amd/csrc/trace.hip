@@ -638,10 +638,11 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
     __shared__ uint32_t s_pst[TV<V>::PACKET ? 4 * PST : 1];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
-    const uint32_t band = blockIdx.y * a.nranks + a.rank;
+    const uint32_t k = a.band0 + blockIdx.y * a.bstep;   // the rank's k-th band
+    const uint32_t band = k * a.nranks + a.rank;
     const uint32_t y = band * 8 + (lane >> 3);
     const bool valid = x < a.W && y < a.H;
-    const size_t out = ((size_t)blockIdx.y * 8 + (lane >> 3)) * a.W + x;
+    const size_t out = ((size_t)k * 8 + (lane >> 3)) * a.W + x;
     Counts c = {0, 0, 0};
     uint32_t hits = 0, tex = 0;
     bool live = false;
@@ -835,10 +836,6 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     // of the last claimed chunks outweighs the saved atomics)
     uint32_t cnext = 0, cend = 0;
     unsigned long long wsteps = 0, mixed = 0, active_lanes = 0;
-    // second half of a 4-wide record pair, loop-carried: a leaf lane skips its load and
-    // keeps the previous values (a per-iteration zero would cost 16 v_mov every iteration;
-    // loading the other half of the leaf's line on leaf lanes cost +2% in TA work)
-    v4f q4 = {0.f, 0.f, 0.f, 0.f}, q5 = q4, q6 = q4, q7 = q4;
     while (true) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -915,7 +912,12 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(lid & ~LEAF_BIT))
                                : reinterpret_cast<const v4f*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
         v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
-        if (WIDE && !isleaf) {   // the right child's record (leaf lanes keep stale q4..q7)
+        // second half of a 4-wide record pair: leaf lanes neither load nor use it, and it
+        // is not carried across iterations (a per-iteration zero would cost 16 v_mov; a
+        // loop-carried copy holds 16 VGPRs through the donation step; loading the other
+        // half of the leaf's line on leaf lanes cost +2% in TA work)
+        v4f q4, q5, q6, q7;
+        if (WIDE && !isleaf) {   // the right child's record
             q4 = rr[4]; q5 = rr[5]; q6 = rr[6]; q7 = rr[7];
         }
         pin(q0); pin(q1); pin(q2); pin(q3);
@@ -1027,6 +1029,11 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         if (done) {
             hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
             has = false;
+            if (COUNT) {   // walk length census (stats trav_max_steps / trav_steps_log2)
+                const uint32_t steps = 2 * T + 2 - guard;
+                atomicAdd(&counters[32 + (31 - __clz(steps | 1u))], 1ull);
+                atomicMax(&counters[13], (unsigned long long)steps);
+            }
         }
     }
     if (COUNT || c.overflow) {
@@ -1209,8 +1216,9 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
 void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, int variant, hipStream_t s) {
     const uint32_t nbands = (a.H + 7) / 8;
     const uint32_t my_bands = a.rank < nbands ? (nbands - a.rank + a.nranks - 1) / a.nranks : 0;
-    if (my_bands == 0 || a.W == 0) return;
-    dim3 grid((a.W + 31) / 32, my_bands);
+    const uint32_t launch_bands = my_bands > a.band0 ? (my_bands - a.band0 + a.bstep - 1) / a.bstep : 0;
+    if (launch_bands == 0 || a.W == 0) return;
+    dim3 grid((a.W + 31) / 32, launch_bands);
 #define RTBVH_PRIM(C, V) launch_primary_t<C, V>(a, q, qcount, emit, grid, s)
     if (variant == 6) count ? RTBVH_PRIM(true, 6) : RTBVH_PRIM(false, 6);
     else if (variant == 7) count ? RTBVH_PRIM(true, 7) : RTBVH_PRIM(false, 7);

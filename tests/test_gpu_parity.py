@@ -495,6 +495,43 @@ def test_primary_general_boxes(mode):
     assert np.count_nonzero(w4[:, 15]) > 100   # the general path is taken
 
 
+@pytest.mark.parametrize("mode", ["nearest+packet+wide", "reference", "nearest+packet+refill"])
+@pytest.mark.parametrize("nsplit", [2, 3, 4])
+def test_trace_chains_match_one_chain(mode, nsplit):
+    """A trace dealt over nsplit primary -> bounce chains on their own streams renders the
+    same frame, intensities, ray records and ray counts as one chain: whole frames, and
+    band shards of N = 3 and 8 ranks (ragged frame, ranks with fewer bands than chains)."""
+    import torch
+    s = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    W, H = 1000, 357
+    base = TRACE_MODES[mode] | rt.FLAG_REFRACT_RECORDS
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(W, H))
+        c.build()
+        out = {}
+        for k in (1, nsplit):
+            c.set_flags(base | k << rt.FLAG_SPLIT_SHIFT)
+            c.trace(W, H, 2)
+            st = c.stats()
+            out[k] = (c.read_framebuffer(), c.read_intensity(), c.read_rays(), st["bounce_rays"])
+            for nranks in (3, 8):
+                for r in range(nranks):
+                    rows = rt.lib().rtbvh_band_rows(H, r, nranks)
+                    buf = torch.full((rows, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
+                    c.trace_band_async(W, H, 2, r, nranks, buf.data_ptr())
+                    c.synchronize()
+                    out[(k, nranks, r)] = (buf.cpu().numpy(), c.stats()["bounce_rays"])
+    fb1, in1, (rf1, rr1), nb1 = out[1]
+    fbk, ink, (rfk, rrk), nbk = out[nsplit]
+    assert np.array_equal(fbk, fb1) and np.array_equal(ink, in1) and nb1 == nbk and nb1 > 0
+    assert np.array_equal(rfk.view(np.uint8), rf1.view(np.uint8)) and np.array_equal(rrk.view(np.uint8), rr1.view(np.uint8))
+    for key in [k for k in out if isinstance(k, tuple) and k[0] == 1]:
+        band, nb = out[key]
+        band_k, nb_k = out[(nsplit,) + key[1:]]
+        assert np.array_equal(band_k, band) and nb_k == nb, key
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_band_split_reassembles_full_frame(nranks):
     import torch
