@@ -256,6 +256,13 @@ rtbvh_status rtbvh_read_bvh(rtbvh_ctx* ctx, rtbvh_node* out, uint32_t capacity);
  * or 0x80000000|j for sorted leaf j.  A leaf child c holds {its box as L and as R,
  * 0x80000000|c, ~0u, 0x80000000|c, 0}.  (The root's record follows at slot 2(n-1).) */
 rtbvh_status rtbvh_read_wide(rtbvh_ctx* ctx, uint32_t* records, uint64_t capacity);
+/* Quantized 4-wide nodes of the bounce walk, one 64-B record (16 words) per slot (2n-1):
+ * internal node k's at the slot of its record (2 * parent + side; the root's at 2n-2;
+ * slots of leaves unused): words 0-2 grid origin xyz, 3-5 grid step xyz (f32; step x ==
+ * 0: not quantized), 6-8 lo bytes x/y/z, 9-11 hi bytes x/y/z (byte c = grandchild c),
+ * 12-15 grandchildren (slot, 0x80000000 | leaf, or 0xFFFFFFFF); decoded corner = origin +
+ * q * step.  capacity in records (>= 2n-1). */
+rtbvh_status rtbvh_read_qnodes(rtbvh_ctx* ctx, uint32_t* nodes, uint64_t capacity);
 /* Per-triangle Morton codes in triangle order (MortonCodes.hlsl:104-112). */
 rtbvh_status rtbvh_read_morton(rtbvh_ctx* ctx, uint32_t* codes);
 /* Stable radix order: sorted codes and the triangle id of each sorted position. */

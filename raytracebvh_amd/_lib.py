@@ -31,7 +31,7 @@ EXPORTS = [
     "rtbvh_set_scene", "rtbvh_set_camera", "rtbvh_build", "rtbvh_build_async", "rtbvh_trace",
     "rtbvh_trace_async", "rtbvh_compute_bvh", "rtbvh_trace_band_async", "rtbvh_band_rows",
     "rtbvh_synchronize", "rtbvh_read_framebuffer", "rtbvh_read_intensity", "rtbvh_framebuffer_device",
-    "rtbvh_read_bvh", "rtbvh_read_wide", "rtbvh_read_morton", "rtbvh_read_sorted", "rtbvh_read_rays", "rtbvh_get_stats",
+    "rtbvh_read_bvh", "rtbvh_read_wide", "rtbvh_read_qnodes", "rtbvh_read_morton", "rtbvh_read_sorted", "rtbvh_read_rays", "rtbvh_get_stats",
     "rtbvh_reset_stats", "rtbvh_set_flags",
     "rtbvh_sort_pairs_async", "rtbvh_sort_pairs_host", "rtbvh_build_from_codes", "rtbvh_scene_load_obj",
     "rtbvh_scene_synthetic", "rtbvh_scene_free", "rtbvh_scene_num_vertices", "rtbvh_scene_num_indices",
@@ -134,6 +134,7 @@ def lib() -> ctypes.CDLL:
         "rtbvh_read_bvh": (i32, [vp, vp, u32]),
         "rtbvh_read_morton": (i32, [vp, vp]),
         "rtbvh_read_wide": (i32, [vp, vp, ctypes.c_uint64]),
+        "rtbvh_read_qnodes": (i32, [vp, vp, ctypes.c_uint64]),
         "rtbvh_read_sorted": (i32, [vp, vp, vp]),
         "rtbvh_read_rays": (i32, [vp, vp, vp]),
         "rtbvh_get_stats": (i32, [vp, ctypes.POINTER(Stats)]),

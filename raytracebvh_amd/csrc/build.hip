@@ -400,6 +400,82 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
     refit_climb(lo, hi, a.pleaf[i], a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
 }
 
+// ---- quantized 4-wide nodes (rtbvh_device.h QNode) ---------------------------------
+// One axis of a QNode: the grid origin o = the min of the four boxes, the step s = the
+// smallest power of two with o + 255 s >= their max in fp32, and for each box the largest
+// lo and smallest hi byte whose decoded corners (qdecode, the traversal's own arithmetic)
+// still contain it.  false: no finite frame (the node keeps the exact record pair).
+__device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float (&hi)[4], float& org, float& scl,
+                                              uint32_t& wlo, uint32_t& whi) {
+    float o = lo[0], m = hi[0];
+    for (int c = 1; c < 4; c++) {
+        o = fminf(o, lo[c]);
+        m = fmaxf(m, hi[c]);
+    }
+    const float ext = m - o;
+    if (!(fabsf(o) <= 1e37f && fabsf(m) <= 1e37f && ext <= 1e37f)) return false;   // also NaN
+    float s = 1.f;
+    if (ext > 0.f) {
+        int e;
+        (void)frexpf(ext / 255.f, &e);   // ext/255 = f 2^e, f in [0.5, 1): 2^e > ext/255
+        s = ldexpf(1.f, e < -120 ? -120 : e);
+    }
+    while (fmaf(255.f, s, o) < m) s *= 2.f;   // the rounding of the add
+    wlo = whi = 0;
+    for (int c = 0; c < 4; c++) {
+        uint32_t l = (uint32_t)fminf(fmaxf(floorf((lo[c] - o) / s), 0.f), 255.f);
+        uint32_t h = (uint32_t)fminf(fmaxf(ceilf((hi[c] - o) / s), 0.f), 255.f);
+        while (l > 0 && fmaf((float)l, s, o) > lo[c]) --l;     // q = 0 decodes to o <= lo[c]
+        while (h < 255 && fmaf((float)h, s, o) < hi[c]) ++h;   // q = 255 decodes to >= m >= hi[c]
+        wlo |= l << (8 * c);
+        whi |= h << (8 * c);
+    }
+    org = o;
+    scl = s;
+    return true;
+}
+
+// The QNode of internal node k from its record pair (slots 2k, 2k+1: the four grandchild
+// boxes and ids), written at k's own slot pint[k] (the root's: 2T-2), so that siblings'
+// nodes share a 128-B line as the records do.  Internal grandchild ids become their
+// slots (2 * their parent + side; the parent's index is word 14 of its record).  One
+// workgroup takes 256 consecutive pairs: coalesced loads into LDS (one float4 of padding
+// per pair: the per-node ds_read_b128 at a 144-B stride is bank-conflict free), then
+// one node per thread.
+__global__ __launch_bounds__(BLOCK) void k_qnodes(const Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
+                                                  QNode* __restrict__ qn, uint32_t T) {
+    __shared__ float4 s_pair[BLOCK * 9];
+    const uint32_t k0 = blockIdx.x * BLOCK, tid = threadIdx.x;
+    const uint32_t nn = min(BLOCK, T - 1 - k0);   // nodes of this workgroup
+    const float4* src = reinterpret_cast<const float4*>(rec + 2 * (size_t)k0);
+    for (uint32_t j = tid; j < 8 * nn; j += BLOCK) s_pair[j + j / 8] = src[j];
+    __syncthreads();
+    if (tid >= nn) return;
+    const uint32_t k = k0 + tid;
+    const float4* r = s_pair + 9 * tid;
+    const float4 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], b0 = r[4], b1 = r[5], b2 = r[6], b3 = r[7];
+    // record words (rtbvh_device.h): 0-1 l.min.xy 2-3 l.max.xy 4-5 r.min.xy 6-7 r.max.xy
+    // 8 l.min.z 9 l.max.z 10 r.min.z 11 r.max.z 12 id_l 13 id_r 14 own
+    const float lx[4] = {a0.x, a1.x, b0.x, b1.x}, ly[4] = {a0.y, a1.y, b0.y, b1.y}, lz[4] = {a2.x, a2.z, b2.x, b2.z};
+    const float hx[4] = {a0.z, a1.z, b0.z, b1.z}, hy[4] = {a0.w, a1.w, b0.w, b1.w}, hz[4] = {a2.y, a2.w, b2.y, b2.w};
+    QNode q;
+    bool ok = quantize_axis(lx, hx, q.org[0], q.scl[0], q.lo[0], q.hi[0]);
+    ok = quantize_axis(ly, hy, q.org[1], q.scl[1], q.lo[1], q.hi[1]) && ok;
+    ok = quantize_axis(lz, hz, q.org[2], q.scl[2], q.lo[2], q.hi[2]) && ok;
+    if (!ok) q.scl[0] = 0.f;   // the traversal reads the exact pair for this node
+    const uint32_t ownl = __float_as_uint(a3.z), ownr = __float_as_uint(b3.z);
+    auto gslot = [](uint32_t id, uint32_t own, uint32_t side) {
+        return (id == INVALID || (id & LEAF_BIT)) ? id : 2 * own + side;
+    };
+    q.id[0] = gslot(__float_as_uint(a3.x), ownl, 0);
+    q.id[1] = gslot(__float_as_uint(a3.y), ownl, 1);
+    q.id[2] = gslot(__float_as_uint(b3.x), ownr, 0);
+    q.id[3] = gslot(__float_as_uint(b3.y), ownr, 1);
+    const float4* qs = reinterpret_cast<const float4*>(&q);
+    float4* dst = reinterpret_cast<float4*>(qn + slot_of(pint[k], T));   // pint[0] = INVALID: the root
+    dst[0] = qs[0]; dst[1] = qs[1]; dst[2] = qs[2]; dst[3] = qs[3];
+}
+
 // ---- small scenes: the whole build in one workgroup ------------------------------
 // The reference's own meshes (Test.obj: 1,952 triangles) rebuild every frame
 // (Graphics.cpp:56), and at that size the multi-kernel build is ~18 dependent launches of
@@ -599,6 +675,10 @@ void launch_build_small(const BuildArgs& a, hipStream_t s) {
     if (a.delta_mode == 0) hipLaunchKernelGGL(k_build_small<0>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
     else hipLaunchKernelGGL(k_build_small<1>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
 }
+void launch_qnodes(const BuildArgs& a, hipStream_t s) {
+    if (a.T > 1)
+        hipLaunchKernelGGL(k_qnodes, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.rec, a.pint, a.qnode, a.T);
+}
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
 }
@@ -610,6 +690,7 @@ void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t 
     else hipLaunchKernelGGL(k_karras_only<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
     if (a.T > 1) (void)hipMemsetAsync(a.refit_cnt, 0, sizeof(uint32_t) * (a.T - 1), s);
     hipLaunchKernelGGL(k_refit_boxes, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a, leaf_boxes);
+    launch_qnodes(a, s);
 }
 
 }  // namespace rtbvh

@@ -44,6 +44,31 @@ struct alignas(64) Inner {
 };
 static_assert(sizeof(Inner) == 64, "Inner must be one 64-B record");
 
+// 64-byte quantized 4-wide node of internal node k, stored at k's slot (qnode[pint[k]], the
+// root's at 2T-2, as the records: siblings share a 128-B line): the boxes of
+// k's four grandchildren -- the children of k's two children, in the order of the record
+// pair at slots 2k, 2k+1 (a leaf child counts once, its second entry has id INVALID) --
+// with every corner on an 8-bit per-axis grid whose origin is the min corner of k's box
+// and whose step is a power of two:
+//   org[3], scl[3]   grid origin and step (scl[0] == 0: not quantized, use the exact pair)
+//   lo[a], hi[a]     byte c = grandchild c's min / max on axis a in grid steps
+//   id[4]            grandchildren: the slot of an internal one, LEAF_BIT | j, or INVALID
+// qdecode() is exact in the product (8-bit q times a power of two) and rounds once in
+// the add; the build picks q so that the decoded box contains the exact box.  The slab
+// test is monotone in the box corners (every operation in it rounds monotonically), so
+// a box the exact test hits is hit here too: a walk on these nodes reaches every leaf
+// the record-pair walk reaches, pruning only on entry distances that are <= the exact
+// ones.  Half the bytes per 4-wide step (64 vs 128).
+struct alignas(64) QNode {
+    float org[3], scl[3];
+    uint32_t lo[3], hi[3];
+    uint32_t id[4];
+};
+static_assert(sizeof(QNode) == 64, "QNode must be one 64-B record");
+__device__ __forceinline__ float qdecode(float org, float scl, uint32_t w, int c) {
+    return fmaf((float)((w >> (8 * c)) & 255u), scl, org);   // == org + q*scl: the product is exact
+}
+
 struct alignas(16) RayQ {   // bounce queue entry (32 B)
     uint32_t idx;           // output pixel index
     float intensity;

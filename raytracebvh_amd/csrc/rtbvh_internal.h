@@ -52,11 +52,14 @@ struct BuildArgs {
     uint32_t* pint;           // [T-1]
     uint32_t* refit_cnt;      // [T-1]
     float* rootbox;           // [6]
+    QNode* qnode;             // [2T-1] quantized 4-wide nodes in slots (rtbvh_device.h), from rec
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
 void launch_leaf_karras(const BuildArgs& a, hipStream_t s);
 void launch_refit(const BuildArgs& a, hipStream_t s);
+// qnode[k] from the record pairs (after the refit)
+void launch_qnodes(const BuildArgs& a, hipStream_t s);
 // the whole build in one workgroup for T <= small_build_max() (sorted pairs into
 // a.sorted_keys / a.sorted_vals, which must be writable)
 uint32_t small_build_max();
@@ -88,6 +91,7 @@ struct TraceArgs {
     unsigned long long* counters;   // 8 x u64: primary, bounce, int visits, leaf visits, hits, tex hits, overflow, -
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
+    const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)
 };
 // traversal kernel variants (A/B switch; DESIGN.md "Traversal")
 // variant: see RTBVH_FLAG_VARIANT_SHIFT in include/rtbvh.h (0 = default)

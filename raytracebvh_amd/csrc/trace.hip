@@ -787,6 +787,7 @@ __device__ __forceinline__ void sort2(float& ta, uint32_t& ia, float& tb, uint32
 // showed ~3.6 GB of stack write-back per C5 bounce pass.
 template <bool COUNT, int MODE, int S>
 __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restrict__ inner,
+                                                          const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
                                                           const RayQ* __restrict__ qin,
                                                           const uint32_t* __restrict__ qin_count,
@@ -800,7 +801,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     // (C5): 90% of wave iterations held both leaf and internal lanes, so the triangle
     // test's VALU ran in nearly every iteration for ~6 of 44 lanes.  The kept answer is
     // the (t, leaf) minimum over every leaf whose box was hit, as in MODE 2.
-    constexpr bool NEAREST = MODE >= 1, WIDE = MODE >= 2, POSTPONE = MODE == 3;
+    // MODE 4 = MODE 2 on the quantized nodes (qn, rtbvh_device.h QNode): a 4-wide step
+    // reads one 64-B node instead of the 128-B record pair.
+    constexpr bool NEAREST = MODE >= 1, WIDE = MODE >= 2, POSTPONE = MODE == 3, QUANT = MODE == 4;
     const uint32_t n = *qin_count;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0};
@@ -865,7 +868,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                     bl = 0;
                     sp = 0;
                     top = INVALID;
-                    node = WIDE ? ((T == 1) ? LEAF_BIT : 0u) : root_slot(T);
+                    node = QUANT ? root_slot(T) : WIDE ? ((T == 1) ? LEAF_BIT : 0u) : root_slot(T);
                     pend = INVALID;
                     if (POSTPONE && T == 1) {   // a one-leaf tree: the leaf is parked, no node
                         pend = LEAF_BIT;
@@ -910,18 +913,19 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         const bool isleaf = POSTPONE ? do_leaf : (node & LEAF_BIT) != 0;
         const uint32_t lid = POSTPONE ? pend : node;
         const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(lid & ~LEAF_BIT))
-                               : reinterpret_cast<const v4f*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
+                        : QUANT ? reinterpret_cast<const v4f*>(qn + node)
+                                : reinterpret_cast<const v4f*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
         v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
         // second half of a 4-wide record pair: leaf lanes neither load nor use it, and it
-        // is not carried across iterations (a per-iteration zero would cost 16 v_mov; a
-        // loop-carried copy holds 16 VGPRs through the donation step; loading the other
-        // half of the leaf's line on leaf lanes cost +2% in TA work)
+        // is not carried across iterations (a per-iteration zero costs 16 v_mov; a
+        // loop-carried copy holds 16 VGPRs; loading the other half of the leaf's line on
+        // leaf lanes cost +2% in TA work)
         v4f q4, q5, q6, q7;
-        if (WIDE && !isleaf) {   // the right child's record
+        if (WIDE && !QUANT && !isleaf) {   // the right child's record
             q4 = rr[4]; q5 = rr[5]; q6 = rr[6]; q7 = rr[7];
         }
         pin(q0); pin(q1); pin(q2); pin(q3);
-        if (WIDE) { pin(q4); pin(q5); pin(q6); pin(q7); }
+        if (WIDE && !QUANT) { pin(q4); pin(q5); pin(q6); pin(q7); }
         if (--guard == 0) {
             c.overflow++;
             done = true;
@@ -951,14 +955,47 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             }
         } else if (WIDE) {
             if (COUNT) c.internal++;
-            // record pair: q0..q3 = the record of the left child, q4..q7 of the right one
-            const uint4 a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
-            const uint4 b3 = make_uint4(__float_as_uint(q7.x), __float_as_uint(q7.y), 0u, 0u);
+            // the four grandchildren: ids (a3.x, a3.y, b3.x, b3.y), entry distances t0..t3
+            uint4 a3, b3;
             float t0, t1, t2, t3;
-            const bool h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, t0);
-            const bool h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, t1) & (a3.y != INVALID);
-            const bool h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, hit, best, t2);
-            const bool h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, hit, best, t3) & (b3.y != INVALID);
+            bool h0, h1, h2, h3;
+            if (QUANT && q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
+                const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w, sy = q1.x, sz = q1.y;
+                const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
+                const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
+                a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
+                b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
+#define RTBVH_QBOX(c, t)                                                                                      \
+    ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
+            qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), hit, best, t)
+                h0 = RTBVH_QBOX(0, t0);
+                h1 = RTBVH_QBOX(1, t1) & (a3.y != INVALID);
+                h2 = RTBVH_QBOX(2, t2);
+                h3 = RTBVH_QBOX(3, t3) & (b3.y != INVALID);
+#undef RTBVH_QBOX
+            } else {
+                uint32_t own = 0;
+                if (QUANT) {   // a node without a finite grid: its exact record pair (node = its slot)
+                    own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
+                    const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
+                    q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
+                    q4 = pr[4]; q5 = pr[5]; q6 = pr[6]; q7 = pr[7];
+                }
+                // record pair: q0..q3 = the record of the left child, q4..q7 of the right one
+                a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
+                b3 = make_uint4(__float_as_uint(q7.x), __float_as_uint(q7.y), 0u, 0u);
+                if (QUANT) {   // grandchild ids -> slots (2 * parent + side; parent = word 14)
+                    const uint32_t ol = __float_as_uint(q3.z), orr = __float_as_uint(q7.z);
+                    if (!(a3.x & LEAF_BIT)) a3.x = 2 * ol;
+                    if (a3.y != INVALID && !(a3.y & LEAF_BIT)) a3.y = 2 * ol + 1;
+                    if (!(b3.x & LEAF_BIT)) b3.x = 2 * orr;
+                    if (b3.y != INVALID && !(b3.y & LEAF_BIT)) b3.y = 2 * orr + 1;
+                }
+                h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, t0);
+                h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, t1) & (a3.y != INVALID);
+                h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, hit, best, t2);
+                h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, hit, best, t3) & (b3.y != INVALID);
+            }
             const float INF = __builtin_inff();
             float k0 = h0 ? t0 : INF, k1 = h1 ? t1 : INF, k2 = h2 ? t2 : INF, k3 = h3 ? t3 : INF;
             uint32_t i0 = h0 ? a3.x : INVALID, i1 = h1 ? a3.y : INVALID, i2 = h2 ? b3.x : INVALID,
@@ -1186,18 +1223,22 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
     const uint32_t blocks = 2048;   // persistent: 8 waves/SIMD x 1024 SIMDs / 4 waves per block
     const uint32_t extra_lds = (chunk >> 24) * 1024u;   // A/B only: dynamic LDS (KB in the top byte)
     chunk &= (1u << 24) - 1;                            // that caps the resident blocks per CU
-    if (mode == 3)
+    if (mode == 4)
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 4, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s,
+                           a.inner4, a.qnode, a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, refill_min,
+                           chunk, leaf_batch);
+    else if (mode == 3)
         hipLaunchKernelGGL((k_bounce_trav<COUNT, 3, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s,
-                           a.inner4, a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk,
+                           a.inner4, a.qnode, a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk,
                            leaf_batch);
     else if (mode == 2)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s, a.inner4, a.leaf, a.T, qin,
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s, a.inner4, a.qnode, a.leaf, a.T, qin,
                            qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
     else if (mode == 1)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 1, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T, qin,
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 1, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, a.T, qin,
                            qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
     else
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 0, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.leaf, a.T,
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 0, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, a.T,
                            qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
 }
 

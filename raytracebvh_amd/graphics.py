@@ -160,6 +160,12 @@ class Context:
         self._check(_L.lib().rtbvh_read_wide(self._h, _L.ptr(out), len(out)))
         return out
 
+    def read_qnodes(self) -> np.ndarray:
+        """Quantized 4-wide nodes of the bounce walk in slots: (2n-1, 16) uint32, see rtbvh_read_qnodes."""
+        out = np.zeros((max(2 * self.num_tris - 1, 0) if self.num_tris > 1 else 0, 16), np.uint32)
+        self._check(_L.lib().rtbvh_read_qnodes(self._h, _L.ptr(out), len(out)))
+        return out
+
     def read_morton(self) -> np.ndarray:
         out = np.zeros(self.num_tris, np.uint32)
         self._check(_L.lib().rtbvh_read_morton(self._h, _L.ptr(out)))

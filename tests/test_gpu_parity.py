@@ -209,7 +209,11 @@ TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest":
                "packet+wide, compare-form primary box test (A/B variant 12)":
                    rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 12 << rt.FLAG_VARIANT_SHIFT,
                "wide+postponed-leaves (A/B variant 15)": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
-               | 15 << rt.FLAG_VARIANT_SHIFT}
+               | 15 << rt.FLAG_VARIANT_SHIFT,
+               "nearest+packet+wide, exact record pairs (variant 17)": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY
+               | rt.FLAG_WIDE_BVH | 17 << rt.FLAG_VARIANT_SHIFT,
+               "packet+wide, exact record pairs (variant 17)": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
+               | 17 << rt.FLAG_VARIANT_SHIFT}
 
 
 def _trace_both(s, W, H, bounces, rows=None, flags=0):
@@ -444,6 +448,58 @@ def test_wide_view_records_match_binary_tree():
             assert rec[15] == gen
 
 
+@pytest.mark.parametrize("scene", ["synthetic", "general boxes", "Test"])
+def test_qnodes_contain_the_exact_boxes(scene):
+    """Quantized node of internal node k (rtbvh_device.h QNode) at k's slot: power-of-two grid
+    steps, the grandchildren of the record pair at slots 2k, 2k+1 (internal ones by their
+    slots), and decoded corners (origin + q * step in fp32, the traversal's arithmetic)
+    that contain every grandchild's exact box."""
+    if scene == "synthetic":
+        s = rt.synthetic(20_000, seed=7, half_extent=(30, 30, 20))
+    elif scene == "general boxes":
+        s = _general_box_scene()
+    else:
+        d = load_scene_fixture("Test")
+        s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(320, 240))
+        c.build()
+        nodes = c.read_bvh()
+        q = c.read_qnodes()
+    T = s.num_tris
+    assert q.shape == (2 * T - 1, 16)
+    cl, cr, par = nodes["child_l"], nodes["child_r"], nodes["parent"]
+
+    def slot(x):   # reference-layout internal node x (>= T): its record's slot
+        if x == T:
+            return 2 * T - 2
+        return 2 * (par[x] - T) + (0 if cl[par[x]] == x else 1)
+
+    q = q[[slot(T + k) for k in range(T - 1)]]   # node-indexed from here on
+    f = q.view(np.float32)
+    org, scl = f[:, 0:3], f[:, 3:6]
+    assert (scl[:, 0] != 0).all()   # every node of these scenes has a finite grid
+    m, e = np.frexp(scl)
+    assert (m == 0.5).all(), "grid steps are powers of two"
+    shifts = np.arange(4, dtype=np.uint32) * 8
+    lo = ((q[:, 6:9, None] >> shifts) & 255).astype(np.float32)   # [k, axis, c]
+    hi = ((q[:, 9:12, None] >> shifts) & 255).astype(np.float32)
+    dlo = org[:, :, None] + lo * scl[:, :, None]   # q * step exact; one rounding in the add
+    dhi = org[:, :, None] + hi * scl[:, :, None]
+    for k in range(T - 1):
+        gc = []
+        for ch in (cl[T + k], cr[T + k]):
+            gc += [ch, None] if ch < T else [cl[ch], cr[ch]]
+        ids = [0xFFFFFFFF if g is None else ((0x80000000 | g) if g < T else slot(g)) for g in gc]
+        assert list(q[k, 12:16]) == ids, k
+        for cidx, g in enumerate(gc):
+            if g is None:
+                continue
+            assert (dlo[k, :, cidx] <= nodes["bb_min"][g]).all(), (k, cidx)
+            assert (dhi[k, :, cidx] >= nodes["bb_max"][g]).all(), (k, cidx)
+
+
 def _general_box(lo, hi):
     """Record word 15's bit (rtbvh_device.h): the box needs the general primary slab test."""
     ok = lo[0] < hi[0] and lo[1] < hi[1] and lo[2] <= hi[2] and 0 <= hi[2] < np.inf
@@ -478,7 +534,8 @@ def _general_box_scene(seed=11):
 
 
 @pytest.mark.parametrize("mode", ["packet+wide", "nearest+packet+wide",
-                                  "packet+wide, compare-form primary box test (A/B variant 12)"])
+                                  "packet+wide, compare-form primary box test (A/B variant 12)",
+                                  "nearest+packet+wide, exact record pairs (variant 17)"])
 def test_primary_general_boxes(mode):
     """Flat and behind-the-eye boxes (record word 15 set) in the axis-parallel primary walk:
     frames identical to the oracle's, and the record bits as the tree's boxes say."""
