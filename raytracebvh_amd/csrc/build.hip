@@ -402,9 +402,14 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
 
 // ---- quantized 4-wide nodes (rtbvh_device.h QNode) ---------------------------------
 // One axis of a QNode: the grid origin o = the min of the four boxes, the step s = the
-// smallest power of two with o + 255 s >= their max in fp32, and for each box the largest
-// lo and smallest hi byte whose decoded corners (qdecode, the traversal's own arithmetic)
-// still contain it.  false: no finite frame (the node keeps the exact record pair).
+// smallest power of two >= 2^-120 with o + 255 s >= their max in fp32, and for each box
+// the largest lo and smallest hi byte whose decoded corners (qdecode, the traversal's own
+// arithmetic) still contain it.  false: no finite frame (the node keeps the exact record
+// pair).  Division-free: s and 1/s are built from exponent bits (both normal: s is in
+// [2^-120, 2^116] for |corners| <= 1e37), so (x - o) * (1/s) is exactly (x - o) / s.
+// PMC: the first form (correctly rounded divisions, frexpf/ldexpf) ran ~3,500 VALU per
+// node and made k_qnodes VALU-bound (0.90 ms at 10M nodes).
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
 __device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float (&hi)[4], float& org, float& scl,
                                               uint32_t& wlo, uint32_t& whi) {
     float o = lo[0], m = hi[0];
@@ -414,19 +419,21 @@ __device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float 
     }
     const float ext = m - o;
     if (!(fabsf(o) <= 1e37f && fabsf(m) <= 1e37f && ext <= 1e37f)) return false;   // also NaN
-    float s = 1.f;
+    // ext in [2^E, 2^(E+1)): 255 * 2^(E-8) < ext, so the smallest valid step is >= 2^(E-8)
+    int e = -120;
     if (ext > 0.f) {
-        int e;
-        (void)frexpf(ext / 255.f, &e);   // ext/255 = f 2^e, f in [0.5, 1): 2^e > ext/255
-        s = ldexpf(1.f, e < -120 ? -120 : e);
+        const int E = (int)((__float_as_uint(ext) >> 23) & 255u) - 127;   // ext >= 0; denormal: E = -127
+        e = max(E - 8, -120);
     }
-    while (fmaf(255.f, s, o) < m) s *= 2.f;   // the rounding of the add
+    while (fmaf(255.f, pow2f(e), o) < m) ++e;   // the rounding of the add (a few steps at most)
+    const float s = pow2f(e), rs = pow2f(-e);
     wlo = whi = 0;
+#pragma unroll
     for (int c = 0; c < 4; c++) {
-        uint32_t l = (uint32_t)fminf(fmaxf(floorf((lo[c] - o) / s), 0.f), 255.f);
-        uint32_t h = (uint32_t)fminf(fmaxf(ceilf((hi[c] - o) / s), 0.f), 255.f);
-        while (l > 0 && fmaf((float)l, s, o) > lo[c]) --l;     // q = 0 decodes to o <= lo[c]
-        while (h < 255 && fmaf((float)h, s, o) < hi[c]) ++h;   // q = 255 decodes to >= m >= hi[c]
+        uint32_t l = (uint32_t)fminf(fmaxf(floorf((lo[c] - o) * rs), 0.f), 255.f);
+        uint32_t h = (uint32_t)fminf(fmaxf(ceilf((hi[c] - o) * rs), 0.f), 255.f);
+        if (l > 0 && fmaf((float)l, s, o) > lo[c]) --l;     // the rounding of the subtraction: q = 0
+        if (h < 255 && fmaf((float)h, s, o) < hi[c]) ++h;   // decodes to o <= lo[c], 255 to >= m
         wlo |= l << (8 * c);
         whi |= h << (8 * c);
     }

@@ -487,6 +487,7 @@ def test_qnodes_contain_the_exact_boxes(scene):
     hi = ((q[:, 9:12, None] >> shifts) & 255).astype(np.float32)
     dlo = org[:, :, None] + lo * scl[:, :, None]   # q * step exact; one rounding in the add
     dhi = org[:, :, None] + hi * scl[:, :, None]
+    top = np.full((T - 1, 3), -np.inf, dtype=np.float32)   # the exact max corner of the four boxes
     for k in range(T - 1):
         gc = []
         for ch in (cl[T + k], cr[T + k]):
@@ -498,6 +499,11 @@ def test_qnodes_contain_the_exact_boxes(scene):
                 continue
             assert (dlo[k, :, cidx] <= nodes["bb_min"][g]).all(), (k, cidx)
             assert (dhi[k, :, cidx] >= nodes["bb_max"][g]).all(), (k, cidx)
+            top[k] = np.maximum(top[k], nodes["bb_max"][g])
+    # the step is the smallest power of two (>= 2^-120) whose grid reaches the boxes' max
+    half = scl / np.float32(2)
+    reach = org + np.float32(255) * half   # product exact, one rounding in the add
+    assert ((reach < top) | (half < np.float32(2.0 ** -120))).all(), "grid step not minimal"
 
 
 def _general_box(lo, hi):
