@@ -10,9 +10,13 @@ scene and builds the same BVH (replicas, deterministic); the frame is split in
 over RCCL (torch.distributed "nccl") and assembled into the frame.
 
 One step = trace of this rank's bands (primary kernel + bounce kernels) + the
-RCCL gather + assembly on rank 0.  Two band buffers keep one gather in flight:
-step i's gather overlaps step i+1's trace, and every step's frame is gathered and
-assembled before the timed region closes.  The BVH is built once before the timed
+RCCL gather + assembly on rank 0.  Two frames are in flight per rank (--inflight 2):
+frame i runs on context i % 2 (two replicas of the scene + BVH, built from the same
+inputs) on its own HIP stream, so frame i+1's primary pass fills the GPU while frame
+i's bounce walk drains its last long walks; two band buffers keep one gather in flight
+(step i's gather overlaps step i+1's trace), and every step's frame is traced,
+gathered and assembled before the timed region closes.  The one-frame latency (one
+context, frames back to back on one stream) is reported beside it.  The BVH is built once before the timed
 loop (the scene is static; replicated build throughput is measured separately and
 reported under "build").  value = all rays of the frame (W*H primary + every
 live bounce ray, summed over ranks) / max-over-ranks time per step.
@@ -150,6 +154,8 @@ def main():
     ap.add_argument("--build-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C4 build / C3 side measurements")
+    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3],
+                    help="frames in flight per rank (one context + stream each)")
     ap.add_argument("--traversal", default="auto", choices=["auto", "reference"],
                     help="auto: report nearest-first when its frame is identical to the reference order's")
     args = ap.parse_args()
@@ -201,29 +207,51 @@ def main():
              "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
                                    [round(x, 4) for x in bst["ms_stage"][:5]]))}
 
+    # ---- frames in flight: context k (own stream) traces frames i = k mod inflight; the
+    # extra contexts are replicas (same inputs, same deterministic build), built untimed
+    ctxs, streams = [ctx], [stream]
+    for _ in range(args.inflight - 1):
+        sk = torch.cuda.Stream(dev)
+        ck = rt.Context(device=local, flags=rt.FLAG_TIMING, stream=sk.cuda_stream)
+        ck.set_scene(scene)
+        ck.set_camera(wvp, wv)
+        ck.build()
+        ctxs.append(ck)
+        streams.append(sk)
+    torch.cuda.synchronize()
+
     # ---- band buffers + RCCL gather plumbing (raytracebvh_amd/tiles.py)
     from raytracebvh_amd.tiles import BandGather
-    # two band buffers: frame i's RCCL gather overlaps frame i+1's trace (tiles.py)
-    g = BandGather(W, H, rank, world, device=dev, nbuf=2)
+    # one band buffer per frame in flight (>= 2): frame i's RCCL gather overlaps frame i+1's
+    # trace (tiles.py), and frames traced concurrently never share a buffer
+    g = BandGather(W, H, rank, world, device=dev, nbuf=max(2, args.inflight))
     band = g.band
 
-    def run(nsteps):
-        """nsteps frames, one gather in flight; every frame is assembled before return."""
+    def run(nsteps, inflight):
+        """nsteps frames: frame i traced by context i % inflight on its stream into band
+        buffer i % nbuf, then gathered (RCCL, after that stream) and assembled on the same
+        stream, so the buffer's next trace waits for its gather; every frame is assembled
+        before return."""
         pending = None
         for i in range(nsteps):
-            ctx.trace_band_async(W, H, bounces, rank, world, g.band_buffer(i).data_ptr())
-            h = g.gather_async(i)
+            k = i % inflight
+            with torch.cuda.stream(streams[k]):
+                ctxs[k].trace_band_async(W, H, bounces, rank, world, g.band_buffer(i).data_ptr())
+                h = g.gather_async(i)
             if pending is not None:
-                g.assemble(*pending)
+                with torch.cuda.stream(streams[pending[0] % inflight]):
+                    g.assemble(*pending)
             pending = (i, h)
         if pending is not None:
-            g.assemble(*pending)
+            with torch.cuda.stream(streams[pending[0] % inflight]):
+                g.assemble(*pending)
         return g.band_buffer(max(nsteps - 1, 0))
 
-    def timed(flags):
+    def timed(flags, inflight=args.inflight):
         """Warm up, then time exactly args.steps steps between barrier + synchronize."""
-        ctx.set_flags(rt.FLAG_TIMING | flags)
-        run(args.warmup)
+        for c in ctxs:
+            c.set_flags(rt.FLAG_TIMING | flags)
+        run(args.warmup, inflight)
         torch.cuda.synchronize()
         st = ctx.stats()
         tot = torch.tensor([st["primary_rays"] + st["bounce_rays"]], dtype=torch.float64, device=dev)
@@ -233,7 +261,7 @@ def main():
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        last = run(args.steps)
+        last = run(args.steps, inflight)
         torch.cuda.synchronize()
         barrier()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
@@ -270,7 +298,16 @@ def main():
     use = res[use_name]
     traversal["mode"] = use_name
     mode_flags = modes[use_name]
-    rays_per_step, ms_step, value, tst = use["rays"], use["ms_step"], use["value"], use["stats"]
+    rays_per_step, ms_step, value = use["rays"], use["ms_step"], use["value"]
+    # one frame at a time (one context, one stream): the per-frame latency, and the kernels'
+    # own HIP-event durations without a concurrent frame on the GPU (the roofline below)
+    lat = timed(mode_flags, inflight=1)
+    tst = lat["stats"]
+    traversal["inflight"] = args.inflight
+    traversal["one_frame_latency_ms"] = round(lat["ms_step"], 4)
+    traversal["one_frame_mrays_s"] = round(lat["value"], 2)
+    if not torch.equal(lat["band"], use["band"]):
+        raise RuntimeError("frames in flight changed the frame")
 
     # ---- visit counts for the byte model (extra, untimed traces of this rank's bands):
     # the chosen mode's own counts, and the reference-order counts of SURVEY §8(d)
@@ -372,7 +409,8 @@ def main():
             "cpu_baseline": cpu,
         }
         result.update(extras)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:

@@ -31,19 +31,24 @@ class BandGather:
 
         dtype = dtype or torch.float32
         self.W, self.H, self.rank, self.world = W, H, rank, world
-        self.nbuf = nbuf if world > 1 else 1
+        self.nbuf = nbuf
         self.rows = [len(band_row_ids(H, r, world)) for r in range(world)]
         self.max_rows = max(self.rows)
         # every rank sends a buffer of the same (max) size: dist.gather needs equal shapes
         self.bands = [torch.zeros((self.max_rows, W, 4), dtype=dtype, device=device) for _ in range(self.nbuf)]
         self.band = self.bands[0]
         self.frame = None
+        self.frames = None
         self.gather_lists = None
         self.row_idx = None
         if world == 1:
+            self.frames = self.bands   # one rank: the band buffer of a frame is that frame
             self.frame = self.band
         elif rank == 0:
-            self.frame = torch.empty((H, W, 4), dtype=dtype, device=device)
+            # one assembled frame per buffer: frames in flight on different streams never
+            # write the same frame buffer
+            self.frames = [torch.empty((H, W, 4), dtype=dtype, device=device) for _ in range(self.nbuf)]
+            self.frame = self.frames[0]
             self.gather_lists = [[torch.empty_like(self.band) for _ in range(world)] for _ in range(self.nbuf)]
             self.row_idx = [torch.tensor(band_row_ids(H, r, world), dtype=torch.long, device=device)
                             for r in range(world)]
@@ -64,13 +69,15 @@ class BandGather:
     def assemble(self, i: int, handle):
         """Wait (on the stream) for gather i and, on rank 0, scatter its rows into the frame."""
         if self.world == 1:
-            return self.frame
+            return self.frames[i % self.nbuf]
         handle.wait()
         if self.rank == 0:
             gl = self.gather_lists[i % self.nbuf]
+            f = self.frames[i % self.nbuf]
             for r in range(self.world):
-                self.frame.index_copy_(0, self.row_idx[r], gl[r][: self.rows[r]])
-        return self.frame
+                f.index_copy_(0, self.row_idx[r], gl[r][: self.rows[r]])
+            return f
+        return None
 
     def gather(self, i: int = 0):
         """Collect frame i's bands on rank 0 and assemble the frame there (synchronous)."""
