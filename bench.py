@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--build-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C4 build / C3 side measurements")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (the bench); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3],
                     help="frames in flight per rank (one context + stream each)")
     ap.add_argument("--traversal", default="auto", choices=["auto", "reference"],
@@ -170,11 +172,16 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.backend == "gloo":   # rehearsal: every rank on the visible device(s), round-robin
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
@@ -186,7 +193,11 @@ def main():
     W, H, bounces = wl["W"], wl["H"], wl["bounces"]
     t_setup = time.perf_counter()
     scene = make_scene(rt, wl)
-    stream = torch.cuda.current_stream(dev)
+    # a real (non-null) torch stream per context: torch's default stream is the null stream
+    # (handle 0), and a context given stream 0 creates a private stream of its own, which
+    # `with torch.cuda.stream(...)` could not order the RCCL gather after
+    stream = torch.cuda.Stream(dev)
+    assert stream.cuda_stream != 0
     ctx = rt.Context(device=local, flags=rt.FLAG_TIMING, stream=stream.cuda_stream)
     ctx.set_scene(scene)
     wvp, wv = rt.camera_reference(W, H)
@@ -226,6 +237,9 @@ def main():
     # trace (tiles.py), and frames traced concurrently never share a buffer
     g = BandGather(W, H, rank, world, device=dev, nbuf=max(2, args.inflight))
     band = g.band
+    # torch fills the new buffers on its current stream; the other contexts' streams are
+    # not ordered after it (a late fill overwrote traced pixels in a 3-process rehearsal)
+    torch.cuda.synchronize()
 
     def run(nsteps, inflight):
         """nsteps frames: frame i traced by context i % inflight on its stream into band
@@ -269,8 +283,10 @@ def main():
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         ms = float(el.item()) / args.steps * 1e3
         rays = float(tot[0].item())
+        # the output: the frame assembled on rank 0 (one rank: its band buffer is the frame)
+        frame = g.frames[(args.steps - 1) % g.nbuf].clone() if rank == 0 else None
         return dict(ms_step=ms, rays=rays, value=rays / (ms * 1e-3) / 1e6, stats=ctx.stats(),
-                    band=last.clone())
+                    band=last.clone(), frame=frame)
 
     # reference order (the exact findCollision DFS), nearest-first, and nearest-first on the
     # 4-wide view; a nearest-first number is the headline only if its frame is bit-identical
@@ -288,7 +304,8 @@ def main():
         traversal[m.replace("-", "_") + "_ms"] = round(r["ms_step"], 4)
         if m == "reference-order":
             continue
-        same = torch.tensor([0.0 if torch.equal(ref["band"], r["band"]) else 1.0], device=dev)
+        # compared on rank 0's assembled frame (the product), the verdict shared with all ranks
+        same = torch.tensor([0.0 if rank != 0 or torch.equal(ref["frame"], r["frame"]) else 1.0], device=dev)
         if world > 1:
             dist.all_reduce(same)
         ident = float(same.item()) == 0.0
@@ -306,8 +323,22 @@ def main():
     traversal["inflight"] = args.inflight
     traversal["one_frame_latency_ms"] = round(lat["ms_step"], 4)
     traversal["one_frame_mrays_s"] = round(lat["value"], 2)
-    if not torch.equal(lat["band"], use["band"]):
-        raise RuntimeError("frames in flight changed the frame")
+    flag = torch.tensor([0.0 if rank != 0 or torch.equal(lat["frame"], use["frame"]) else 1.0], device=dev)
+    if world > 1:
+        dist.all_reduce(flag)
+    same_lat = float(flag.item()) == 0.0
+    if world > 1 and rank == 0:   # the frame assembled from every rank's bands vs one traced whole here
+        full = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        ctx.set_flags(rt.FLAG_TIMING | mode_flags)
+        ctx.trace_band_async(W, H, bounces, 0, 1, full.data_ptr())
+        ctx.synchronize()
+        traversal["assembled_frame_identical"] = bool(torch.equal(full, use["frame"]))
+    traversal["inflight_frame_identical"] = same_lat
+    if not same_lat and rank == 0:
+        d = (lat["frame"] != use["frame"]).any(dim=2)
+        print(f"[bench] frames in flight differ from one-frame frames: {int(d.sum())} pixels", file=sys.stderr,
+              flush=True)
 
     # ---- visit counts for the byte model (extra, untimed traces of this rank's bands):
     # the chosen mode's own counts, and the reference-order counts of SURVEY §8(d)
