@@ -42,6 +42,11 @@ S_BOUNCE = 112                   # reflectRay record read + write per bounce ray
 S_HIT = 72                       # matIndex + Material per hit
 S_TEX = 16                       # texel per textured hit
 S_BUILD_PER_TRI = 348            # B_build: Morton 80 + sort 160 + Karras 24 + refit 84
+# dependent random 64-B record fetches per second on MI355X (scripts/gather_roofline.hip,
+# profiles/r01_gather_roofline.jsonl): from HBM / the Infinity Cache (1.25 GiB and 128 MiB
+# tables, 2-8 waves/SIMD: 55-56 G/s) and from L2 (2 MiB table: 150 G/s)
+GATHER_HBM_RPS = 5.6e10
+GATHER_L2_RPS = 1.496e11
 WORKLOADS = {
     "c5": dict(name="C5: synthetic 10M tris (seed 0x5EED0005, box 100x100x50), 3840x2160, primary+1 bounce",
                ntris=10_000_000, seed=0x5EED0005, half=(100.0, 100.0, 50.0), W=3840, H=2160, bounces=1),
@@ -80,14 +85,15 @@ def frame_bytes(st):
             + S_BOUNCE * st["bounce_rays"] + S_HIT * sum(st["hits"]) + S_TEX * st["textured_hits"])
 
 
-def load_pmc(workload, mode, kernel):
-    """Per-launch HBM bytes of `kernel` from the PMC passes of the same traversal mode
-    (profiles/pmc_<workload>_<mode>.json, written by scripts/make_pmc_json.py)."""
+def load_pmc(workload, mode, kernel, counters=False):
+    """Per-launch HBM bytes of `kernel` (or its raw counters) from the PMC passes of the same
+    traversal mode (profiles/pmc_<workload>_<mode>.json, written by scripts/make_pmc_json.py)."""
     path = os.path.join(REPO, "profiles", f"pmc_{workload}_{mode}.json")
     if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path))["kernels"][kernel]["hbm_bytes_per_launch"]
+        k = json.load(open(path))["kernels"][kernel]
+        return k["counters"] if counters else k["hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -370,6 +376,19 @@ def main():
         tg = traffic / (kern[dom]["ms"] * 1e-3) / 1e9
         roofline.update({"traffic_gbs": round(tg, 1), "traffic_frac": round(tg / PEAK_HBM_GBS, 4),
                          "cache_served_frac": round(max(0.0, 1.0 - traffic / kern[dom]["bytes"]), 4)})
+    if dom == "k_bounce_trav":
+        # the roofline of a dependent-gather walk: one 64-B record per step (QNode or leaf), at
+        # the measured random-record rates of L2 and of HBM/Infinity Cache, split by the L2 hit
+        # fraction of the same kernel (PMC); frac = model time / measured time
+        pc = load_pmc(args.workload, use_name, dom, counters=True)
+        recs = cst["internal_visits"][1] + cst["leaf_visits"][1]
+        if pc and pc.get("TCC_HIT_sum") is not None and pc.get("TCC_MISS_sum"):
+            h = pc["TCC_HIT_sum"] / (pc["TCC_HIT_sum"] + pc["TCC_MISS_sum"])
+            model_ms = recs * (h / GATHER_L2_RPS + (1 - h) / GATHER_HBM_RPS) * 1e3
+            roofline["gather"] = {"records": int(recs), "l2_hit_frac": round(h, 4),
+                                  "peak_records_per_s": {"l2": GATHER_L2_RPS, "hbm": GATHER_HBM_RPS},
+                                  "model_ms": round(model_ms, 4), "kernel_ms": round(kern[dom]["ms"], 4),
+                                  "frac": round(model_ms / kern[dom]["ms"], 4)}
     fb = frame_bytes(rst)
     # SURVEY 8(d)'s whole-frame figure prices the REFERENCE-ORDER walk's visits; a traversal
     # that visits fewer nodes than that walk can exceed 1 here, so it is reported beside the
