@@ -11,9 +11,9 @@ over RCCL (torch.distributed "nccl") and assembled into the frame.
 
 One step = trace of this rank's bands (primary kernel + bounce kernels) + the
 RCCL gather + assembly on rank 0.  Two frames are in flight per rank (--inflight 2):
-frame i runs on context i % 2 (two replicas of the scene + BVH, built from the same
-inputs) on its own HIP stream, so frame i+1's primary pass fills the GPU while frame
-i's bounce walk drains its last long walks; two band buffers keep one gather in flight
+frame i is traced on stream i % 2 (the context gives each caller stream a trace-buffer
+set of its own over the one BVH: rtbvh_trace_band_async), so frame i+1's primary pass
+fills the GPU while frame i's bounce walk drains its last long walks; two band buffers keep one gather in flight
 (step i's gather overlaps step i+1's trace), and every step's frame is traced,
 gathered and assembled before the timed region closes.  The one-frame latency (one
 context, frames back to back on one stream) is reported beside it.  The BVH is built once before the timed
@@ -224,18 +224,10 @@ def main():
              "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
                                    [round(x, 4) for x in bst["ms_stage"][:5]]))}
 
-    # ---- frames in flight: context k (own stream) traces frames i = k mod inflight; the
-    # extra contexts are replicas (same inputs, same deterministic build), built untimed
-    ctxs, streams = [ctx], [stream]
-    for _ in range(args.inflight - 1):
-        sk = torch.cuda.Stream(dev)
-        ck = rt.Context(device=local, flags=rt.FLAG_TIMING, stream=sk.cuda_stream)
-        ck.set_scene(scene)
-        ck.set_camera(wvp, wv)
-        ck.build()
-        ctxs.append(ck)
-        streams.append(sk)
-    torch.cuda.synchronize()
+    # ---- frames in flight: frame i is traced on streams[i % inflight] (stream 0 is the
+    # context's); the context keeps a trace-buffer set per stream, all over the one BVH
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.inflight - 1)]
+    ctxs = [ctx]
 
     # ---- band buffers + RCCL gather plumbing (raytracebvh_amd/tiles.py)
     from raytracebvh_amd.tiles import BandGather
@@ -248,15 +240,15 @@ def main():
     torch.cuda.synchronize()
 
     def run(nsteps, inflight):
-        """nsteps frames: frame i traced by context i % inflight on its stream into band
-        buffer i % nbuf, then gathered (RCCL, after that stream) and assembled on the same
+        """nsteps frames: frame i traced on stream i % inflight into band buffer i % nbuf, then gathered (RCCL, after that stream) and assembled on the same
         stream, so the buffer's next trace waits for its gather; every frame is assembled
         before return."""
         pending = None
         for i in range(nsteps):
             k = i % inflight
             with torch.cuda.stream(streams[k]):
-                ctxs[k].trace_band_async(W, H, bounces, rank, world, g.band_buffer(i).data_ptr())
+                ctx.trace_band_async(W, H, bounces, rank, world, g.band_buffer(i).data_ptr(),
+                                     stream_ptr=streams[k].cuda_stream)
                 h = g.gather_async(i)
             if pending is not None:
                 with torch.cuda.stream(streams[pending[0] % inflight]):

@@ -198,7 +198,12 @@ rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* ctx, uint32_t width, uint32_t height, 
  * only the 8-row bands b with b % nranks == rank of a W x H frame and write them
  * compacted (band order) as RGBA f32 into dev_out (device memory, at least
  * rtbvh_band_rows(H, rank, nranks) * W * 4 floats), enqueued on `stream`
- * (hipStream_t, NULL = the context stream).  The caller gathers the shards. */
+ * (hipStream_t, NULL = the context stream).  The caller gathers the shards.
+ * Frames in flight: each caller stream other than the context's (up to 3) gets trace
+ * buffers of its own over the one BVH, so traces on different streams run concurrently
+ * (each into its own dev_out); they wait for the last build, and the next build waits for
+ * them; rtbvh_synchronize waits for them too, and rtbvh_get_stats reports the last
+ * trace.  Ray records (RTBVH_FLAG_REFRACT_RECORDS) are traced on the context stream only. */
 rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces,
                                     uint32_t rank, uint32_t nranks, float* dev_out, void* stream);
 uint32_t rtbvh_band_rows(uint32_t height, uint32_t rank, uint32_t nranks);

@@ -90,6 +90,16 @@ struct rtbvh_ctx {
     bool evt_trav[RING] = {};
     uint32_t n_builds = 0, n_traces = 0;   // timed samples since reset
     hipEvent_t ev_ready = nullptr;
+    // Frames in flight (rtbvh_trace_band_async on a caller stream other than the context's):
+    // such a stream gets a trace-buffer set of its own -- slot k >= 1: d_qs[k], d_hits[k],
+    // the queue counts at d_qcount + 32k and the counters at d_counters + 64k -- so traces on
+    // different streams run concurrently over the one BVH.  They wait only for the last
+    // build (ev_built); the next build waits for them (ev_slot).
+    hipStream_t slot_stream[MAXSPLIT] = {};
+    hipEvent_t ev_built = nullptr, ev_slot[MAXSPLIT] = {};
+    bool slot_busy[MAXSPLIT] = {};
+    uint32_t last_slot = 0;   // slot of the last trace (its counters are the stats)
+    bool slots_used = false;  // a foreign-stream slot was used: trace chains are off
 };
 
 namespace {
@@ -163,7 +173,7 @@ rtbvh_status ensure_trace_capacity(rtbvh_ctx* c, size_t P) {
     HIPC(c, dalloc(c->d_bscratch, sort_scratch_words((uint32_t)P)));
     HIPC(c, dalloc(c->d_hit, P));
     if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 32 * rtbvh_ctx::MAXSPLIT));
-    if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 64));
+    if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 64 * rtbvh_ctx::MAXSPLIT));
     c->cap_P = P;
     return RTBVH_OK;
 }
@@ -180,6 +190,8 @@ rtbvh_status ensure_split_capacity(rtbvh_ctx* c, uint32_t nsplit, size_t rays) {
     if (nsplit < 2) return RTBVH_OK;
     const bool grow = rays > c->cap_split;
     if (grow) {   // every chain's queues hold cap_split rays: drop the smaller ones
+        for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // (after any frame in flight on them)
+            if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
         c->cap_split = rays;
         for (uint32_t g = nsplit; g < rtbvh_ctx::MAXSPLIT; g++) {
             dfree(c->d_qs[g][0]); dfree(c->d_qs[g][1]); dfree(c->d_hits[g]);
@@ -305,7 +317,7 @@ rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
 }
 
 rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
-                           float4* color, float* inten, hipStream_t s) {
+                           float4* color, float* inten, hipStream_t s, uint32_t slot = 0) {
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
     if (W == 0 || H == 0 || nranks == 0 || rank >= nranks || bounces > 14)
         return fail(c, RTBVH_ERR_INVALID_ARG, "bad trace dimensions");
@@ -315,7 +327,8 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool count = (c->cfg.flags & RTBVH_FLAG_COUNT_VISITS) != 0;
     const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream;
     TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, 64 * sizeof(unsigned long long), s));
+    a.counters = c->d_counters + 64 * slot;
+    HIPC(c, hipMemsetAsync(a.counters, 0, 64 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
     // kernel variant: 0 reference order, 1 nearest-first, 2 first version (A/B)
     int variant = (c->cfg.flags & RTBVH_FLAG_NEAREST_FIRST) ? 1 : 0;
@@ -326,6 +339,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
     const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && vsel != 1;
     const bool records = (c->cfg.flags & RTBVH_FLAG_REFRACT_RECORDS) != 0;
+    if (records && slot) return fail(c, RTBVH_ERR_INVALID_ARG, "ray records are traced on the context stream only");
     // the records are written by k_primary and k_bounce_shade: the split bounce path
     const bool refill = ((c->cfg.flags & RTBVH_FLAG_REFILL_BOUNCE) != 0 || wide || records) && vsel != 1;
     // A/B of the refill kernel's LDS stack depth: variant 2 -> none, 3 -> 8, 4 -> 20, else 16
@@ -362,11 +376,12 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t nbands = (H + 7) / 8;
     const uint32_t my_bands = rank < nbands ? (nbands - rank + nranks - 1) / nranks : 0;
     uint32_t nsplit = trace_split(c, (size_t)W * 8 * my_bands);
-    if (sort || my_bands < nsplit) nsplit = 1;   // the coherence sort has one set of buffers
+    // the coherence sort has one set of buffers; frames-in-flight slots use the chains' buffers
+    if (sort || my_bands < nsplit || slot || c->slots_used) nsplit = 1;
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
-    st = ensure_split_capacity(c, nsplit, Pg);
+    st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
-    HIPC(c, hipMemsetAsync(c->d_qcount, 0, 32 * nsplit * sizeof(uint32_t), s));
+    HIPC(c, hipMemsetAsync(c->d_qcount + 32 * slot, 0, 32 * nsplit * sizeof(uint32_t), s));
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (nsplit > 1) HIPC(c, hipEventRecord(c->ev_fork, s));
     for (uint32_t g = 0; g < nsplit; g++) {
@@ -375,9 +390,10 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         TraceArgs ag = a;
         ag.band0 = g;
         ag.bstep = nsplit;
-        RayQ* q[2] = {g ? c->d_qs[g][0] : c->d_q[0], g ? c->d_qs[g][1] : c->d_q[1]};
-        float2* hit = g ? c->d_hits[g] : c->d_hit;
-        uint32_t* qc = c->d_qcount + 32 * g;
+        const uint32_t b = g + slot;   // buffer set: chain g of the context stream's trace, or the slot
+        RayQ* q[2] = {b ? c->d_qs[b][0] : c->d_q[0], b ? c->d_qs[b][1] : c->d_q[1]};
+        float2* hit = b ? c->d_hits[b] : c->d_hit;
+        uint32_t* qc = c->d_qcount + 32 * b;
         const bool tg = timing && g == 0;   // stage events: chain 0's kernels
         launch_primary(ag, q[0], &qc[0], count, bounces > 0, pvariant, sg);
         if (tg) HIPC(c, hipEventRecord(ev[1], sg));
@@ -405,6 +421,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         }
     }
     c->nsplit = nsplit;
+    c->last_slot = slot;
     if (timing) {
         HIPC(c, hipEventRecord(ev[2], s));
         c->evt_trav[c->n_traces % rtbvh_ctx::RING] = refill && bounces > 0;
@@ -477,7 +494,8 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
         rtbvh_destroy(c);
         return fail(nullptr, RTBVH_ERR_HIP, "hipEventCreate failed");
     }
-    if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_built, hipEventDisableTiming) != hipSuccess) {
         rtbvh_destroy(c);
         return fail(nullptr, RTBVH_ERR_HIP, "hipEventCreate failed");
     }
@@ -489,6 +507,12 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)
+        if (c->ev_slot[k]) {
+            (void)hipEventSynchronize(c->ev_slot[k]);   // frames in flight on caller streams
+            (void)hipEventDestroy(c->ev_slot[k]);
+        }
+    if (c->ev_built) (void)hipEventDestroy(c->ev_built);
     for (uint32_t g = 1; g < rtbvh_ctx::MAXSPLIT; g++) {
         if (c->sub[g]) {
             (void)hipStreamSynchronize(c->sub[g]);
@@ -604,6 +628,11 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     hipStream_t s = c->stream;
     const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0;
     BuildArgs a = build_args(c);
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // frames in flight read the old BVH
+        if (c->slot_busy[k]) {
+            HIPC(c, hipStreamWaitEvent(s, c->ev_slot[k], 0));
+            c->slot_busy[k] = false;
+        }
     hipEvent_t* ev = c->evb[c->n_builds % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (c->T <= small_build_max() && !(c->cfg.flags & RTBVH_FLAG_MULTI_KERNEL_BUILD)) {
@@ -615,6 +644,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         launch_qnodes(a, s);
         if (timing) for (int k = 1; k <= 5; k++) HIPC(c, hipEventRecord(ev[k], s));
         if (timing) c->n_builds++;
+        HIPC(c, hipEventRecord(c->ev_built, s));
         c->built = true;
         return check_launch(c, "build kernel");
     }
@@ -636,6 +666,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     launch_qnodes(a, s);   // timed with the refit stage
     if (timing) HIPC(c, hipEventRecord(ev[5], s));
     if (timing) c->n_builds++;
+    HIPC(c, hipEventRecord(c->ev_built, s));
     c->built = true;
     return check_launch(c, "build kernels");
 }
@@ -680,15 +711,25 @@ rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32
     if (!c || !dev_out) return RTBVH_ERR_INVALID_ARG;
     HIPC(c, hipSetDevice(c->cfg.device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (s != c->stream) {   // order after the build / previous work on the context stream
-        HIPC(c, hipEventRecord(c->ev_ready, c->stream));
-        HIPC(c, hipStreamWaitEvent(s, c->ev_ready, 0));
+    uint32_t slot = 0;
+    if (s != c->stream) {   // a frame in flight: this stream's buffer slot, after the last build
+        for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT && !slot; k++)
+            if (c->slot_stream[k] == s) slot = k;
+        for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT && !slot; k++)
+            if (!c->slot_stream[k]) {
+                c->slot_stream[k] = s;
+                slot = k;
+            }
+        if (!slot) return fail(c, RTBVH_ERR_INVALID_ARG, "more than 3 caller streams trace one context");
+        if (!c->ev_slot[slot]) HIPC(c, hipEventCreateWithFlags(&c->ev_slot[slot], hipEventDisableTiming));
+        c->slots_used = true;
+        HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
     }
-    rtbvh_status st = enqueue_trace(c, W, H, bounces, rank, nranks, (float4*)dev_out, nullptr, s);
+    rtbvh_status st = enqueue_trace(c, W, H, bounces, rank, nranks, (float4*)dev_out, nullptr, s, slot);
     if (st) return st;
-    if (s != c->stream) {   // and make later context work wait for this trace
-        HIPC(c, hipEventRecord(c->ev_ready, s));
-        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_ready, 0));
+    if (slot) {   // the next build (context stream) waits for this trace
+        HIPC(c, hipEventRecord(c->ev_slot[slot], s));
+        c->slot_busy[slot] = true;
     }
     return RTBVH_OK;
 }
@@ -784,6 +825,8 @@ rtbvh_status rtbvh_trace_tiles(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
 rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
     if (!c) return RTBVH_ERR_INVALID_ARG;
     HIPC(c, hipStreamSynchronize(c->stream));
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // and the frames in flight on caller streams
+        if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
     return RTBVH_OK;
 }
 
@@ -900,6 +943,8 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
     if (!c || !out) return RTBVH_ERR_INVALID_ARG;
     memset(out, 0, sizeof(*out));
     HIPC(c, hipStreamSynchronize(c->stream));
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)
+        if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
     out->num_tris = c->T;
     out->num_nodes = c->T ? 2 * c->T - 1 : 0;
     out->width = c->W;
@@ -933,8 +978,9 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
     if (c->traced && c->d_counters) {
         unsigned long long cnt[64];
         uint32_t q[32 * rtbvh_ctx::MAXSPLIT];
-        HIPC(c, hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
-        HIPC(c, hipMemcpy(q, c->d_qcount, sizeof(uint32_t) * 32 * c->nsplit, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(cnt, c->d_counters + 64 * c->last_slot, sizeof(cnt), hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(q, c->d_qcount + 32 * c->last_slot, sizeof(uint32_t) * 32 * c->nsplit,
+                          hipMemcpyDeviceToHost));
         out->primary_rays = (uint64_t)c->W * rtbvh_band_rows(c->H, c->rank, c->nranks);
         uint64_t b = 0;
         for (uint32_t g = 0; g < c->nsplit; g++)

@@ -582,6 +582,7 @@ def test_trace_chains_match_one_chain(mode, nsplit):
                 for r in range(nranks):
                     rows = rt.lib().rtbvh_band_rows(H, r, nranks)
                     buf = torch.full((rows, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
+                    torch.cuda.synchronize()   # the fill runs on torch's stream, not the context's
                     c.trace_band_async(W, H, 2, r, nranks, buf.data_ptr())
                     c.synchronize()
                     out[(k, nranks, r)] = (buf.cpu().numpy(), c.stats()["bounce_rays"])
@@ -593,6 +594,43 @@ def test_trace_chains_match_one_chain(mode, nsplit):
         band, nb = out[key]
         band_k, nb_k = out[(nsplit,) + key[1:]]
         assert np.array_equal(band_k, band) and nb_k == nb, key
+
+
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+def test_frames_in_flight_match_one_at_a_time(nranks):
+    """Frames in flight (bench.py): one context, frames dealt over three caller streams
+    (each gets a trace-buffer slot of its own over the one BVH) and traced back to back
+    without synchronisation -- every frame equals the one traced alone on the context
+    stream, and the stats are the last frame's; rank 1's bands of N ranks (N = 1: the
+    whole frame).  A rebuild waits for the frames in flight."""
+    import torch
+    s = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    W, H = 1000, 357
+    r = min(1, nranks - 1)
+    rows = rt.lib().rtbvh_band_rows(H, r, nranks)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    with rt.Context(device=0, flags=TRACE_MODES["nearest+packet+wide"]) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(W, H))
+        c.build()
+        alone = torch.full((rows, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
+        bufs = [torch.full((rows, W, 4), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(6)]
+        torch.cuda.synchronize()
+        c.trace_band_async(W, H, 1, r, nranks, alone.data_ptr())
+        c.synchronize()
+        st_alone = c.stats()
+        for i, b in enumerate(bufs):
+            c.trace_band_async(W, H, 1, r, nranks, b.data_ptr(), stream_ptr=streams[i % 3].cuda_stream)
+        c.build()   # waits for the frames in flight before it rewrites the BVH
+        c.synchronize()
+        torch.cuda.synchronize()
+        st = c.stats()
+        for i, b in enumerate(bufs):
+            assert torch.equal(b, alone), i
+        assert (alone[:, :, 3] != -1.0).all()
+        assert st["bounce_rays"] == st_alone["bounce_rays"] > 0 and st["hits"] == st_alone["hits"]
+        with pytest.raises(rt.RtbvhError):   # a fourth caller stream has no slot
+            c.trace_band_async(W, H, 1, r, nranks, bufs[0].data_ptr(), stream_ptr=torch.cuda.Stream().cuda_stream)
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
@@ -611,6 +649,7 @@ def test_band_split_reassembles_full_frame(nranks):
         for r in range(nranks):
             rows = rt.lib().rtbvh_band_rows(H, r, nranks)
             buf = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda:0")
+            torch.cuda.synchronize()   # the fill runs on torch's stream, not the context's
             c.trace_band_async(W, H, 1, r, nranks, buf.data_ptr())
             c.synchronize()
             got = buf.cpu().numpy()
@@ -635,6 +674,7 @@ def test_assemble_bands_matches_full_frame(nranks):
         full = c.read_framebuffer()
         rows0 = rt.lib().rtbvh_band_rows(H, 0, nranks)
         bands = torch.full((nranks, rows0, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()   # the fill runs on torch's stream, not the context's
         for r in range(nranks):
             c.trace_band_async(W, H, 1, r, nranks, bands[r].data_ptr())
         frame = torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0")
