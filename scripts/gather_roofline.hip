@@ -54,6 +54,23 @@ __global__ __launch_bounds__(256) void k_chase(const uint4* __restrict__ a, uint
     if (s == 0x12345u) out[0] = s ^ r;
 }
 
+// k_chase with RECW-byte records (RECW = 16, 32, 64): does the rate follow the records
+// (requests) or the bytes / load instructions?
+template <int RECW>
+__global__ __launch_bounds__(256) void k_chase_w(const uint4* __restrict__ a, uint32_t nrec, uint32_t steps,
+                                                 uint32_t* out) {
+    uint32_t r = ((blockIdx.x * blockDim.x + threadIdx.x) * 0x9E3779B1u) & (nrec - 1);
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < steps; k++) {
+        const uint4* p = a + (RECW / 16) * (size_t)r;
+        uint4 v = p[0];
+        if (RECW >= 32) { const uint4 w = p[1]; v.y ^= w.x; v.z ^= w.w; }
+        s ^= v.y ^ v.z;
+        r = (v.x ^ (r * 0x85EBCA6Bu) ^ k) & (nrec - 1);
+    }
+    if (s == 0x12345u) out[0] = s ^ r;
+}
+
 int main(int argc, char** argv) {
     const int wps = argc > 1 ? atoi(argv[1]) : 8;
     const uint32_t steps = argc > 2 ? (uint32_t)atoi(argv[2]) : 256;
@@ -87,15 +104,22 @@ int main(int argc, char** argv) {
     const uint32_t blocks = (uint32_t)(cus * 4 * wps / 4);   // 4 waves per 256-thread block
     if (nrec2 < 256) return 1;
     const float ms_chase = timed([&] { k_chase<<<blocks, 256>>>(a, nrec2, steps, out); }, 5);
+    // the same table as 16- and 32-B records (4x / 2x as many, same bytes)
+    uint32_t n16 = 1, n32 = 1;
+    while (n16 * 2 <= (uint32_t)(bytes / 16)) n16 *= 2;
+    while (n32 * 2 <= (uint32_t)(bytes / 32)) n32 *= 2;
+    const float ms_c16 = timed([&] { k_chase_w<16><<<blocks, 256>>>(a, n16, steps, out); }, 5);
+    const float ms_c32 = timed([&] { k_chase_w<32><<<blocks, 256>>>(a, n32, steps, out); }, 5);
     CHECK(hipDeviceSynchronize());
     const double lanes = (double)blocks * 256;
     const double recs = lanes * steps;
     printf("{\"cus\": %d, \"table_bytes\": %zu, \"stream_gbs\": %.1f, \"gather_records_per_s\": %.4g, "
            "\"gather_record_gbs\": %.1f, \"gather_line_gbs\": %.1f, \"chase_waves_per_simd\": %d, \"chase_lanes\": %.0f, "
            "\"chase_steps\": %u, \"chase_ms\": %.4f, \"chase_records_per_s\": %.4g, \"chase_record_gbs\": %.1f, "
-           "\"chase_step_latency_us\": %.3f}\n",
+           "\"chase_step_latency_us\": %.3f, \"chase16_records_per_s\": %.4g, \"chase32_records_per_s\": %.4g}\n",
            cus, bytes, bytes / (ms_stream * 1e-3) / 1e9, nrec2 / (ms_gather * 1e-3),
            nrec2 * 64.0 / (ms_gather * 1e-3) / 1e9, nrec2 * 128.0 / (ms_gather * 1e-3) / 1e9, wps, lanes, steps,
-           ms_chase, recs / (ms_chase * 1e-3), recs * 64 / (ms_chase * 1e-3) / 1e9, ms_chase * 1e3 / steps);
+           ms_chase, recs / (ms_chase * 1e-3), recs * 64 / (ms_chase * 1e-3) / 1e9, ms_chase * 1e3 / steps,
+           recs / (ms_c16 * 1e-3), recs / (ms_c32 * 1e-3));
     return 0;
 }
