@@ -52,6 +52,8 @@ WORKLOADS = {
                ntris=10_000_000, seed=0x5EED0005, half=(100.0, 100.0, 50.0), W=3840, H=2160, bounces=1),
     "c3": dict(name="C3: Obj/Test.obj (1952 tris), 1920x1080, primary+1 bounce", obj="Test", W=1920, H=1080,
                bounces=1),
+    "c2": dict(name="C2: Obj/Image_Test.obj (3072 tris), 1920x1080, primary rays only", obj="Image_Test", W=1920,
+               H=1080, bounces=0),
 }
 
 
@@ -156,7 +158,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c5", choices=["c5", "c3"])
     ap.add_argument("--build-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C4 build / C3 side measurements")
@@ -411,22 +413,29 @@ def main():
                                   "achieved_gbs": round(S_BUILD_PER_TRI * 1e7 / (s4["ms_build"] * 1e-3) / 1e9, 1),
                                   "stages_ms": [round(x, 4) for x in s4["ms_stage"][:5]]}
             del c4
-            s3 = make_scene(rt, WORKLOADS["c3"])
-            with rt.Context(device=local, flags=rt.FLAG_TIMING) as c:
-                c.set_scene(s3)
-                c.set_camera(*rt.camera_reference(1920, 1080))
-                c.compute_bvh(1920, 1080, 1)
-                q = c.stats()
-                c.reset_stats()
-                t0 = time.perf_counter()
-                for _ in range(50):
-                    c.compute_bvh(1920, 1080, 1)
-                dt = (time.perf_counter() - t0) / 50
-                q2 = c.stats()
-            r3 = q["primary_rays"] + q["bounce_rays"]
-            extras["c3_frame"] = {"mrays_s_trace": round(r3 / (q2["ms_trace"] * 1e-3) / 1e6, 1),
-                                  "mrays_s_build_plus_trace_wall": round(r3 / dt / 1e6, 1),
-                                  "ms_build": round(q2["ms_build"], 4), "ms_trace": round(q2["ms_trace"], 4)}
+            # C3 (Test.obj, primary + 1 bounce) and C2 (Image_Test.obj, primary only): the
+            # reference rebuilds and traces every frame (Graphics.cpp:56), so build + trace
+            for key in ("c3", "c2"):
+                wk = WORKLOADS[key]
+                sk = make_scene(rt, wk)
+                # the reference-order kernels (the exact findCollision DFS): on these few-thousand-
+                # triangle scenes they beat the packet / wide walks (C3 trace 0.28 vs 0.33 ms)
+                with rt.Context(device=local, flags=rt.FLAG_TIMING) as c:
+                    c.set_scene(sk)
+                    c.set_camera(*rt.camera_reference(wk["W"], wk["H"]))
+                    c.compute_bvh(wk["W"], wk["H"], wk["bounces"])
+                    q = c.stats()
+                    c.reset_stats()
+                    t0 = time.perf_counter()
+                    for _ in range(50):
+                        c.compute_bvh(wk["W"], wk["H"], wk["bounces"])
+                    dt = (time.perf_counter() - t0) / 50
+                    q2 = c.stats()
+                rk = q["primary_rays"] + q["bounce_rays"]
+                extras[f"{key}_frame"] = {"workload": wk["name"], "rays": int(rk),
+                                          "mrays_s_trace": round(rk / (q2["ms_trace"] * 1e-3) / 1e6, 1),
+                                          "mrays_s_build_plus_trace_wall": round(rk / dt / 1e6, 1),
+                                          "ms_build": round(q2["ms_build"], 4), "ms_trace": round(q2["ms_trace"], 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline (oracle, bounded sample) ...")
