@@ -781,6 +781,15 @@ __device__ __forceinline__ void sort2(float& ta, uint32_t& ia, float& tb, uint32
     ia = i;
 }
 
+// bf16 of an entry distance rounded toward -inf (so bf16_up(bf16_down(t)) <= t: positive t
+// truncated, negative t rounded away from zero; infinities and NaNs keep their class)
+__device__ __forceinline__ uint16_t bf16_down(float t) {
+    uint32_t b = __float_as_uint(t);
+    if ((b & 0x80000000u) && (b & 0xFFFFu) && (b & 0x7F800000u) != 0x7F800000u) b += 0x10000u;
+    return (uint16_t)(b >> 16);
+}
+__device__ __forceinline__ float bf16_up(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
 // Binary modes keep the stack entries [0, S) in LDS, [entry][lane] (a wave's lanes hit
 // 64 distinct banks whatever their depths), and only deeper entries in scratch: the
 // all-scratch stack of 8192 resident waves (17 KB each) does not fit in L2 and PMC
@@ -814,8 +823,14 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
     __shared__ uint32_t s_stk[WIDE || S == 0 ? 1 : S][BLOCK];
     uint32_t stack[WIDE ? 1 : STACK_SIZE - S];   // entries [S, STACK_SIZE)
-    constexpr int SW = WIDE ? S : 0;             // 4-wide: (node, entry distance) pairs in LDS
-    __shared__ uint2 s_wstk[SW == 0 ? 1 : SW][BLOCK];
+    // 4-wide: (node, entry distance) entries [0, SW) in LDS as a node id and the distance as a
+    // bf16 rounded toward -inf (6 B: SW entries in the LDS that held 2/3 SW full pairs; the
+    // pop's prune test on the rounded-down distance keeps every entry the exact test keeps),
+    // deeper entries as full pairs in scratch.  PMC (C5, SW = 8 full pairs): ~26% of the
+    // walk's L2 requests were scratch-stack traffic.
+    constexpr int SW = WIDE ? S : 0;
+    __shared__ uint32_t s_wid[SW == 0 ? 1 : SW][BLOCK];
+    __shared__ uint16_t s_wt[SW == 0 ? 1 : SW][BLOCK];
     uint2 wstack[WIDE ? STACK4 - SW : 1];        // entries [SW, STACK4)
     const uint32_t tid = threadIdx.x;
     auto spush = [&](uint32_t v) {
@@ -827,9 +842,12 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         if (--sp >= 0) top = sp < S ? s_stk[sp][tid] : stack[sp - S];
     };
     auto wpush = [&](uint32_t id, float t) {
-        const uint2 e = make_uint2(id, __float_as_uint(t));
-        if (sp < SW) s_wstk[sp][tid] = e;
-        else wstack[sp - SW] = e;
+        if (sp < SW) {
+            s_wid[sp][tid] = id;
+            s_wt[sp][tid] = bf16_down(t);
+        } else {
+            wstack[sp - SW] = make_uint2(id, __float_as_uint(t));
+        }
         ++sp;
     };
     bool drained = false;
@@ -1051,7 +1069,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         if (WIDE && !done && node == INVALID) {   // pop, dropping entries that cannot improve
             while (sp > 0) {
                 --sp;
-                const uint2 e = sp < SW ? s_wstk[sp][tid] : wstack[sp - SW];
+                uint2 e;
+                if (sp < SW) e = make_uint2(s_wid[sp][tid], __float_as_uint(bf16_up(s_wt[sp][tid])));
+                else e = wstack[sp - SW];
                 if (!hit || __uint_as_float(e.y) <= best) {
                     if (POSTPONE && (e.x & LEAF_BIT) && pend == INVALID) {
                         pend = e.x;   // park a popped leaf too, and keep popping for a node
@@ -1223,8 +1243,8 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
     const uint32_t blocks = 2048;   // persistent: 8 waves/SIMD x 1024 SIMDs / 4 waves per block
     const uint32_t extra_lds = (chunk >> 24) * 1024u;   // A/B only: dynamic LDS (KB in the top byte)
     chunk &= (1u << 24) - 1;                            // that caps the resident blocks per CU
-    if (mode == 4)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 4, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s,
+    if (mode == 4)   // 12 entries x 6 B x 256 lanes = 18 KB per block (8 blocks per CU)
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, 4, (S > 8 ? 12 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s,
                            a.inner4, a.qnode, a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, refill_min,
                            chunk, leaf_batch);
     else if (mode == 3)
