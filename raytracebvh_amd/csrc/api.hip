@@ -89,7 +89,6 @@ struct rtbvh_ctx {
     hipEvent_t evt[RING][5] = {};   // trace start, primary done, end, first bounce traversal start/end
     bool evt_trav[RING] = {};
     uint32_t n_builds = 0, n_traces = 0;   // timed samples since reset
-    hipEvent_t ev_ready = nullptr;
     // Frames in flight (rtbvh_trace_band_async on a caller stream other than the context's):
     // such a stream gets a trace-buffer set of its own -- slot k >= 1: d_qs[k], d_hits[k],
     // the queue counts at d_qcount + 32k and the counters at d_counters + 64k -- so traces on
@@ -494,8 +493,7 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
         rtbvh_destroy(c);
         return fail(nullptr, RTBVH_ERR_HIP, "hipEventCreate failed");
     }
-    if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_built, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c->ev_built, hipEventDisableTiming) != hipSuccess) {
         rtbvh_destroy(c);
         return fail(nullptr, RTBVH_ERR_HIP, "hipEventCreate failed");
     }
@@ -538,7 +536,6 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     for (auto& row : c->evt)
         for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
-    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
