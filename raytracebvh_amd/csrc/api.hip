@@ -359,6 +359,11 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1)
         pvariant = wide ? (vsel == 11 ? 6 : vsel == 12 ? 7 : 5) : (variant == 1 ? 4 : 3);
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
+    // persistent grid of the bounce walk: 2048 blocks (8 waves/SIMD), 1024 for a shard of
+    // < 4M pixels -- with frames in flight the next frame's primary blocks then share the CUs
+    // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame); A/B: variant 19
+    // -> 1024, 21 -> 1536, 27 -> 2048
+    const uint32_t tblocks = vsel == 19 ? 1024 : vsel == 21 ? 1536 : vsel == 27 ? 2048 : (P < (1u << 22) ? 1024 : 2048);
     if (records) {
         if (c->cap_rec < P) {
             HIPC(c, dalloc(c->d_refl_rec, 14 * (size_t)P));
@@ -406,7 +411,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             if (refill) {
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[3], sg));
                 launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, bmode, hit, &qc[16 + b], lds_stack,
-                                       refill_min, chunk, leaf_batch, sg);
+                                       refill_min, chunk, leaf_batch, tblocks, sg);
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[4], sg));
                 launch_bounce_shade(ag, q[b & 1], &qc[b], hit, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
                                     Pg, sg);

@@ -105,7 +105,7 @@ void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_coun
 // refill (0: default); chunk = rays one work-counter atomic claims for the wave (0: as many as idle)
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
-                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, hipStream_t s);
+                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, uint32_t blocks, hipStream_t s);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
 // frame from per-rank compact band buffers (stride_rows rows apart), see rtbvh_assemble_bands

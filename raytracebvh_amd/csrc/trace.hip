@@ -1239,8 +1239,8 @@ __global__ __launch_bounds__(BLOCK) void k_assemble(const float4* __restrict__ b
 template <bool COUNT, int S>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           int mode, float2* hitrec, uint32_t* next, uint32_t refill_min, uint32_t chunk,
-                          uint32_t leaf_batch, hipStream_t s) {
-    const uint32_t blocks = 2048;   // persistent: 8 waves/SIMD x 1024 SIMDs / 4 waves per block
+                          uint32_t leaf_batch, uint32_t blocks, hipStream_t s) {
+    // persistent: 2048 blocks = 8 waves/SIMD x 1024 SIMDs / 4 waves per block
     const uint32_t extra_lds = (chunk >> 24) * 1024u;   // A/B only: dynamic LDS (KB in the top byte)
     chunk &= (1u << 24) - 1;                            // that caps the resident blocks per CU
     if (mode == 4)   // 12 entries x 6 B x 256 lanes = 18 KB per block (8 blocks per CU)
@@ -1301,11 +1301,14 @@ void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, 
 
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
-                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, hipStream_t s) {
+                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, uint32_t blocks, hipStream_t s) {
     if (refill_min == 0) refill_min = REFILL_MIN;
+    if (blocks == 0) blocks = 2048;
 #define RTBVH_TRAV(S)                                                                                        \
-    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, s) \
-           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, s))
+    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, \
+                                           blocks, s)                                                              \
+           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, \
+                                            blocks, s))
     switch (lds_stack) {
         case 0: RTBVH_TRAV(0); break;
         case 8: RTBVH_TRAV(8); break;
