@@ -431,10 +431,19 @@ def main():
                         c.compute_bvh(wk["W"], wk["H"], wk["bounces"])
                     dt = (time.perf_counter() - t0) / 50
                     q2 = c.stats()
+                with rt.Context(device=local, flags=rt.FLAG_GRAPH) as c:   # the frame as one hipGraph
+                    c.set_scene(sk)
+                    c.set_camera(*rt.camera_reference(wk["W"], wk["H"]))
+                    c.compute_bvh(wk["W"], wk["H"], wk["bounces"])   # capture
+                    t0 = time.perf_counter()
+                    for _ in range(50):
+                        c.compute_bvh(wk["W"], wk["H"], wk["bounces"])
+                    dtg = (time.perf_counter() - t0) / 50
                 rk = q["primary_rays"] + q["bounce_rays"]
                 extras[f"{key}_frame"] = {"workload": wk["name"], "rays": int(rk),
                                           "mrays_s_trace": round(rk / (q2["ms_trace"] * 1e-3) / 1e6, 1),
                                           "mrays_s_build_plus_trace_wall": round(rk / dt / 1e6, 1),
+                                          "mrays_s_build_plus_trace_wall_graph": round(rk / dtg / 1e6, 1),
                                           "ms_build": round(q2["ms_build"], 4), "ms_trace": round(q2["ms_trace"], 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

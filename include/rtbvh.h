@@ -126,7 +126,11 @@ enum {
     RTBVH_FLAG_VARIANT_SHIFT = 8,
     /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n
        independent primary -> bounce kernel chains on n streams (same results) */
-    RTBVH_FLAG_SPLIT_SHIFT = 17
+    RTBVH_FLAG_SPLIT_SHIFT = 17,
+    RTBVH_FLAG_GRAPH = 1u << 20   /* rtbvh_compute_bvh replays one hipGraph of the whole frame (build +
+                                     trace: ~20 launches and memsets), captured on the first call and
+                                     re-captured when W, H, bounces, the flags, the scene or the
+                                     camera change; no per-stage times (rtbvh_get_stats) */
 };
 
 typedef struct {

@@ -24,6 +24,7 @@ FLAG_WIDE_BVH = 1 << 7
 FLAG_MULTI_KERNEL_BUILD = 1 << 16
 FLAG_VARIANT_SHIFT = 8
 FLAG_SPLIT_SHIFT = 17   # trace chains: (n << FLAG_SPLIT_SHIFT), 0 = automatic
+FLAG_GRAPH = 1 << 20    # compute_bvh replays a captured hipGraph of the frame
 
 # every symbol include/rtbvh.h declares (tests check the library exports them all)
 EXPORTS = [

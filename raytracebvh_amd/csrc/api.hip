@@ -99,6 +99,11 @@ struct rtbvh_ctx {
     bool slot_busy[MAXSPLIT] = {};
     uint32_t last_slot = 0;   // slot of the last trace (its counters are the stats)
     bool slots_used = false;  // a foreign-stream slot was used: trace chains are off
+    // RTBVH_FLAG_GRAPH: the captured frame (build + trace) of rtbvh_compute_bvh and its key
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    uint64_t graph_key[4] = {};
+    bool capturing = false;   // enqueueing into a capture: no event records
 };
 
 namespace {
@@ -309,6 +314,13 @@ const Rccl& rccl() {
     return lib;
 }
 
+void drop_graph(rtbvh_ctx* c) {
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->graph_exec = nullptr;
+    c->graph = nullptr;
+}
+
 rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(c, RTBVH_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -324,7 +336,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (st) return st;
     if (!color) color = c->d_color;
     const bool count = (c->cfg.flags & RTBVH_FLAG_COUNT_VISITS) != 0;
-    const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream;
+    const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream && !c->capturing;
     TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
     a.counters = c->d_counters + 64 * slot;
     HIPC(c, hipMemsetAsync(a.counters, 0, 64 * sizeof(unsigned long long), s));
@@ -516,6 +528,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
             (void)hipEventDestroy(c->ev_slot[k]);
         }
     if (c->ev_built) (void)hipEventDestroy(c->ev_built);
+    drop_graph(c);
     for (uint32_t g = 1; g < rtbvh_ctx::MAXSPLIT; g++) {
         if (c->sub[g]) {
             (void)hipStreamSynchronize(c->sub[g]);
@@ -551,6 +564,7 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
                              uint32_t nidx, const uint32_t* mat_idx, const rtbvh_material* mats, uint32_t nmats,
                              const rtbvh_texture* textures, uint32_t ntex) {
     if (!c) return RTBVH_ERR_INVALID_ARG;
+    drop_graph(c);   // a captured frame holds the old buffers
     if (ntex && !textures) return fail(c, RTBVH_ERR_INVALID_ARG, "set_scene: ntex > 0 without textures");
     for (uint32_t k = 0; k < ntex; k++)
         if (textures[k].width == 0 || textures[k].height == 0 || !textures[k].rgba8)
@@ -620,6 +634,7 @@ rtbvh_status rtbvh_set_camera(rtbvh_ctx* c, const float wvp[16], const float wv[
     memcpy(c->wvp, wvp, sizeof(c->wvp));
     memcpy(c->wv, wv, sizeof(c->wv));
     c->have_camera = true;
+    drop_graph(c);   // the camera is baked into a captured frame
     return RTBVH_OK;
 }
 
@@ -628,7 +643,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (!c->have_scene || !c->have_camera) return fail(c, RTBVH_ERR_NOT_READY, "build before set_scene/set_camera");
     HIPC(c, hipSetDevice(c->cfg.device));
     hipStream_t s = c->stream;
-    const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0;
+    const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && !c->capturing;
     BuildArgs a = build_args(c);
     for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // frames in flight read the old BVH
         if (c->slot_busy[k]) {
@@ -646,7 +661,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         launch_qnodes(a, s);
         if (timing) for (int k = 1; k <= 5; k++) HIPC(c, hipEventRecord(ev[k], s));
         if (timing) c->n_builds++;
-        HIPC(c, hipEventRecord(c->ev_built, s));
+        if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
         c->built = true;
         return check_launch(c, "build kernel");
     }
@@ -668,7 +683,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     launch_qnodes(a, s);   // timed with the refit stage
     if (timing) HIPC(c, hipEventRecord(ev[5], s));
     if (timing) c->n_builds++;
-    HIPC(c, hipEventRecord(c->ev_built, s));
+    if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
     c->built = true;
     return check_launch(c, "build kernels");
 }
@@ -693,7 +708,42 @@ rtbvh_status rtbvh_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces)
     return rtbvh_synchronize(c);
 }
 
+// RTBVH_FLAG_GRAPH: Graphics.cpp:56 rebuilds and traces every frame, ~20 launches and memsets
+// of little work each on the reference's own meshes; the frame is captured once into a
+// hipGraph and replayed.  A plain frame runs first so that every buffer exists before the
+// capture; kernel arguments (camera, sizes, buffers) are baked into the graph, hence the key
+// and the drop on set_scene / set_camera.
+static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
+    const uint64_t key[4] = {W, H, bounces, (uint64_t)c->cfg.flags | (uint64_t)c->T << 32};
+    if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
+        drop_graph(c);
+        rtbvh_status st = rtbvh_build_async(c);
+        if (!st) st = rtbvh_trace_async(c, W, H, bounces);
+        if (!st) st = rtbvh_synchronize(c);
+        if (st) return st;
+        HIPC(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        c->capturing = true;
+        st = rtbvh_build_async(c);
+        if (!st) st = rtbvh_trace_async(c, W, H, bounces);
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(c->stream, &g);
+        c->capturing = false;
+        if (st || e != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            return st ? st : fail(c, RTBVH_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+        }
+        c->graph = g;
+        HIPC(c, hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
+        memcpy(c->graph_key, key, sizeof(key));
+    }
+    HIPC(c, hipGraphLaunch(c->graph_exec, c->stream));
+    HIPC(c, hipEventRecord(c->ev_built, c->stream));
+    return rtbvh_synchronize(c);
+}
+
 rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    if (c->cfg.flags & RTBVH_FLAG_GRAPH) return compute_graph(c, W, H, bounces);
     rtbvh_status st = rtbvh_build_async(c);
     if (st) return st;
     st = rtbvh_trace_async(c, W, H, bounces);

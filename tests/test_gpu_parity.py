@@ -633,6 +633,25 @@ def test_frames_in_flight_match_one_at_a_time(nranks):
             c.trace_band_async(W, H, 1, r, nranks, bufs[0].data_ptr(), stream_ptr=torch.cuda.Stream().cuda_stream)
 
 
+def test_compute_bvh_graph_replays_the_frame():
+    """RTBVH_FLAG_GRAPH: compute_bvh captures build + trace into a hipGraph and replays it; the
+    frames and trees equal a plain context's, across replays and the re-captures that a new
+    frame size, bounce count or camera forces."""
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    with rt.Context(device=0) as plain, rt.Context(device=0, flags=rt.FLAG_GRAPH) as g:
+        for c in (plain, g):
+            c.set_scene(s)
+        for W, H, b, cam in [(320, 240, 1, (320, 240)), (320, 240, 1, (320, 240)), (400, 200, 2, (400, 200)),
+                             (400, 200, 2, (640, 480)), (400, 200, 2, (640, 480))]:
+            wvp, wv = rt.camera_reference(*cam)
+            for c in (plain, g):
+                c.set_camera(wvp, wv)
+                c.compute_bvh(W, H, b)
+            np.testing.assert_array_equal(g.read_framebuffer(), plain.read_framebuffer())
+            np.testing.assert_array_equal(g.read_bvh()["bb_min"], plain.read_bvh()["bb_min"])
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_band_split_reassembles_full_frame(nranks):
     import torch
