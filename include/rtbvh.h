@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RTBVH_ABI_VERSION 2
+#define RTBVH_ABI_VERSION 3
 
 typedef enum {
     RTBVH_OK = 0,
@@ -35,7 +35,12 @@ typedef enum {
     RTBVH_ERR_HIP = 2,            /* a HIP runtime call failed (message has the HIP error) */
     RTBVH_ERR_OOM = 3,
     RTBVH_ERR_NOT_READY = 4,      /* e.g. trace before build, build before set_scene */
-    RTBVH_ERR_STACK_OVERFLOW = 5, /* a traversal stack overflowed (never for a clz64 tree) */
+    RTBVH_ERR_STACK_OVERFLOW = 5, /* rays of a trace hit rtbvh_config.stack_limit (or a cyclic CPUTests-delta
+                                     tree tripped the walk-length guard): the frame is complete, those rays
+                                     ended with the best hit found so far; returned by the synchronising call
+                                     after the trace (rtbvh_trace, rtbvh_compute_bvh, rtbvh_trace_tiles,
+                                     rtbvh_synchronize), once per new overflow.  The reference's 32-entry
+                                     stack is unchecked (RayTraceTraversal.hlsl:9,115,187). */
     RTBVH_ERR_IO = 6,             /* scene file could not be read / parsed */
     RTBVH_ERR_NO_DEVICE = 7,
     RTBVH_ERR_COMM = 8            /* RCCL missing or an RCCL call failed (message has the RCCL error) */
@@ -120,10 +125,14 @@ enum {
     RTBVH_FLAG_WIDE_BVH = 1u << 7,        /* trace: walk the node records 4-wide (a node's four grandchild
                                              boxes share one 128-B line), keeping the lexicographic
                                              (t, leaf) minimum as NEAREST_FIRST does */
+    RTBVH_FLAG_AUTO_WALK = 1u << 8,       /* choose the walks by scene size, ignoring the four walk flags above:
+                                             up to 65536 triangles the reference-order kernels (exact by
+                                             construction; the fastest on the reference's own meshes), above
+                                             that NEAREST_FIRST | PACKET_PRIMARY | REFILL_BOUNCE | WIDE_BVH
+                                             (identical frames whenever containment holds: check a scene
+                                             once with rtbvh_verify_walk) */
     RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
                                               build instead of the one-workgroup build (same output) */
-    /* bits 8..15: kernel variant for A/B measurement (0 = default, 1 = first version) */
-    RTBVH_FLAG_VARIANT_SHIFT = 8,
     /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n
        independent primary -> bounce kernel chains on n streams (same results) */
     RTBVH_FLAG_SPLIT_SHIFT = 17,
@@ -141,6 +150,11 @@ typedef struct {
     float scene_bb_min[3];   /* MORTON_HLSL only: cbuffer sceneBBMin (Graphics.cpp:529 uses -700) */
     float scene_bb_max[3];   /* MORTON_HLSL only: cbuffer sceneBBMax (Graphics.cpp:528 uses +700) */
     void* stream;            /* hipStream_t to use, or NULL: the context creates its own */
+    uint32_t stack_limit;    /* traversal stack entries a ray may use, 0 = the compiled capacity (66 binary,
+                                100 4-wide; a clz64 tree never needs more); 32 = the reference's stack
+                                (RayTraceTraversal.hlsl:9): rays that would overflow it end early and the
+                                trace reports RTBVH_ERR_STACK_OVERFLOW */
+    uint32_t reserved;       /* must be 0 */
 } rtbvh_config;
 
 typedef struct {
@@ -162,6 +176,9 @@ typedef struct {
     /* ... and the walk length of the bounce rays (loop iterations per ray): the longest,
      * and a histogram, [k] = rays of floor(log2(iterations)) == k */
     uint64_t trav_max_steps, trav_steps_log2[32];
+    uint64_t graph_captures;   /* RTBVH_FLAG_GRAPH: frames captured so far (a replay captures nothing) */
+    uint32_t walk_flags;       /* the walk flags the next trace uses (after RTBVH_FLAG_AUTO_WALK) */
+    uint32_t reserved;
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 
@@ -211,6 +228,13 @@ rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* ctx, uint32_t width, uint32_t height, 
 rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces,
                                     uint32_t rank, uint32_t nranks, float* dev_out, void* stream);
 uint32_t rtbvh_band_rows(uint32_t height, uint32_t rank, uint32_t nranks);
+/* The per-scene identity check of a fast walk: traces the W x H frame in the reference order
+ * (the exact findCollision DFS) and with the context's walk flags, compares the two on the device
+ * and stores the number of pixels whose RGBA bits differ (0: the fast walk renders this frame
+ * exactly as the reference order).  Synchronous; afterwards the context holds the frame of its
+ * own walks, as after rtbvh_trace. */
+rtbvh_status rtbvh_verify_walk(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces,
+                               uint64_t* differing_pixels);
 /* The frame from the ranks' compact band buffers, all on this device: buffer r (rank r's
  * rtbvh_trace_band_async output) starts stride_rows * W * 4 floats after buffer r-1
  * (stride_rows >= rtbvh_band_rows(H, 0, nranks)); writes W*H*4 floats to dev_frame.

@@ -22,7 +22,7 @@ FLAG_PACKET_PRIMARY = 1 << 5
 FLAG_REFILL_BOUNCE = 1 << 6
 FLAG_WIDE_BVH = 1 << 7
 FLAG_MULTI_KERNEL_BUILD = 1 << 16
-FLAG_VARIANT_SHIFT = 8
+FLAG_AUTO_WALK = 1 << 8   # walks chosen by scene size (include/rtbvh.h)
 FLAG_SPLIT_SHIFT = 17   # trace chains: (n << FLAG_SPLIT_SHIFT), 0 = automatic
 FLAG_GRAPH = 1 << 20    # compute_bvh replays a captured hipGraph of the frame
 
@@ -30,7 +30,7 @@ FLAG_GRAPH = 1 << 20    # compute_bvh replays a captured hipGraph of the frame
 EXPORTS = [
     "rtbvh_config_default", "rtbvh_create", "rtbvh_destroy", "rtbvh_last_error", "rtbvh_abi_version",
     "rtbvh_set_scene", "rtbvh_set_camera", "rtbvh_build", "rtbvh_build_async", "rtbvh_trace",
-    "rtbvh_trace_async", "rtbvh_compute_bvh", "rtbvh_trace_band_async", "rtbvh_band_rows",
+    "rtbvh_trace_async", "rtbvh_compute_bvh", "rtbvh_trace_band_async", "rtbvh_band_rows", "rtbvh_verify_walk",
     "rtbvh_synchronize", "rtbvh_read_framebuffer", "rtbvh_read_intensity", "rtbvh_framebuffer_device",
     "rtbvh_read_bvh", "rtbvh_read_wide", "rtbvh_read_qnodes", "rtbvh_read_morton", "rtbvh_read_sorted", "rtbvh_read_rays", "rtbvh_get_stats",
     "rtbvh_reset_stats", "rtbvh_set_flags",
@@ -55,7 +55,8 @@ assert NODE_DTYPE.itemsize == 44 and MATERIAL_DTYPE.itemsize == 68
 class Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("morton_mode", ctypes.c_uint32), ("delta_mode", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("scene_bb_min", ctypes.c_float * 3),
-                ("scene_bb_max", ctypes.c_float * 3), ("stream", ctypes.c_void_p)]
+                ("scene_bb_max", ctypes.c_float * 3), ("stream", ctypes.c_void_p),
+                ("stack_limit", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class Texture(ctypes.Structure):
@@ -72,7 +73,8 @@ class Stats(ctypes.Structure):
                 ("timed_traces", ctypes.c_uint32), ("ms_build", ctypes.c_float), ("ms_trace", ctypes.c_float),
                 ("ms_stage", ctypes.c_float * 8), ("trav_wave_steps", ctypes.c_uint64),
                 ("trav_mixed_steps", ctypes.c_uint64), ("trav_active_lanes", ctypes.c_uint64),
-                ("trav_max_steps", ctypes.c_uint64), ("trav_steps_log2", ctypes.c_uint64 * 32)]
+                ("trav_max_steps", ctypes.c_uint64), ("trav_steps_log2", ctypes.c_uint64 * 32),
+                ("graph_captures", ctypes.c_uint64), ("walk_flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
     def as_dict(self) -> dict:
         d = {}
@@ -123,6 +125,7 @@ def lib() -> ctypes.CDLL:
         "rtbvh_compute_bvh": (i32, [vp, u32, u32, u32]),
         "rtbvh_trace_band_async": (i32, [vp, u32, u32, u32, u32, u32, vp, vp]),
         "rtbvh_band_rows": (u32, [u32, u32, u32]),
+        "rtbvh_verify_walk": (i32, [vp, u32, u32, u32, ctypes.POINTER(u64)]),
         "rtbvh_assemble_bands": (i32, [vp, u32, u32, u32, vp, u32, vp, vp]),
         "rtbvh_comm_unique_id": (i32, [vp]),
         "rtbvh_comm_init": (i32, [vp, u32, u32, vp, ctypes.POINTER(vp)]),

@@ -52,6 +52,10 @@ struct rtbvh_ctx {
     float* d_refr_rec = nullptr;             //   RayPresent records, 14 floats per traced pixel
     size_t cap_rec = 0, rec_P = 0;           // record capacity; pixels of the last records trace
     uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr;
+    unsigned long long* d_ovf = nullptr;     // stack overflows + guard trips of every trace (never reset)
+    unsigned long long* h_ovf = nullptr;     // pinned: a snapshot of *d_ovf copied at the end of each trace,
+                                             //   one word per slot; ovf_seen: the value last reported
+    unsigned long long ovf_seen = 0;
     float* d_bounds = nullptr;
     float* d_rootbox = nullptr;
     SortResult sorted{nullptr, nullptr};
@@ -102,8 +106,14 @@ struct rtbvh_ctx {
     // RTBVH_FLAG_GRAPH: the captured frame (build + trace) of rtbvh_compute_bvh and its key
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
-    uint64_t graph_key[4] = {};
+    uint64_t graph_key[5] = {};
     bool capturing = false;   // enqueueing into a capture: no event records
+    uint64_t graph_captures = 0;
+    // host-side trace state of the captured frame, restored after every replay
+    struct TraceState {
+        uint32_t W, H, bounces, nsplit;
+        size_t rec_P;
+    } graph_state{};
 };
 
 namespace {
@@ -245,7 +255,6 @@ BuildArgs build_args(rtbvh_ctx* c) {
 TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks, float4* color, float* inten) {
     TraceArgs a{};
     a.inner = c->d_rec;
-    a.inner4 = c->d_rec;
     a.leaf = c->d_leaf;
     a.qnode = c->d_qnode;
     a.tclip = c->d_tclip;
@@ -268,7 +277,48 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.color = color;
     a.intensity = inten;
     a.counters = c->d_counters;
+    a.overflow = c->d_ovf;
+    const uint32_t lim = c->cfg.stack_limit;
+    a.stack_limit = lim && lim < (uint32_t)STACK_SIZE ? (int)lim : STACK_SIZE;
+    a.stack_limit4 = lim && lim < (uint32_t)STACK4 ? (int)lim : STACK4;
     return a;
+}
+
+// The walks of a trace (include/rtbvh.h RTBVH_FLAG_*).  RTBVH_FLAG_AUTO_WALK: the
+// reference-order kernels (the exact findCollision DFS) up to AUTO_WALK_MAX_TRIS triangles,
+// where they are the fastest (C2/C3: Image_Test.obj, Test.obj), and the 4-wide nearest-first
+// walks above (C5: 2.4x the reference order).
+constexpr uint32_t AUTO_WALK_MAX_TRIS = 1u << 16;
+constexpr uint32_t WALK_FLAGS =
+    RTBVH_FLAG_NEAREST_FIRST | RTBVH_FLAG_PACKET_PRIMARY | RTBVH_FLAG_REFILL_BOUNCE | RTBVH_FLAG_WIDE_BVH;
+uint32_t effective_flags(const rtbvh_ctx* c) {
+    uint32_t f = c->cfg.flags;
+    if (f & RTBVH_FLAG_AUTO_WALK) {
+        f &= ~WALK_FLAGS;
+        if (c->T > AUTO_WALK_MAX_TRIS) f |= WALK_FLAGS;
+    }
+    return f;
+}
+struct Walks {
+    PrimaryKind primary;
+    bool refill;        // bounce passes as persistent refill traversal + shading kernel
+    BounceWalk bounce;  // refill walk
+    bool nearest;       // one-ray-per-lane bounce kernel: nearest-first
+    bool sort;          // coherence sort of the bounce queue
+};
+Walks choose_walks(uint32_t f) {
+    Walks w{};
+    const bool nearest = (f & RTBVH_FLAG_NEAREST_FIRST) != 0, wide = (f & RTBVH_FLAG_WIDE_BVH) != 0;
+    const bool packet = (f & RTBVH_FLAG_PACKET_PRIMARY) != 0;
+    w.primary = packet ? (wide ? PrimaryKind::PACKET_WIDE : nearest ? PrimaryKind::PACKET_NEAREST
+                                                                    : PrimaryKind::PACKET_REFERENCE)
+                       : (nearest ? PrimaryKind::LANE_NEAREST : PrimaryKind::LANE_REFERENCE);
+    // the ray records are written by k_primary and k_bounce_shade: the split bounce path
+    w.refill = (f & (RTBVH_FLAG_REFILL_BOUNCE | RTBVH_FLAG_WIDE_BVH | RTBVH_FLAG_REFRACT_RECORDS)) != 0;
+    w.bounce = wide ? BounceWalk::WIDE_QUANTIZED : nearest ? BounceWalk::NEAREST : BounceWalk::REFERENCE;
+    w.nearest = nearest;
+    w.sort = (f & RTBVH_FLAG_SORT_BOUNCE) != 0;
+    return w;
 }
 
 // RCCL, resolved at run time: the process's librccl.so.1 if one is already loaded (e.g.
@@ -341,41 +391,16 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     a.counters = c->d_counters + 64 * slot;
     HIPC(c, hipMemsetAsync(a.counters, 0, 64 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
-    // kernel variant: 0 reference order, 1 nearest-first, 2 first version (A/B)
-    int variant = (c->cfg.flags & RTBVH_FLAG_NEAREST_FIRST) ? 1 : 0;
-    const uint32_t vsel = (c->cfg.flags >> RTBVH_FLAG_VARIANT_SHIFT) & 255u;
-    if (vsel == 1) variant = 2;
-    int pvariant = variant;   // primary kernel: 2 = wave packets
-
-    const bool sort = (c->cfg.flags & RTBVH_FLAG_SORT_BOUNCE) != 0;
-    const bool wide = (c->cfg.flags & RTBVH_FLAG_WIDE_BVH) != 0 && vsel != 1;
-    const bool records = (c->cfg.flags & RTBVH_FLAG_REFRACT_RECORDS) != 0;
+    const uint32_t flags = effective_flags(c);
+    const Walks wk = choose_walks(flags);
+    const bool sort = wk.sort, refill = wk.refill;
+    const bool records = (flags & RTBVH_FLAG_REFRACT_RECORDS) != 0;
     if (records && slot) return fail(c, RTBVH_ERR_INVALID_ARG, "ray records are traced on the context stream only");
-    // the records are written by k_primary and k_bounce_shade: the split bounce path
-    const bool refill = ((c->cfg.flags & RTBVH_FLAG_REFILL_BOUNCE) != 0 || wide || records) && vsel != 1;
-    // A/B of the refill kernel's LDS stack depth: variant 2 -> none, 3 -> 8, 4 -> 20, else 16
-    const int lds_stack = vsel == 2 ? 0 : vsel == 3 ? 8 : vsel == 4 ? 20 : 16;
-    // ... and of the refill policy (idle lanes that trigger it, rays per atomic claim):
-    // 5 -> (16, none), 6 -> (8, 128), 7 -> (16, 128), 8 -> (8, 256), 9 -> (16, 64), 10 -> (4, 128);
-    // default (32, none)
-    const uint32_t refill_min = vsel == 8 ? 8 : vsel == 9 ? 16 : vsel == 10 ? 4 : 0;
-    uint32_t chunk = vsel == 10 ? 128 : vsel == 8 ? 256 : vsel == 9 ? 64 : 0;
-    if (vsel == 13) chunk = 22u << 24;   // A/B: +22 KB LDS per block -> 4 blocks (4 waves/SIMD) per CU
-    if (vsel == 14) chunk = 9u << 24;    // A/B: +9 KB -> 6 blocks per CU
-    // A/B of postponed leaves in the 4-wide bounce walk: variant 15 -> batch 16, 2 -> ... (see below)
-    const uint32_t leaf_batch = vsel == 15 ? 16 : vsel == 5 ? 8 : vsel == 6 ? 24 : vsel == 7 ? 32 : 16;
-    // 4-wide bounce walk: quantized nodes (mode 4; C5 bounce traversal 3.45 -> 3.18 ms), the
-    // exact record pairs with variant 17 (mode 2, A/B)
-    const int bmode = wide ? ((vsel == 15 || (vsel >= 5 && vsel <= 7)) ? 3 : vsel == 17 ? 2 : 4)
-                           : (variant == 1 ? 1 : 0);
-    if ((c->cfg.flags & RTBVH_FLAG_PACKET_PRIMARY) && vsel != 1)
-        pvariant = wide ? (vsel == 11 ? 6 : vsel == 12 ? 7 : 5) : (variant == 1 ? 4 : 3);
     const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
     // persistent grid of the bounce walk: 2048 blocks (8 waves/SIMD), 1024 for a shard of
     // < 4M pixels -- with frames in flight the next frame's primary blocks then share the CUs
-    // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame); A/B: variant 19
-    // -> 1024, 21 -> 1536, 27 -> 2048
-    const uint32_t tblocks = vsel == 19 ? 1024 : vsel == 21 ? 1536 : vsel == 27 ? 2048 : (P < (1u << 22) ? 1024 : 2048);
+    // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame)
+    const uint32_t tblocks = P < (1u << 22) ? 1024 : 2048;
     if (records) {
         if (c->cap_rec < P) {
             HIPC(c, dalloc(c->d_refl_rec, 14 * (size_t)P));
@@ -411,7 +436,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         float2* hit = b ? c->d_hits[b] : c->d_hit;
         uint32_t* qc = c->d_qcount + 32 * b;
         const bool tg = timing && g == 0;   // stage events: chain 0's kernels
-        launch_primary(ag, q[0], &qc[0], count, bounces > 0, pvariant, sg);
+        launch_primary(ag, q[0], &qc[0], count, bounces > 0, wk.primary, sg);
         if (tg) HIPC(c, hipEventRecord(ev[1], sg));
         for (uint32_t b = 0; b < bounces; b++) {
             const uint32_t* perm = nullptr;
@@ -422,20 +447,21 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             }
             if (refill) {
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[3], sg));
-                launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, bmode, hit, &qc[16 + b], lds_stack,
-                                       refill_min, chunk, leaf_batch, tblocks, sg);
+                launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, wk.bounce, hit, &qc[16 + b], tblocks, sg);
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[4], sg));
                 launch_bounce_shade(ag, q[b & 1], &qc[b], hit, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
                                     Pg, sg);
             } else
                 launch_bounce(ag, q[b & 1], &qc[b], perm, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
-                              variant, sg);
+                              wk.nearest, sg);
         }
         if (g) {
             HIPC(c, hipEventRecord(c->ev_join[g], sg));
             HIPC(c, hipStreamWaitEvent(s, c->ev_join[g], 0));
         }
     }
+    // a snapshot of the overflow word for this stream's slot (rtbvh_synchronize reports a change)
+    HIPC(c, hipMemcpyAsync(c->h_ovf + slot, c->d_ovf, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     c->nsplit = nsplit;
     c->last_slot = slot;
     if (timing) {
@@ -479,7 +505,7 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
     if (!c) return fail(nullptr, RTBVH_ERR_OOM, "host allocation failed");
     if (cfg) c->cfg = *cfg;
     else rtbvh_config_default(&c->cfg);
-    if (c->cfg.morton_mode > 1 || c->cfg.delta_mode > 1) {
+    if (c->cfg.morton_mode > 1 || c->cfg.delta_mode > 1 || c->cfg.reserved != 0) {
         delete c;
         return fail(nullptr, RTBVH_ERR_INVALID_ARG, "bad morton/delta mode");
     }
@@ -514,6 +540,14 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
         rtbvh_destroy(c);
         return fail(nullptr, RTBVH_ERR_HIP, "hipEventCreate failed");
     }
+    if (hipMalloc((void**)&c->d_ovf, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_ovf, 0, sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_ovf, sizeof(unsigned long long) * rtbvh_ctx::MAXSPLIT, hipHostMallocDefault) !=
+            hipSuccess) {
+        rtbvh_destroy(c);
+        return fail(nullptr, RTBVH_ERR_OOM, "overflow counter allocation failed");
+    }
+    memset(c->h_ovf, 0, sizeof(unsigned long long) * rtbvh_ctx::MAXSPLIT);
     *out = c;
     return RTBVH_OK;
 }
@@ -548,6 +582,8 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);
     dfree(c->d_texels); dfree(c->d_texinfo); dfree(c->d_srgb);
     dfree(c->d_counters);
+    dfree(c->d_ovf);
+    if (c->h_ovf) (void)hipHostFree(c->h_ovf);
     for (auto& row : c->evb)
         for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
@@ -631,10 +667,15 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
 
 rtbvh_status rtbvh_set_camera(rtbvh_ctx* c, const float wvp[16], const float wv[16]) {
     if (!c || !wvp || !wv) return RTBVH_ERR_INVALID_ARG;
+    // Graphics::onUpdate writes the same matrices every frame (Graphics.cpp:44-53): a
+    // captured frame (RTBVH_FLAG_GRAPH), whose kernels hold the camera, is kept unless
+    // the matrices change
+    if (c->have_camera && memcmp(c->wvp, wvp, sizeof(c->wvp)) == 0 && memcmp(c->wv, wv, sizeof(c->wv)) == 0)
+        return RTBVH_OK;
     memcpy(c->wvp, wvp, sizeof(c->wvp));
     memcpy(c->wv, wv, sizeof(c->wv));
     c->have_camera = true;
-    drop_graph(c);   // the camera is baked into a captured frame
+    drop_graph(c);
     return RTBVH_OK;
 }
 
@@ -714,13 +755,14 @@ rtbvh_status rtbvh_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces)
 // capture; kernel arguments (camera, sizes, buffers) are baked into the graph, hence the key
 // and the drop on set_scene / set_camera.
 static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
-    const uint64_t key[4] = {W, H, bounces, (uint64_t)c->cfg.flags | (uint64_t)c->T << 32};
+    const uint64_t key[5] = {W, H, bounces, (uint64_t)c->cfg.flags | (uint64_t)c->T << 32,
+                             (uint64_t)c->slots_used | (uint64_t)c->cfg.stack_limit << 1};
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
         drop_graph(c);
         rtbvh_status st = rtbvh_build_async(c);
         if (!st) st = rtbvh_trace_async(c, W, H, bounces);
         if (!st) st = rtbvh_synchronize(c);
-        if (st) return st;
+        if (st && st != RTBVH_ERR_STACK_OVERFLOW) return st;
         HIPC(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         c->capturing = true;
         st = rtbvh_build_async(c);
@@ -735,9 +777,30 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
         c->graph = g;
         HIPC(c, hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
         memcpy(c->graph_key, key, sizeof(key));
+        c->graph_state = rtbvh_ctx::TraceState{c->W, c->H, c->bounces, c->nsplit, c->rec_P};
+        c->graph_captures++;
     }
+    // the replayed build rewrites the BVH (and a split trace the slot queues): after the
+    // frames in flight on caller streams, as rtbvh_build_async
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)
+        if (c->slot_busy[k]) {
+            HIPC(c, hipStreamWaitEvent(c->stream, c->ev_slot[k], 0));
+            c->slot_busy[k] = false;
+        }
     HIPC(c, hipGraphLaunch(c->graph_exec, c->stream));
     HIPC(c, hipEventRecord(c->ev_built, c->stream));
+    // the host-side state of the captured trace (a trace in between may have changed it)
+    const rtbvh_ctx::TraceState& g = c->graph_state;
+    c->W = g.W;
+    c->H = g.H;
+    c->bounces = g.bounces;
+    c->nsplit = g.nsplit;
+    c->rec_P = g.rec_P;
+    c->rank = 0;
+    c->nranks = 1;
+    c->last_slot = 0;
+    c->traced = c->built = true;
+    c->frame_here = c->intensity_here = true;
     return rtbvh_synchronize(c);
 }
 
@@ -748,6 +811,45 @@ rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
     if (st) return st;
     st = rtbvh_trace_async(c, W, H, bounces);
     if (st) return st;
+    return rtbvh_synchronize(c);
+}
+
+// The identity check of a fast walk (DESIGN.md "Traversal orders"): the frame in the
+// reference order (the exact findCollision DFS, RayTraceTraversal.hlsl:106-193) into a
+// scratch buffer, then the frame with the context's walks into the framebuffer, compared
+// on the device.  Leaves the context as rtbvh_trace with its own flags does.
+rtbvh_status rtbvh_verify_walk(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint64_t* differing) {
+    if (!c || !differing) return RTBVH_ERR_INVALID_ARG;
+    if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "verify_walk before build");
+    if (W == 0 || H == 0 || bounces > 14) return fail(c, RTBVH_ERR_INVALID_ARG, "bad trace dimensions");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    rtbvh_status st = ensure_trace_capacity(c, (size_t)W * H);
+    if (st) return st;
+    const size_t n = (size_t)W * H;
+    float4* ref = nullptr;
+    unsigned long long* d_diff = nullptr;
+    HIPC(c, hipMallocAsync((void**)&ref, n * sizeof(float4) + 256, c->stream));
+    d_diff = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ref) + n * sizeof(float4));
+    const uint32_t saved = c->cfg.flags;
+    c->cfg.flags = saved & ~(WALK_FLAGS | RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_REFRACT_RECORDS);
+    st = enqueue_trace(c, W, H, bounces, 0, 1, ref, nullptr, c->stream);
+    c->cfg.flags = saved & ~RTBVH_FLAG_REFRACT_RECORDS;
+    if (!st) st = enqueue_trace(c, W, H, bounces, 0, 1, c->d_color, c->d_intensity, c->stream);
+    c->cfg.flags = saved;
+    unsigned long long diff = 0;
+    if (!st) {
+        hipError_t e = hipMemsetAsync(d_diff, 0, sizeof(unsigned long long), c->stream);
+        if (e == hipSuccess) {
+            launch_count_diff(ref, c->d_color, n, d_diff, c->stream);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&diff, d_diff, sizeof(diff), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) st = fail(c, RTBVH_ERR_HIP, std::string("verify_walk: ") + hipGetErrorString(e));
+    }
+    (void)hipFreeAsync(ref, c->stream);
+    if (st) return st;
+    *differing = diff;
     return rtbvh_synchronize(c);
 }
 
@@ -870,8 +972,7 @@ rtbvh_status rtbvh_trace_tiles(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
         if (st) return st;
     }
     c->frame_here = rank == 0;
-    HIPC(c, hipStreamSynchronize(c->stream));
-    return RTBVH_OK;
+    return rtbvh_synchronize(c);
 }
 
 rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
@@ -879,6 +980,19 @@ rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
     HIPC(c, hipStreamSynchronize(c->stream));
     for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // and the frames in flight on caller streams
         if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
+    // each trace ends by copying the never-reset overflow word into its slot's pinned word
+    unsigned long long ovf = c->ovf_seen;
+    for (uint32_t k = 0; k < rtbvh_ctx::MAXSPLIT; k++)
+        if (c->h_ovf[k] > ovf) ovf = c->h_ovf[k];
+    if (ovf > c->ovf_seen) {
+        const unsigned long long n = ovf - c->ovf_seen;
+        c->ovf_seen = ovf;
+        return fail(c, RTBVH_ERR_STACK_OVERFLOW,
+                    "traversal stack overflow: " + std::to_string(n) +
+                        " ray(s) ended early with the best hit found so far (stack limit " +
+                        std::to_string(c->cfg.stack_limit ? c->cfg.stack_limit : (uint32_t)STACK_SIZE) +
+                        " entries; the reference's 32-entry stack is unchecked, RayTraceTraversal.hlsl:9,115)");
+    }
     return RTBVH_OK;
 }
 
@@ -1051,6 +1165,8 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         out->trav_mixed_steps = cnt[11];
         out->trav_active_lanes = cnt[12];
     }
+    out->graph_captures = c->graph_captures;
+    out->walk_flags = effective_flags(c) & WALK_FLAGS;
     return RTBVH_OK;
 }
 

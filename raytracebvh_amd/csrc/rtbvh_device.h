@@ -33,7 +33,8 @@ namespace rtbvh {
 
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t INVALID = 0xFFFFFFFFu;
-constexpr int STACK_SIZE = 66;   // >= 64 levels of a clz64 Karras tree + sentinel
+constexpr int STACK_SIZE = 66;   // binary walks: >= 64 levels of a clz64 Karras tree + sentinel
+constexpr int STACK4 = 100;      // 4-wide walks: <= 3 pushes per level of a <= 32-level 4-wide tree
 
 // 64-byte child-pair record of internal node k (boxes of both children, then ids)
 struct alignas(64) Inner {

@@ -72,7 +72,6 @@ void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t 
 // ---- trace (trace.hip) ------------------------------------------------------
 struct TraceArgs {
     const Inner* inner;       // node records in slots (BuildArgs::rec); the 4-wide walks read the same array
-    const Inner* inner4;      // == inner
     const float4* leaf;       // [4T] sorted leaf records (see build.hip)
     const float4* tclip;      // [3T] clip-space triangles in triangle order (hit shading)
     const float* verts;       // rtbvh_vertex AoS, 8 floats each
@@ -88,26 +87,32 @@ struct TraceArgs {
     Mat4 wv;
     float4* color;            // output pixels (compacted band rows when nranks > 1)
     float* intensity;         // optional, same indexing as color
-    unsigned long long* counters;   // 8 x u64: primary, bounce, int visits, leaf visits, hits, tex hits, overflow, -
+    unsigned long long* counters;   // [64] per trace: see flush_counts (trace.hip) and rtbvh_get_stats
+    unsigned long long* overflow;   // stack overflows / guard trips, accumulated over every trace (never reset)
+    int stack_limit, stack_limit4;  // stack entries the binary / 4-wide walks may use (<= STACK_SIZE / STACK4)
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)
 };
-// traversal kernel variants (A/B switch; DESIGN.md "Traversal")
-// variant: see RTBVH_FLAG_VARIANT_SHIFT in include/rtbvh.h (0 = default)
-void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, int variant, hipStream_t s);
+// primary-ray walks (trace.hip k_primary): per lane in reference order / nearest-first, wave
+// packets in reference order / nearest-first, 4-wide wave packets (axis-parallel box test)
+enum class PrimaryKind { LANE_REFERENCE, LANE_NEAREST, PACKET_REFERENCE, PACKET_NEAREST, PACKET_WIDE };
+// bounce walks of the persistent refill kernel (k_bounce_trav)
+enum class BounceWalk { REFERENCE, NEAREST, WIDE_QUANTIZED };
+void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, PrimaryKind kind,
+                    hipStream_t s);
+// one ray per lane bounce pass (reference order or nearest-first), shading included
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
-                   uint32_t* qout_count, bool count, bool emit, int variant, hipStream_t s);
+                   uint32_t* qout_count, bool count, bool emit, bool nearest, hipStream_t s);
 // bounce pass as persistent refill traversal (hit records) + shading kernel; `next` is a
-// zeroed work counter; mode 0 reference order, 1 nearest-first, 2 nearest-first 4-wide,
-// 3 = 2 with postponed leaves (leaf_batch parked leaves start a leaf phase);
-// lds_stack = stack entries kept in LDS (0, 8, 16, 20); refill_min = idle lanes that trigger a
-// refill (0: default); chunk = rays one work-counter atomic claims for the wave (0: as many as idle)
+// zeroed work counter; `blocks` persistent workgroups (0: 2048)
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
-                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, uint32_t blocks, hipStream_t s);
+                            bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
+                            hipStream_t s);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
+// *diff += the number of the n float4 pixels of a and b whose bits differ
+void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long long* diff, hipStream_t s);
 // frame from per-rank compact band buffers (stride_rows rows apart), see rtbvh_assemble_bands
 void launch_assemble(const float4* bands, uint32_t stride_rows, uint32_t W, uint32_t H, uint32_t nranks,
                      float4* frame, hipStream_t s);

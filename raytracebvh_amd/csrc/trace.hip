@@ -17,9 +17,15 @@
 //  * nearest-first (RTBVH_FLAG_NEAREST_FIRST): the nearer child first, with the
 //    lexicographic (t, leaf index) minimum kept, which is what the left-first DFS
 //    returns whenever box/triangle rounding is consistent.
-// A/B-measured alternatives that lost (LDS stacks, while-while loops, leaf
-// batching) are recorded in DESIGN.md; the kept loop is a do-while over a
-// scratch stack whose top lives in a register.
+// The walks that lost their A/B measurements are not compiled here.
+//
+// Stack limit: the reference keeps a 32-entry stack and never checks it
+// (RayTraceTraversal.hlsl:9,115,187).  Every walk here checks its own stack against
+// a run-time limit (TraceArgs::stack_limit, <= the compiled capacity); a ray that would
+// overflow ends with the best hit found so far, counts into counters[8] (the last
+// trace's stats) and into *overflow (never reset: the API turns a change of it into
+// RTBVH_ERR_STACK_OVERFLOW).  The walk-length guard (2T + 2 steps, only a cyclic tree
+// from the CPUTests delta can trip it) counts the same way.
 #include "rtbvh_internal.h"
 
 namespace rtbvh {
@@ -40,7 +46,6 @@ __device__ __forceinline__ uint32_t child_slot(uint32_t id, uint32_t own, uint32
     return (id & LEAF_BIT) ? id : 2 * own + side;
 }
 __device__ __forceinline__ uint32_t root_slot(uint32_t T) { return T == 1 ? LEAF_BIT : 2 * T - 2; }
-constexpr int STACK4 = 100;   // 4-wide walks: <= 3 pushes per level of a <= 32-level tree
 
 // Make loaded values live at this point, so the compiler issues every load of a
 // record together (one memory round trip) instead of sinking some of them below
@@ -87,7 +92,7 @@ __device__ __forceinline__ bool ray_box(f3 o, f3 inv, float bx0, float by0, floa
 // ray_box on a node record's layout (rtbvh_device.h): the (x, y) of a box corner is an
 // aligned register pair, so the x and y slabs run as packed fp32 (v_pk_add_f32 /
 // v_pk_mul_f32: two IEEE operations per instruction, the roundings of the scalar form,
-// no contraction under -ffp-contract=off) -- the traversal kernels are VALU-issue-bound.
+// no contraction under -ffp-contract=off).
 __device__ __forceinline__ bool ray_box_xy(f3 o, f3 inv, f2v lo, f2v hi, float lz, float hz, bool hit, float best,
                                            float& tmin) {
     const f2v oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
@@ -103,10 +108,10 @@ __device__ __forceinline__ bool ray_box_xy(f3 o, f3 inv, f2v lo, f2v hi, float l
 // and loops `do { ... } while (stackIndex != -1)`; here the entry at the top of
 // the stack is cached in a register (`top`), so a pop hands over the next node at
 // once and refills `top` from scratch in the background.  Returns hit;
-// best_leaf = sorted leaf index.
+// best_leaf = sorted leaf index.  `limit` <= STACK_SIZE entries.
 template <bool COUNT, bool NEAREST>
 __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const float4* __restrict__ leaf, uint32_t T,
-                                         f3 o, f3 d, f3 inv, float& best, uint32_t& best_leaf, Counts& c) {
+                                         f3 o, f3 d, f3 inv, int limit, float& best, uint32_t& best_leaf, Counts& c) {
     bool hit = false;
     best = 0.f;
     best_leaf = 0;
@@ -148,7 +153,7 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
         } else {
             const bool swap = NEAREST && lh && rh && tr < tl;
             if (lh && rh) {
-                if (sp + 1 >= STACK_SIZE) {
+                if (sp + 1 >= limit) {
                     c.overflow++;
                     node = top;
                     if (--sp >= 0) top = stack[sp];
@@ -158,59 +163,6 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
                 top = swap ? cl : cr;
             }
             node = swap ? cr : (lh ? cl : cr);
-        }
-    } while (sp != -1);
-    return hit;
-}
-
-// The first version of the loop (reference order, whole stack in scratch, no top
-// cache, default occupancy), kept as an A/B variant.
-template <bool COUNT>
-__device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
-                                                       uint32_t T, f3 o, f3 d, f3 inv, float& best, uint32_t& best_leaf,
-                                                       Counts& c) {
-    bool hit = false;
-    best = 0.f;
-    best_leaf = 0;
-    uint32_t stack[STACK_SIZE];
-    int sp = 0;
-    stack[0] = INVALID;
-    uint32_t node = root_slot(T);
-    uint32_t guard = 2 * T + 2;
-    do {
-        if (--guard == 0) { c.overflow++; break; }
-        if (node & LEAF_BIT) {
-            const uint32_t j = node & ~LEAF_BIT;
-            const float4* r = leaf + 4 * (size_t)j;
-            float4 a = r[0], b = r[1];
-            float e2z = r[2].x;
-            pin(a); pin(b); pin(e2z);
-            if (COUNT) c.leaf++;
-            const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
-            if (t != -1.f && (!hit || t < best)) {
-                best = t;
-                best_leaf = j;
-                hit = true;
-            }
-            node = stack[sp--];
-            continue;
-        }
-        if (COUNT) c.internal++;
-        const v4f* r = reinterpret_cast<const v4f*>(inner + node);
-        const v4f q0 = r[0], q1 = r[1], q2 = r[2];
-        const uint4 q3 = reinterpret_cast<const uint4*>(r)[3];
-        const uint32_t cl = child_slot(q3.x, q3.z, 0), cr = child_slot(q3.y, q3.z, 1);
-        float tl, tr;
-        const bool lh = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, tl);
-        const bool rh = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, tr);
-        if (!lh && !rh) {
-            node = stack[sp--];
-        } else {
-            if (lh && rh) {
-                if (sp + 1 >= STACK_SIZE) { c.overflow++; node = stack[sp--]; continue; }
-                stack[++sp] = cr;
-            }
-            node = lh ? cl : cr;
         }
     } while (sp != -1);
     return hit;
@@ -227,21 +179,15 @@ __device__ __forceinline__ bool traverse_first_version(const Inner* __restrict__
 // order, and nothing changes its state in between), so results and per-lane visit
 // counts are identical to the per-lane DFS.  In nearest-first mode the wave takes
 // the child most of its lanes see first.
-typedef const v4f __attribute__((address_space(4))) cv4f;
-
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef const v16f __attribute__((address_space(4))) cv16f;
 
-__device__ __forceinline__ float4 sload(const float4* p) {
-    const v4f v = *(cv4f*)p;
-    return make_float4(v.x, v.y, v.z, v.w);
-}
 // the whole 64-B record in one s_load_dwordx16 (one scalar-memory round trip per step)
 __device__ __forceinline__ v16f sload16(const void* p) { return *(cv16f*)p; }
 
 template <bool COUNT, bool NEAREST>
 __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
-                                                uint32_t T, f3 o, f3 d, f3 inv, bool valid, float& best,
+                                                uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
                                                 uint32_t& best_leaf, Counts& c, uint32_t* s_st /* per wave [3*STACK_SIZE] */) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lanebit = 1ull << lane;
@@ -291,8 +237,10 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
                     const uint64_t rfirst = __ballot(lh && rh && tr < tl);
                     swap = 2 * __popcll(rfirst) > __popcll(both);
                 }
-                if (sp + 1 >= STACK_SIZE) { c.overflow++; pop = true; }
-                else {
+                if (sp + 1 >= limit) {   // the lanes of both children lose them
+                    c.overflow += ((ml | mr) & lanebit) != 0;
+                    pop = true;
+                } else {
                     // push the second child and its lanes: the old top goes to LDS, the
                     // new entry stays in SGPRs (top cache, as in the per-lane loop)
                     if (sp > 0 && lane == 0) {
@@ -330,27 +278,21 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
 // As traverse_packet, but one step reads the 128-B record pair inner4[2p], inner4[2p+1]
 // (two s_load_dwordx16 of one line): the boxes of p's four grandchildren.  Children
 // are taken left to right (the left-first DFS's order LL, LR, RL, RR).  The per-lane
-// result is the (t, leaf) minimum, as for the 4-wide bounce walk.  A/B (C5): a
-// front-to-back order (box zmin: primary rays run along +z) made the per-lane visits
-// 6% fewer but lost the compiler's wave-uniform tracking of the node id and ran 1.6x
-// slower, so there is one order.
+// result is the (t, leaf) minimum, as for the 4-wide bounce walk.  (A front-to-back
+// order lost the compiler's wave-uniform tracking of the node id: DESIGN.md §6.)
 //
-// AXIS: the rays run along d = (0, 0, 1) from z = 0 (k_primary), so inv = (inf, inf, 1)
-// and each x/y slab of ray_box_xy yields [-inf, inf] (or NaNs that fminf/fmaxf drop)
-// exactly when min < o < max, and an empty slab otherwise.  For a box whose record bit
-// (word 15, build.hip general_box) is clear -- min < max in x and y, min.z <= max.z,
-// 0 <= max.z < inf -- the test is therefore exactly
+// Axis-parallel box test: the rays run along d = (0, 0, 1) from z = 0 (k_primary), so
+// inv = (inf, inf, 1) and each x/y slab of ray_box_xy yields [-inf, inf] (or NaNs that
+// fminf/fmaxf drop) exactly when min < o < max, and an empty slab otherwise.  For a box
+// whose record bit (word 15, build.hip general_box) is clear -- min < max in x and y,
+// min.z <= max.z, 0 <= max.z < inf -- the test is therefore exactly
 //     min.x < o.x < max.x  &&  min.y < o.y < max.y  &&  (!hit || min.z <= best)
-// (denormals are kept, so min < o has the sign of min - o): five compares instead of
-// ~17 VALU operations.  A node with any bit set takes the general test.
-// AXIS 2 (default): o - min and max - o as packed differences and min(...) > 0 (a rounded
-// difference of non-NaN floats, infinities included, is > 0 exactly when the exact one
-// is): 6 VALU + 2 lane-mask ANDs per box.  AXIS 1 (A/B): five v_cmp ANDed as lane masks, 5 VALU + 5 SALU per box --
-// 11% slower (C5 primary 2.96 vs 2.67 ms): the loop's lane-mask and stack work already
-// loads the CU's one scalar unit.  AXIS 0 (A/B): the general test everywhere, 3.13 ms.
-template <bool COUNT, int AX>
+// (denormals are kept, so min < o has the sign of min - o), evaluated as o - min and
+// max - o as packed differences and min(...) > 0: 6 VALU + 2 lane-mask ANDs per box.  A
+// node with any bit set takes the general test.
+template <bool COUNT>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
-                                                 uint32_t T, f3 o, f3 d, f3 inv, bool valid, float& best,
+                                                 uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
                                                  uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*STACK4] */) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lanebit = 1ull << lane;
@@ -361,12 +303,8 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
     int sp = 0;
     uint32_t node = (T == 1) ? LEAF_BIT : 0u;
     if (mask == 0) return false;
-    float bound = INFINITY;   // AXIS: best once hit, +inf before (min.z <= bound == !hit || min.z <= best)
-    // The stack is lane 0's LDS words, one lane-0 region per push.  Measured against it
-    // (C5 primary, A/B, since removed): the stack in VGPR lanes (v_writelane/v_readlane at
-    // the scalar index sp, LDS beyond 64 entries) +3%; all lanes storing the same words (no
-    // exec region) and branch-free pushes at a running top 0% and +3%; one lane-0 region
-    // for all pushes of a node +26% (the compiler moved the walk state out of SGPRs).
+    float bound = INFINITY;   // best once hit, +inf before (min.z <= bound == !hit || min.z <= best)
+    // The stack is lane 0's LDS words, one lane-0 region per push (alternatives: DESIGN.md §6).
     uint32_t guard = 2 * T + 2;
     while (true) {
         if (--guard == 0) { c.overflow++; break; }
@@ -393,26 +331,12 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
                               __float_as_uint(B[13])};
             if (COUNT && (mask & lanebit)) c.internal++;
             uint64_t m[4];
-            if (AX == 2 && (__float_as_uint(A[15]) | __float_as_uint(B[15])) == 0) {   // wave-uniform
+            if ((__float_as_uint(A[15]) | __float_as_uint(B[15])) == 0) {   // wave-uniform
                 const f2v oxy = {o.x, o.y};
                 const auto lanes = [&](f2v lo, f2v hi, float lz) {
                     const f2v d0 = oxy - lo, d1 = hi - oxy;
                     const float m = fminf(fminf(d0.x, d0.y), fminf(d1.x, d1.y));
                     return __builtin_amdgcn_ballot_w64(m > 0.f) & __builtin_amdgcn_ballot_w64(lz <= bound);
-                };
-                m[0] = lanes(A.s01, A.s23, A[8]) & mask;
-                m[1] = lanes(A.s45, A.s67, A[10]) & mask;
-                m[2] = lanes(B.s01, B.s23, B[8]) & mask;
-                m[3] = lanes(B.s45, B.s67, B[10]) & mask;
-                if (id[1] == INVALID) m[1] = 0;
-                if (id[3] == INVALID) m[3] = 0;
-            } else if (AX == 1 && (__float_as_uint(A[15]) | __float_as_uint(B[15])) == 0) {   // wave-uniform
-                // one ballot per compare: each lowers to the v_cmp's own lane mask (an && chain
-                // would be materialised as a bool and compared again)
-                const auto lanes = [&](f2v lo, f2v hi, float lz) {
-                    return __builtin_amdgcn_ballot_w64(lo.x < o.x) & __builtin_amdgcn_ballot_w64(o.x < hi.x) &
-                           __builtin_amdgcn_ballot_w64(lo.y < o.y) & __builtin_amdgcn_ballot_w64(o.y < hi.y) &
-                           __builtin_amdgcn_ballot_w64(lz <= bound);
                 };
                 m[0] = lanes(A.s01, A.s23, A[8]) & mask;
                 m[1] = lanes(A.s45, A.s67, A[10]) & mask;
@@ -438,7 +362,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             const int first = om[0] ? 0 : om[1] ? 1 : om[2] ? 2 : om[3] ? 3 : -1;
             if (first < 0) {
                 pop = true;
-            } else if (sp + 3 > STACK4) {
+            } else if (sp + 3 > limit) {
                 c.overflow++;
                 pop = true;
             } else {
@@ -469,24 +393,13 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
     return hit;
 }
 
-// kernel variants: 0 = reference order (default), 1 = nearest-first,
-// 2 = the first version (reference order) kept for A/B
-// 3 = reference order with wave-packet primary rays, 4 = nearest-first with packets
-// 5 = 4-wide packets (left-to-right order, (t, leaf) minimum)
-template <int V> struct TV {
-    static constexpr bool NEAREST = (V == 1 || V == 4);
-    static constexpr bool PACKET = (V == 3 || V == 4 || V >= 5);
-    static constexpr bool WIDE = (V >= 5);
-    static constexpr int AXIS = V == 5 ? 2 : V == 7 ? 1 : 0;   // 6, 7: A/B forms of 5's box test
-    static constexpr int OCC = (V == 2) ? 1 : 8;   // 8 waves/SIMD => <= 64 VGPRs (A/B: -25% bounce time)
+// Primary walks: 0 per-lane reference order, 1 per-lane nearest-first,
+// 2 packet reference order, 3 packet nearest-first, 4 4-wide packet (axis-parallel test)
+template <int K> struct PrimaryWalk {
+    static constexpr bool NEAREST = (K == 1 || K == 3);
+    static constexpr bool PACKET = (K >= 2);
+    static constexpr bool WIDE = (K == 4);
 };
-
-template <bool COUNT, int V>
-__device__ __forceinline__ bool trace_ray(const Inner* __restrict__ inner, const float4* __restrict__ leaf, uint32_t T,
-                                          f3 o, f3 d, f3 inv, float& best, uint32_t& best_leaf, Counts& c) {
-    if (V == 2) return traverse_first_version<COUNT>(inner, leaf, T, o, d, inv, best, best_leaf, c);
-    return traverse<COUNT, TV<V>::NEAREST>(inner, leaf, T, o, d, inv, best, best_leaf, c);
-}
 
 struct HitInfo {
     float4 color;   // renderPixel(...) * specular
@@ -610,7 +523,7 @@ __device__ __forceinline__ uint32_t wave_append(bool active, uint32_t* counter) 
 }
 
 // counters: [base] internal visits, [base+1] leaf visits, [base+2] hits (base 2 primary,
-// 5 bounce), [8] stack overflows / guard trips, [9] textured hits
+// 5 bounce), [8] stack overflows / guard trips (also added to *overflow), [9] textured hits
 template <bool COUNT>
 __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c, uint32_t hits, uint32_t tex,
                                              int base) {
@@ -626,16 +539,20 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
             atomicAdd(&a.counters[base + 2], v[2]);
             atomicAdd(&a.counters[9], v[4]);
         }
-        if (v[3]) atomicAdd(&a.counters[8], v[3]);
+        if (v[3]) {
+            atomicAdd(&a.counters[8], v[3]);
+            atomicAdd(a.overflow, v[3]);
+        }
     }
 }
 
 // RayTraceLaunch.hlsl:6-93
-template <bool COUNT, int V>
-__global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ* __restrict__ q,
-                                                               uint32_t* __restrict__ qcount, int emit) {
-    constexpr int PST = TV<V>::WIDE ? 3 * STACK4 : 3 * STACK_SIZE;   // per-wave packet stack words
-    __shared__ uint32_t s_pst[TV<V>::PACKET ? 4 * PST : 1];
+template <bool COUNT, int K>
+__global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restrict__ q, uint32_t* __restrict__ qcount,
+                                                      int emit) {
+    using PW = PrimaryWalk<K>;
+    constexpr int PST = PW::WIDE ? 3 * STACK4 : 3 * STACK_SIZE;   // per-wave packet stack words
+    __shared__ uint32_t s_pst[PW::PACKET ? 4 * PST : 1];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t k = a.band0 + blockIdx.y * a.bstep;   // the rank's k-th band
@@ -654,16 +571,17 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
     float best = 0.f;
     uint32_t bl = 0;
     bool phit = false;
-    if (TV<V>::WIDE)     // whole wave, before any divergence
-        phit = traverse_packet4<COUNT, TV<V>::AXIS>(a.inner4, a.leaf, a.T, o, d, inv, valid, best, bl, c,
-                                                       s_pst + w * PST);
-    else if (TV<V>::PACKET)
-        phit = traverse_packet<COUNT, TV<V>::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, best, bl, c,
-                                                      s_pst + w * PST);
+    if (PW::WIDE)     // whole wave, before any divergence
+        phit = traverse_packet4<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, a.stack_limit4, best, bl, c,
+                                       s_pst + w * PST);
+    else if (PW::PACKET)
+        phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, a.stack_limit, best, bl,
+                                                   c, s_pst + w * PST);
     if (valid) {
         float4 color;
         float intensity = 0.f;
-        if (TV<V>::PACKET ? phit : trace_ray<COUNT, V>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
+        if (PW::PACKET ? phit
+                       : traverse<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, a.stack_limit, best, bl, c)) {
             hits = 1;
             const HitInfo h = shade_hit(a, bl, o, d, best);
             tex = h.textured;
@@ -704,12 +622,12 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_primary(TraceArgs a, RayQ
 }
 
 // RayTraceReflection.hlsl:6-62 over the compacted queue of live rays (in `perm`
-// order when the queue was sorted for coherence)
-template <bool COUNT, int V>
-__global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_bounce(TraceArgs a, const RayQ* __restrict__ qin,
-                                                              const uint32_t* __restrict__ qin_count,
-                                                              const uint32_t* __restrict__ perm, RayQ* __restrict__ qout,
-                                                              uint32_t* __restrict__ qout_count, int emit) {
+// order when the queue was sorted for coherence), one ray per lane
+template <bool COUNT, bool NEAREST>
+__global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __restrict__ qin,
+                                                     const uint32_t* __restrict__ qin_count,
+                                                     const uint32_t* __restrict__ perm, RayQ* __restrict__ qout,
+                                                     uint32_t* __restrict__ qout_count, int emit) {
     const uint32_t n = *qin_count;
     Counts c = {0, 0, 0};
     uint32_t hits = 0, tex = 0;
@@ -725,7 +643,7 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_bounce(TraceArgs a, const
             uint32_t bl;
             float4 col = a.color[e.idx];
             float intensity = e.intensity;
-            if (trace_ray<COUNT, V>(a.inner, a.leaf, a.T, o, d, inv, best, bl, c)) {
+            if (traverse<COUNT, NEAREST>(a.inner, a.leaf, a.T, o, d, inv, a.stack_limit, best, bl, c)) {
                 hits++;
                 const HitInfo h = shade_hit(a, bl, o, d, best);
                 tex += h.textured;
@@ -760,17 +678,11 @@ __global__ __launch_bounds__(BLOCK, TV<V>::OCC) void k_bounce(TraceArgs a, const
 // wave stays full; the finished ray's (t, leaf) goes to a hit record, and the
 // shading runs afterwards as a plain one-thread-per-ray kernel (k_bounce_shade).
 // Per-lane traversal state and visit order are exactly those of traverse().
-// default: refill when at least this many lanes are idle.  A/B on C5 (bounce pass):
+// A wave refills when at least REFILL_MIN lanes are idle.  A/B on C5 (bounce pass):
 // 4 -> 15.6 ms, 8 -> 9.2, 16 -> 5.5, 24 -> 4.13, 32 -> 3.87, 40 -> 3.84, 48 -> 3.90,
-// 64 -> 5.36; claiming chunks of 64-256 rays per atomic at 4-16 idle lanes: 4.1-4.5
+// 64 -> 5.36 (the single work counter's atomic contention below 32).
 constexpr uint32_t REFILL_MIN = 32;
 
-// one nearest-first step on the 4-wide view (inner4): the four grandchild boxes of
-// binary node `node` come from one 128-B line; hit children are visited nearest
-// first, the others pushed with their entry distance, and a popped entry whose
-// entry distance is already beyond `best` is dropped without a fetch (the box test
-// at its visit would fail: best only decreases).  The (t, leaf) minimum kept is
-// the reference DFS's answer under the same condition as nearest-first.
 __device__ __forceinline__ void sort2(float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta;
@@ -790,11 +702,20 @@ __device__ __forceinline__ uint16_t bf16_down(float t) {
 }
 __device__ __forceinline__ float bf16_up(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
-// Binary modes keep the stack entries [0, S) in LDS, [entry][lane] (a wave's lanes hit
+// Walk modes of k_bounce_trav: 0 reference order, 1 nearest-first (binary records), 2 the
+// 4-wide nearest-first walk on the quantized nodes (qn, rtbvh_device.h QNode: one 64-B node
+// per 4-wide step; a node without a finite grid falls back to its exact record pair).
+// Binary modes keep the stack entries [0, SB) in LDS, [entry][lane] (a wave's lanes hit
 // 64 distinct banks whatever their depths), and only deeper entries in scratch: the
 // all-scratch stack of 8192 resident waves (17 KB each) does not fit in L2 and PMC
-// showed ~3.6 GB of stack write-back per C5 bounce pass.
-template <bool COUNT, int MODE, int S>
+// showed ~3.6 GB of stack write-back per C5 bounce pass.  The 4-wide walk keeps
+// (node, entry distance) entries [0, SW) in LDS as a node id and the distance as a bf16
+// rounded toward -inf (6 B each; the pop's prune test on the rounded-down distance keeps
+// every entry the exact test keeps), deeper entries as full pairs in scratch.
+constexpr int SB = 16;   // 16 x 4 B x 256 lanes = 16 KB per block
+constexpr int SW = 12;   // 12 x 6 B x 256 lanes = 18 KB per block (8 blocks per CU)
+
+template <bool COUNT, int MODE>
 __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
@@ -803,43 +724,29 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch) {
-    // MODE 3 = MODE 2 with postponed leaves: a lane that reaches a leaf parks it (one per
-    // lane) and keeps walking; leaf tests run only in "leaf phases" -- when leaf_batch
-    // lanes hold a parked leaf, or a lane cannot go on without testing its leaf.  Census
-    // (C5): 90% of wave iterations held both leaf and internal lanes, so the triangle
-    // test's VALU ran in nearly every iteration for ~6 of 44 lanes.  The kept answer is
-    // the (t, leaf) minimum over every leaf whose box was hit, as in MODE 2.
-    // MODE 4 = MODE 2 on the quantized nodes (qn, rtbvh_device.h QNode): a 4-wide step
-    // reads one 64-B node instead of the 128-B record pair.
-    constexpr bool NEAREST = MODE >= 1, WIDE = MODE >= 2, POSTPONE = MODE == 3, QUANT = MODE == 4;
+                                                          unsigned long long* __restrict__ overflow, int limit) {
+    constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     const uint32_t n = *qin_count;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0};
     bool has = false, hit = false;
-    uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0, pend = INVALID;
+    uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
     int sp = 0;
     float best = 0.f;
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
-    __shared__ uint32_t s_stk[WIDE || S == 0 ? 1 : S][BLOCK];
-    uint32_t stack[WIDE ? 1 : STACK_SIZE - S];   // entries [S, STACK_SIZE)
-    // 4-wide: (node, entry distance) entries [0, SW) in LDS as a node id and the distance as a
-    // bf16 rounded toward -inf (6 B: SW entries in the LDS that held 2/3 SW full pairs; the
-    // pop's prune test on the rounded-down distance keeps every entry the exact test keeps),
-    // deeper entries as full pairs in scratch.  PMC (C5, SW = 8 full pairs): ~26% of the
-    // walk's L2 requests were scratch-stack traffic.
-    constexpr int SW = WIDE ? S : 0;
-    __shared__ uint32_t s_wid[SW == 0 ? 1 : SW][BLOCK];
-    __shared__ uint16_t s_wt[SW == 0 ? 1 : SW][BLOCK];
+    __shared__ uint32_t s_stk[WIDE ? 1 : SB][BLOCK];
+    uint32_t stack[WIDE ? 1 : STACK_SIZE - SB];   // entries [SB, STACK_SIZE)
+    __shared__ uint32_t s_wid[WIDE ? SW : 1][BLOCK];
+    __shared__ uint16_t s_wt[WIDE ? SW : 1][BLOCK];
     uint2 wstack[WIDE ? STACK4 - SW : 1];        // entries [SW, STACK4)
     const uint32_t tid = threadIdx.x;
     auto spush = [&](uint32_t v) {
-        if (sp < S) s_stk[sp][tid] = v;
-        else stack[sp - S] = v;
+        if (sp < SB) s_stk[sp][tid] = v;
+        else stack[sp - SB] = v;
         ++sp;
     };
     auto spop_top = [&]() {   // --sp; refill the cached top from entry sp
-        if (--sp >= 0) top = sp < S ? s_stk[sp][tid] : stack[sp - S];
+        if (--sp >= 0) top = sp < SB ? s_stk[sp][tid] : stack[sp - SB];
     };
     auto wpush = [&](uint32_t id, float t) {
         if (sp < SW) {
@@ -851,29 +758,19 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         ++sp;
     };
     bool drained = false;
-    // rays [cnext, cend) of the queue belong to this wave; with chunk > 0 one atomic
-    // claims `chunk` rays and later refills take from them without touching the
-    // global counter (chunks lost to the plain threshold in the A/B above: the tail
-    // of the last claimed chunks outweighs the saved atomics)
-    uint32_t cnext = 0, cend = 0;
     unsigned long long wsteps = 0, mixed = 0, active_lanes = 0;
     while (true) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (!drained && (nidle >= refill_min || nidle == 64)) {
-            const uint32_t avail = cend - cnext;
+        if (!drained && (nidle >= REFILL_MIN || nidle == 64)) {
             uint32_t base = 0;
-            const uint32_t want = chunk ? chunk : nidle;
-            if (avail < nidle) {
-                if (lane == 0) base = atomicAdd(next, want);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (base >= n) drained = true;
-            }
+            if (lane == 0) base = atomicAdd(next, nidle);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base + nidle >= n) drained = true;   // nothing left after these
             if (!has) {
                 const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-                const uint32_t k = (uint32_t)__popcll(idle & lt);
-                const uint32_t p = k < avail ? cnext + k : base + (k - avail);
-                if (p < n && (k < avail || !drained)) {
+                const uint32_t p = base + (uint32_t)__popcll(idle & lt);
+                if (p < n) {
                     r = perm ? perm[p] : p;
                     const float4 q0 = reinterpret_cast<const float4*>(qin + r)[0];
                     const float4 q1 = reinterpret_cast<const float4*>(qin + r)[1];
@@ -886,27 +783,13 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                     bl = 0;
                     sp = 0;
                     top = INVALID;
-                    node = QUANT ? root_slot(T) : WIDE ? ((T == 1) ? LEAF_BIT : 0u) : root_slot(T);
-                    pend = INVALID;
-                    if (POSTPONE && T == 1) {   // a one-leaf tree: the leaf is parked, no node
-                        pend = LEAF_BIT;
-                        node = INVALID;
-                    }
+                    node = root_slot(T);
                     guard = 2 * T + 2;
                 }
             }
-            if (avail >= nidle) {
-                cnext += nidle;
-            } else if (!drained) {
-                cnext = base + (nidle - avail);
-                cend = base + want;
-                if (cnext >= n) drained = true;   // nothing left after these
-            } else {
-                cnext = cend;
-            }
         }
-        // every refill either hands out a ray or moves toward `drained`, so a wave with no
-        // ray left loops back to refill until the queue is drained
+        // every refill either hands out rays or sets `drained`, so a wave with no ray left
+        // loops back to refill until the queue is drained
         if (__ballot(has) == 0 && drained) break;
         if (COUNT) {   // wave-level divergence census (stats trav_*; all lanes converged here)
             const uint64_t act = __ballot(has);
@@ -915,40 +798,22 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             active_lanes += (uint32_t)__popcll(act);
             mixed += (lf != 0 && lf != act);
         }
-        bool do_leaf = false;   // POSTPONE: this lane tests its parked leaf in this iteration
-        if (POSTPONE) {         // wave-uniform phase choice (all lanes converged here)
-            const bool blocked = has && ((node & LEAF_BIT) != 0 || (node == INVALID && pend != INVALID));
-            const uint64_t bm = __ballot(blocked);
-            const uint32_t np = (uint32_t)__popcll(__ballot(has && pend != INVALID));
-            do_leaf = has && pend != INVALID && (bm != 0 || np >= leaf_batch);
-        }
         if (!has) continue;
         bool done = false;
         // one fetch for every active lane, leaf or internal, before the branch: a wave
         // holding both kinds would otherwise wait for two dependent round trips
-        // (leaf and child-pair records are both 64-B aligned records of 64 B; the
-        // 4-wide record pair adds a second 64 B for internal lanes)
-        const bool isleaf = POSTPONE ? do_leaf : (node & LEAF_BIT) != 0;
-        const uint32_t lid = POSTPONE ? pend : node;
-        const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(lid & ~LEAF_BIT))
-                        : QUANT ? reinterpret_cast<const v4f*>(qn + node)
-                                : reinterpret_cast<const v4f*>(inner + (WIDE ? 2 * (size_t)node : (size_t)node));
+        // (leaf records, child-pair records and quantized nodes are all 64-B aligned records)
+        const bool isleaf = (node & LEAF_BIT) != 0;
+        const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(node & ~LEAF_BIT))
+                        : WIDE ? reinterpret_cast<const v4f*>(qn + node)
+                               : reinterpret_cast<const v4f*>(inner + node);
         v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
-        // second half of a 4-wide record pair: leaf lanes neither load nor use it, and it
-        // is not carried across iterations (a per-iteration zero costs 16 v_mov; a
-        // loop-carried copy holds 16 VGPRs; loading the other half of the leaf's line on
-        // leaf lanes cost +2% in TA work)
-        v4f q4, q5, q6, q7;
-        if (WIDE && !QUANT && !isleaf) {   // the right child's record
-            q4 = rr[4]; q5 = rr[5]; q6 = rr[6]; q7 = rr[7];
-        }
         pin(q0); pin(q1); pin(q2); pin(q3);
-        if (WIDE && !QUANT) { pin(q4); pin(q5); pin(q6); pin(q7); }
         if (--guard == 0) {
             c.overflow++;
             done = true;
         } else if (isleaf) {
-            const uint32_t j = lid & ~LEAF_BIT;
+            const uint32_t j = node & ~LEAF_BIT;
             const v4f la = q0, lb = q1;
             const float e2z = q2.x;
             if (COUNT) c.leaf++;
@@ -958,13 +823,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 bl = j;
                 hit = true;
             }
-            if (POSTPONE) {
-                pend = INVALID;
-                if (node & LEAF_BIT) {   // the leaf that blocked this lane is parked now
-                    pend = node;
-                    node = INVALID;
-                }
-            } else if (WIDE) {
+            if (WIDE) {
                 node = INVALID;   // pop below
             } else {
                 node = top;                             // pop
@@ -977,7 +836,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             uint4 a3, b3;
             float t0, t1, t2, t3;
             bool h0, h1, h2, h3;
-            if (QUANT && q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
+            if (q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
                 const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w, sy = q1.x, sz = q1.y;
                 const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
                 const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
@@ -992,23 +851,20 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 h3 = RTBVH_QBOX(3, t3) & (b3.y != INVALID);
 #undef RTBVH_QBOX
             } else {
-                uint32_t own = 0;
-                if (QUANT) {   // a node without a finite grid: its exact record pair (node = its slot)
-                    own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
-                    const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
-                    q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
-                    q4 = pr[4]; q5 = pr[5]; q6 = pr[6]; q7 = pr[7];
-                }
-                // record pair: q0..q3 = the record of the left child, q4..q7 of the right one
+                // a node without a finite grid: its exact record pair (node = its slot; the
+                // pair of its children's records is at 2 * own, own = word 14 of its record)
+                const uint32_t own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
+                const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
+                q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
+                const v4f q4 = pr[4], q5 = pr[5], q6 = pr[6], q7 = pr[7];
                 a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
                 b3 = make_uint4(__float_as_uint(q7.x), __float_as_uint(q7.y), 0u, 0u);
-                if (QUANT) {   // grandchild ids -> slots (2 * parent + side; parent = word 14)
-                    const uint32_t ol = __float_as_uint(q3.z), orr = __float_as_uint(q7.z);
-                    if (!(a3.x & LEAF_BIT)) a3.x = 2 * ol;
-                    if (a3.y != INVALID && !(a3.y & LEAF_BIT)) a3.y = 2 * ol + 1;
-                    if (!(b3.x & LEAF_BIT)) b3.x = 2 * orr;
-                    if (b3.y != INVALID && !(b3.y & LEAF_BIT)) b3.y = 2 * orr + 1;
-                }
+                // grandchild ids -> slots (2 * parent + side; parent = word 14)
+                const uint32_t ol = __float_as_uint(q3.z), orr = __float_as_uint(q7.z);
+                if (!(a3.x & LEAF_BIT)) a3.x = 2 * ol;
+                if (a3.y != INVALID && !(a3.y & LEAF_BIT)) a3.y = 2 * ol + 1;
+                if (!(b3.x & LEAF_BIT)) b3.x = 2 * orr;
+                if (b3.y != INVALID && !(b3.y & LEAF_BIT)) b3.y = 2 * orr + 1;
                 h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, t0);
                 h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, t1) & (a3.y != INVALID);
                 h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, hit, best, t2);
@@ -1025,11 +881,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             sort2(k1, i1, k3, i3);
             sort2(k1, i1, k2, i2);
             node = i0;   // nearest (INVALID when no child is hit -> pop below)
-            if (POSTPONE && (i0 & LEAF_BIT) && i0 != INVALID && pend == INVALID) {
-                pend = i0;   // park it and walk on
-                node = INVALID;
-            }
-            if (sp + 3 > STACK4) {
+            if (sp + 3 > limit) {
                 c.overflow++;
                 done = true;
             } else {   // push the others farthest first
@@ -1051,7 +903,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             } else {
                 const bool swap = NEAREST && lh && rh && tr < tl;
                 if (lh && rh) {
-                    if (sp + 1 >= STACK_SIZE) {
+                    if (sp + 1 >= limit) {
                         c.overflow++;
                         node = top;
                         spop_top();
@@ -1073,15 +925,11 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 if (sp < SW) e = make_uint2(s_wid[sp][tid], __float_as_uint(bf16_up(s_wt[sp][tid])));
                 else e = wstack[sp - SW];
                 if (!hit || __uint_as_float(e.y) <= best) {
-                    if (POSTPONE && (e.x & LEAF_BIT) && pend == INVALID) {
-                        pend = e.x;   // park a popped leaf too, and keep popping for a node
-                        continue;
-                    }
                     node = e.x;
                     break;
                 }
             }
-            done = node == INVALID && (!POSTPONE || pend == INVALID);
+            done = node == INVALID;
         }
         if (done) {
             hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
@@ -1093,7 +941,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             }
         }
     }
-    if (COUNT || c.overflow) {
+    if (COUNT || __ballot(c.overflow != 0)) {
         unsigned long long v[3] = {c.internal, c.leaf, c.overflow};
 #pragma unroll
         for (int k = 0; k < 3; k++)
@@ -1107,7 +955,10 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 atomicAdd(&counters[11], mixed);
                 atomicAdd(&counters[12], active_lanes);
             }
-            if (v[2]) atomicAdd(&counters[8], v[2]);
+            if (v[2]) {
+                atomicAdd(&counters[8], v[2]);
+                atomicAdd(overflow, v[2]);
+            }
         }
     }
 }
@@ -1168,8 +1019,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
 
 // bounce-ray coherence sort key (results do not depend on the order): direction
 // octant in bits 27..29, 9-bit-per-axis Morton code of the origin inside the scene
-// box in bits 0..26 (A/B vs direction-only / origin-only / mixed keys: DESIGN.md).
-// Entries past the live count get the largest key and sort last.
+// box in bits 0..26.  Entries past the live count get the largest key and sort last.
 __device__ __forceinline__ uint32_t spread9(uint32_t v) {
     v &= 0x1FFu;
     v = (v | (v << 16)) & 0x030000FFu;
@@ -1200,18 +1050,6 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_keys(const RayQ* __restrict__ 
     vals[i] = i;
 }
 
-template <bool COUNT, int V>
-void launch_primary_t(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool emit, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_primary<COUNT, V>), grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
-}
-template <bool COUNT, int V>
-void launch_bounce_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
-                     uint32_t* qout_count, bool emit, hipStream_t s) {
-    const uint32_t blocks = 2048;   // 8 waves/SIMD x 1024 SIMDs / 4 waves per block; grid-stride over the queue
-    hipLaunchKernelGGL((k_bounce<COUNT, V>), dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, perm, qout,
-                       qout_count, (int)emit);
-}
-
 // RayTraceBVHPS.hlsl:13-16 + the R8G8B8A8_UNORM target: screen row y <- framebuffer row H-1-y
 __device__ __forceinline__ uint32_t unorm8(float c) { return (uint32_t)floorf(sat(c) * 255.f + .5f); }
 __global__ __launch_bounds__(BLOCK) void k_present(const float4* __restrict__ color, uint32_t W, uint32_t H,
@@ -1236,61 +1074,63 @@ __global__ __launch_bounds__(BLOCK) void k_assemble(const float4* __restrict__ b
     frame[i] = bands[((size_t)r * stride_rows + k) * W + x];
 }
 
-template <bool COUNT, int S>
+// frames compared pixel for pixel (rtbvh_compare_frames): *diff += pixels whose 16 bytes differ
+__global__ __launch_bounds__(BLOCK) void k_count_diff(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                      size_t n, unsigned long long* __restrict__ diff) {
+    unsigned long long cnt = 0;
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) {
+        const uint4 x = a[i], y = b[i];
+        cnt += (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane_id() == 0 && cnt) atomicAdd(diff, cnt);
+}
+
+template <bool COUNT, int K>
+void launch_primary_t(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool emit, dim3 grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_primary<COUNT, K>), grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
+}
+template <int K>
+void launch_primary_c(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, dim3 grid, hipStream_t s) {
+    if (count) launch_primary_t<true, K>(a, q, qcount, emit, grid, s);
+    else launch_primary_t<false, K>(a, q, qcount, emit, grid, s);
+}
+
+template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                          int mode, float2* hitrec, uint32_t* next, uint32_t refill_min, uint32_t chunk,
-                          uint32_t leaf_batch, uint32_t blocks, hipStream_t s) {
-    // persistent: 2048 blocks = 8 waves/SIMD x 1024 SIMDs / 4 waves per block
-    const uint32_t extra_lds = (chunk >> 24) * 1024u;   // A/B only: dynamic LDS (KB in the top byte)
-    chunk &= (1u << 24) - 1;                            // that caps the resident blocks per CU
-    if (mode == 4)   // 12 entries x 6 B x 256 lanes = 18 KB per block (8 blocks per CU)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 4, (S > 8 ? 12 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s,
-                           a.inner4, a.qnode, a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, refill_min,
-                           chunk, leaf_batch);
-    else if (mode == 3)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 3, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s,
-                           a.inner4, a.qnode, a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk,
-                           leaf_batch);
-    else if (mode == 2)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 2, (S > 8 ? 8 : S)>), dim3(blocks), dim3(BLOCK), extra_lds, s, a.inner4, a.qnode, a.leaf, a.T, qin,
-                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
-    else if (mode == 1)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 1, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, a.T, qin,
-                           qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
-    else
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, 0, S>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, a.T,
-                           qin, qin_count, perm, hitrec, next, a.counters, refill_min, chunk, leaf_batch);
+                          float2* hitrec, uint32_t* next, uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, a.T,
+                       qin, qin_count, perm, hitrec, next, a.counters, a.overflow,
+                       MODE == 2 ? a.stack_limit4 : a.stack_limit);
 }
 
 }  // namespace
 
-#define RTBVH_VARIANTS(M)                                 \
-    switch (variant) {                                    \
-        case 1: count ? M(true, 1) : M(false, 1); break;  \
-        case 2: count ? M(true, 2) : M(false, 2); break;  \
-        case 3: count ? M(true, 3) : M(false, 3); break;  \
-        case 4: count ? M(true, 4) : M(false, 4); break;  \
-        case 5: count ? M(true, 5) : M(false, 5); break;  \
-        default: count ? M(true, 0) : M(false, 0); break; \
-    }
-
-void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, int variant, hipStream_t s) {
+void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, PrimaryKind kind,
+                    hipStream_t s) {
     const uint32_t nbands = (a.H + 7) / 8;
     const uint32_t my_bands = a.rank < nbands ? (nbands - a.rank + a.nranks - 1) / a.nranks : 0;
     const uint32_t launch_bands = my_bands > a.band0 ? (my_bands - a.band0 + a.bstep - 1) / a.bstep : 0;
     if (launch_bands == 0 || a.W == 0) return;
     dim3 grid((a.W + 31) / 32, launch_bands);
-#define RTBVH_PRIM(C, V) launch_primary_t<C, V>(a, q, qcount, emit, grid, s)
-    if (variant == 6) count ? RTBVH_PRIM(true, 6) : RTBVH_PRIM(false, 6);
-    else if (variant == 7) count ? RTBVH_PRIM(true, 7) : RTBVH_PRIM(false, 7);
-    else RTBVH_VARIANTS(RTBVH_PRIM)
-#undef RTBVH_PRIM
+    switch (kind) {
+        case PrimaryKind::LANE_NEAREST: launch_primary_c<1>(a, q, qcount, count, emit, grid, s); break;
+        case PrimaryKind::PACKET_REFERENCE: launch_primary_c<2>(a, q, qcount, count, emit, grid, s); break;
+        case PrimaryKind::PACKET_NEAREST: launch_primary_c<3>(a, q, qcount, count, emit, grid, s); break;
+        case PrimaryKind::PACKET_WIDE: launch_primary_c<4>(a, q, qcount, count, emit, grid, s); break;
+        default: launch_primary_c<0>(a, q, qcount, count, emit, grid, s); break;
+    }
 }
 
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
-                   uint32_t* qout_count, bool count, bool emit, int variant, hipStream_t s) {
-#define RTBVH_BNC(C, V) launch_bounce_t<C, V>(a, qin, qin_count, perm, qout, qout_count, emit, s)
-    RTBVH_VARIANTS(RTBVH_BNC)
+                   uint32_t* qout_count, bool count, bool emit, bool nearest, hipStream_t s) {
+    const uint32_t blocks = 2048;   // 8 waves/SIMD x 1024 SIMDs / 4 waves per block; grid-stride over the queue
+#define RTBVH_BNC(C, N)                                                                                            \
+    hipLaunchKernelGGL((k_bounce<C, N>), dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, perm, qout, qout_count, \
+                       (int)emit)
+    if (count) { if (nearest) RTBVH_BNC(true, true); else RTBVH_BNC(true, false); }
+    else { if (nearest) RTBVH_BNC(false, true); else RTBVH_BNC(false, false); }
 #undef RTBVH_BNC
 }
 
@@ -1300,20 +1140,14 @@ void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, 
 }
 
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                            bool count, int mode, float2* hitrec, uint32_t* next, int lds_stack,
-                            uint32_t refill_min, uint32_t chunk, uint32_t leaf_batch, uint32_t blocks, hipStream_t s) {
-    if (refill_min == 0) refill_min = REFILL_MIN;
+                            bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
+                            hipStream_t s) {
     if (blocks == 0) blocks = 2048;
-#define RTBVH_TRAV(S)                                                                                        \
-    (count ? launch_bounce_trav_t<true, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, \
-                                           blocks, s)                                                              \
-           : launch_bounce_trav_t<false, S>(a, qin, qin_count, perm, mode, hitrec, next, refill_min, chunk, leaf_batch, \
-                                            blocks, s))
-    switch (lds_stack) {
-        case 0: RTBVH_TRAV(0); break;
-        case 8: RTBVH_TRAV(8); break;
-        case 20: RTBVH_TRAV(20); break;
-        default: RTBVH_TRAV(16); break;
+#define RTBVH_TRAV(C, M) launch_bounce_trav_t<C, M>(a, qin, qin_count, perm, hitrec, next, blocks, s)
+    switch (walk) {
+        case BounceWalk::NEAREST: if (count) RTBVH_TRAV(true, 1); else RTBVH_TRAV(false, 1); break;
+        case BounceWalk::WIDE_QUANTIZED: if (count) RTBVH_TRAV(true, 2); else RTBVH_TRAV(false, 2); break;
+        default: if (count) RTBVH_TRAV(true, 0); else RTBVH_TRAV(false, 0); break;
     }
 #undef RTBVH_TRAV
 }
@@ -1339,6 +1173,14 @@ void launch_assemble(const float4* bands, uint32_t stride_rows, uint32_t W, uint
 void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, hipStream_t s) {
     const size_t n = (size_t)W * H;
     if (n) hipLaunchKernelGGL(k_present, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, color, W, H, out);
+}
+
+void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long long* diff, hipStream_t s) {
+    if (n == 0) return;
+    size_t blocks = (n + BLOCK - 1) / BLOCK;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_count_diff, dim3((uint32_t)blocks), dim3(BLOCK), 0, s, reinterpret_cast<const uint4*>(a),
+                       reinterpret_cast<const uint4*>(b), n, diff);
 }
 
 }  // namespace rtbvh

@@ -21,7 +21,8 @@ class Context:
     """One rtbvh_ctx: one HIP device, one stream, the scene/BVH/frame buffers."""
 
     def __init__(self, device: int = 0, morton_mode: int = _L.MORTON_CPUTESTS, delta_mode: int = _L.DELTA_CLZ64,
-                 flags: int = 0, scene_bb_min=(-700.0,) * 3, scene_bb_max=(700.0,) * 3, stream: int | None = None):
+                 flags: int = 0, scene_bb_min=(-700.0,) * 3, scene_bb_max=(700.0,) * 3, stream: int | None = None,
+                 stack_limit: int = 0):
         L = _L.lib()
         cfg = _L.Config()
         L.rtbvh_config_default(ctypes.byref(cfg))
@@ -32,6 +33,7 @@ class Context:
         cfg.scene_bb_min[:] = list(scene_bb_min)
         cfg.scene_bb_max[:] = list(scene_bb_max)
         cfg.stream = stream
+        cfg.stack_limit = stack_limit
         h = ctypes.c_void_p()
         _L.check(L.rtbvh_create(ctypes.byref(cfg), ctypes.byref(h)), None)
         self._h = h
@@ -90,6 +92,14 @@ class Context:
     def compute_bvh(self, width: int, height: int, bounces: int = 1):
         self._check(_L.lib().rtbvh_compute_bvh(self._h, width, height, bounces))
         self.width, self.height = width, height
+
+    def verify_walk(self, width: int, height: int, bounces: int = 1) -> int:
+        """rtbvh_verify_walk: pixels whose bits differ between the reference-order frame and
+        the frame of this context's walks (0: identical); leaves the latter in the framebuffer."""
+        n = ctypes.c_uint64()
+        self._check(_L.lib().rtbvh_verify_walk(self._h, width, height, bounces, ctypes.byref(n)))
+        self.width, self.height = width, height
+        return n.value
 
     def trace_band_async(self, width: int, height: int, bounces: int, rank: int, nranks: int, dev_out_ptr: int,
                          stream_ptr: int | None = None):

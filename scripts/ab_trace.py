@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B the traversal kernel variants on the C5 frame in ONE process (interleaved
+"""A/B traversal walk flags (or, with AB_SET=base, two library builds via RTBVH_LIB) on the C5 frame in ONE process (interleaved
 rounds, cdna_hip_programming.md §5.4 rule 24).  Every variant's framebuffer must
 equal the baseline's bit for bit.  Prints one JSON line per variant."""
 import json
@@ -29,36 +29,12 @@ def main():
                 ("nearest+wide", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH),
                 ("nearest+wide+sort", rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
                  | rt.FLAG_SORT_BOUNCE)]
-    if os.environ.get("AB_SET") == "stack":   # LDS stack depth of the refill traversal
-        base = rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
-        V = rt.FLAG_VARIANT_SHIFT
-        variants = [("nearest+refill lds16", base), ("lds20", base | 4 << V),
-                    ("nearest+wide lds8", base | rt.FLAG_WIDE_BVH), ("nearest+wide lds0", base | rt.FLAG_WIDE_BVH | 2 << V)]
-    if os.environ.get("AB_SET") == "refill":   # idle lanes that trigger a refill
-        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
-        V = rt.FLAG_VARIANT_SHIFT
-        variants = [("wide refill32", base), ("refill16", base | 5 << V), ("thr8 chunk128", base | 6 << V), ("thr16 chunk128", base | 7 << V),
-                    ("thr8 chunk256", base | 8 << V), ("thr16 chunk64", base | 9 << V), ("thr4 chunk128", base | 10 << V),
-                    ("binary nearest thr8 chunk128", base & ~rt.FLAG_WIDE_BVH | 6 << V)]
-    if os.environ.get("AB_SET") == "occupancy":
-        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
-        V = rt.FLAG_VARIANT_SHIFT
-        variants = [("8 waves/SIMD", base), ("6 waves/SIMD", base | 14 << V), ("4 waves/SIMD", base | 13 << V)]
     if os.environ.get("AB_SET") == "sort":
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
         variants = [("wide", base), ("wide + bounce sort", base | rt.FLAG_SORT_BOUNCE)]
-    if os.environ.get("AB_SET") == "postpone":
-        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
-        V = rt.FLAG_VARIANT_SHIFT
-        variants = [("wide", base), ("postpone 8", base | 5 << V), ("postpone 16", base | 15 << V),
-                    ("postpone 24", base | 6 << V), ("postpone 32", base | 7 << V)]
     if os.environ.get("AB_SET") == "base":   # the bench's mode only (A/B of two builds via RTBVH_LIB)
         variants = [("nearest-first-wide", rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST
                      | rt.FLAG_WIDE_BVH)]
-    if os.environ.get("AB_SET") == "axis":   # primary box test for axis-parallel rays
-        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
-        V = rt.FLAG_VARIANT_SHIFT
-        variants = [("axis min3", base), ("general", base | 11 << V), ("axis cmp", base | 12 << V)]
     if os.environ.get("AB_SET") == "wide":
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
         variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),

@@ -17,7 +17,6 @@ K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 W, H = 3840, 2160
 scene = rt.synthetic(10_000_000, seed=0x5EED0005, half_extent=(100.0, 100.0, 50.0))
 flags = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
-variants = [int(x) for x in os.environ.get("INFLIGHT_VARIANTS", "0").split(",")]   # A/B kernel variants
 torch.cuda.set_device(0)
 streams = [torch.cuda.Stream() for _ in range(3)]
 out = {}
@@ -27,8 +26,8 @@ with rt.Context(device=0, flags=flags, stream=streams[0].cuda_stream) as c:
     c.build()
     bufs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in range(3)]
     torch.cuda.synchronize()
-    for N, vv in ((N, vv) for vv in variants for N in (1, 2, 4, 8)):
-        c.set_flags(flags | vv << rt.FLAG_VARIANT_SHIFT)
+    for N in (1, 2, 4, 8):
+        c.set_flags(flags)
         row = {}
         for F in (1, 2, 3):
             def frames(n):
@@ -41,5 +40,5 @@ with rt.Context(device=0, flags=flags, stream=streams[0].cuda_stream) as c:
             frames(K)
             torch.cuda.synchronize()
             row[f"ms_per_frame_{F}_in_flight"] = round((time.perf_counter() - t0) / K * 1e3, 4)
-        out[f"N{N}_rank0" + (f"_v{vv}" if vv else "")] = row
+        out[f"N{N}_rank0"] = row
 print(json.dumps(out))

@@ -40,10 +40,9 @@ with rt.Context(device=0, flags=flags, stream=stream.cuda_stream) as ctx:
         print(json.dumps({"only": [N, r], "ms_trace": ctx.stats()["ms_trace"]}))
         sys.exit(0)
     splits = [int(x) for x in os.environ.get("RANK_SIM_SPLITS", "0").split(",")]
-    variants = [int(x) for x in os.environ.get("RANK_SIM_VARIANTS", "0").split(",")]   # A/B kernel variants
     Ns = [int(x) for x in os.environ.get("RANK_SIM_N", "1,2,4,8").split(",")]
-    for N, sp, vv in ((N, sp, vv) for vv in variants for sp in splits for N in Ns):
-        ctx.set_flags(flags | sp << rt.FLAG_SPLIT_SHIFT | vv << rt.FLAG_VARIANT_SHIFT)
+    for N, sp in ((N, sp) for sp in splits for N in Ns):
+        ctx.set_flags(flags | sp << rt.FLAG_SPLIT_SHIFT)
         per, stages = [], []
         for r in range(N):
             for _ in range(2):
@@ -64,7 +63,7 @@ with rt.Context(device=0, flags=flags, stream=stream.cuda_stream) as ctx:
                     ctx.trace_band_async(W, H, 1, r, N, buf.data_ptr())
                 torch.cuda.synchronize()
                 wall0 = (time.perf_counter() - t0) / K * 1e3
-        out[f"N{N}_split{sp}" + (f"_v{vv}" if vv else "")] = {"rank_ms": per, "max_ms": max(per), "rank0_wall_ms": round(wall0, 4),
+        out[f"N{N}_split{sp}"] = {"rank_ms": per, "max_ms": max(per), "rank0_wall_ms": round(wall0, 4),
                   "stages_primary_trav_shade": stages,
                   "rows": len(band_row_ids(H, 0, N))}
     for key in out:

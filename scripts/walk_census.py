@@ -15,9 +15,6 @@ W, H = 3840, 2160
 scene = rt.synthetic(10_000_000, seed=0x5EED0005, half_extent=(100.0, 100.0, 50.0))
 FAST = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST
 modes = {"nearest-first-wide": FAST | rt.FLAG_WIDE_BVH, "nearest-first": FAST}
-extra = os.environ.get("CENSUS_VARIANTS", "")   # e.g. "16,0": A/B kernel variants of the wide mode
-for v in (int(x) for x in extra.split(",") if x):
-    modes[f"nearest-first-wide-v{v}"] = FAST | rt.FLAG_WIDE_BVH | v << rt.FLAG_VARIANT_SHIFT
 out = {}
 with rt.Context(device=0, flags=FAST) as c:
     c.set_scene(scene)

@@ -197,23 +197,17 @@ def test_build_10m_tree_properties():
 
 
 # ---------------------------------------------------------------- trace
+# the shipped walk combinations (include/rtbvh.h RTBVH_FLAG_*; "auto" picks one of them by size)
+WALK_FLAGS = rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_WIDE_BVH
 TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest": rt.FLAG_NEAREST_FIRST,
-               "first_version": 1 << rt.FLAG_VARIANT_SHIFT, "packet": rt.FLAG_PACKET_PRIMARY,
+               "packet": rt.FLAG_PACKET_PRIMARY,
                "nearest+packet": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY,
                "refill+sort": rt.FLAG_REFILL_BOUNCE | rt.FLAG_SORT_BOUNCE,
                "nearest+packet+refill": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE,
                "nearest+packet+wide": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
                "packet+wide": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
-               "packet+wide, general primary box test (A/B variant 11)":
-                   rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 11 << rt.FLAG_VARIANT_SHIFT,
-               "packet+wide, compare-form primary box test (A/B variant 12)":
-                   rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH | 12 << rt.FLAG_VARIANT_SHIFT,
-               "wide+postponed-leaves (A/B variant 15)": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
-               | 15 << rt.FLAG_VARIANT_SHIFT,
-               "nearest+packet+wide, exact record pairs (variant 17)": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY
-               | rt.FLAG_WIDE_BVH | 17 << rt.FLAG_VARIANT_SHIFT,
-               "packet+wide, exact record pairs (variant 17)": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH
-               | 17 << rt.FLAG_VARIANT_SHIFT}
+               "wide+sort": rt.FLAG_WIDE_BVH | rt.FLAG_SORT_BOUNCE,
+               "auto": rt.FLAG_AUTO_WALK}
 
 
 def _trace_both(s, W, H, bounces, rows=None, flags=0):
@@ -243,7 +237,7 @@ def test_trace_matches_oracle_on_obj(name, W, H, bounces, mode):
     np.testing.assert_array_equal(inten, oint)
     assert sum(st["hits"]) == ost["hits"] and st["textured_hits"] == ost["textured_hits"]
     assert st["bounce_rays"] == ost["bounce"] and st["stack_overflows"] == 0
-    if "nearest" not in mode and "wide" not in mode:   # reference-order kernels take exactly the oracle's steps
+    if "nearest" not in mode and "wide" not in mode and mode != "auto":   # reference order: the oracle's steps
         assert sum(st["internal_visits"]) == ost["internal_visits"]
         assert sum(st["leaf_visits"]) == ost["leaf_visits"]
     else:
@@ -539,9 +533,7 @@ def _general_box_scene(seed=11):
     return rt.Scene(verts, idx, mats, base.materials)
 
 
-@pytest.mark.parametrize("mode", ["packet+wide", "nearest+packet+wide",
-                                  "packet+wide, compare-form primary box test (A/B variant 12)",
-                                  "nearest+packet+wide, exact record pairs (variant 17)"])
+@pytest.mark.parametrize("mode", ["packet+wide", "nearest+packet+wide", "packet"])
 def test_primary_general_boxes(mode):
     """Flat and behind-the-eye boxes (record word 15 set) in the axis-parallel primary walk:
     frames identical to the oracle's, and the record bits as the tree's boxes say."""
@@ -650,6 +642,117 @@ def test_compute_bvh_graph_replays_the_frame():
                 c.compute_bvh(W, H, b)
             np.testing.assert_array_equal(g.read_framebuffer(), plain.read_framebuffer())
             np.testing.assert_array_equal(g.read_bvh()["bb_min"], plain.read_bvh()["bb_min"])
+        assert g.stats()["graph_captures"] == 3   # (320, 240, 1), (400, 200, 2), the new camera
+
+
+def test_graph_replay_writes_the_frame():
+    """A replayed graph (not a re-capture) renders the frame: the camera set every frame with
+    the same matrices (Graphics::onUpdate) keeps the graph; between replays the framebuffer is
+    overwritten by a different frame of the same size (0 bounces), and each replay must restore
+    the 1-bounce frame of a plain context, with one capture in all."""
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    W, H = 320, 240
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0) as plain, rt.Context(device=0, flags=rt.FLAG_GRAPH) as g:
+        for c in (plain, g):
+            c.set_scene(s)
+            c.set_camera(wvp, wv)
+        plain.compute_bvh(W, H, 1)
+        want = plain.read_framebuffer()
+        plain.trace(W, H, 0)
+        other = plain.read_framebuffer()
+        assert not np.array_equal(other, want)
+        for i in range(4):
+            g.set_camera(wvp.copy(), wv.copy())   # every frame, unchanged
+            g.compute_bvh(W, H, 1)
+            np.testing.assert_array_equal(g.read_framebuffer(), want, err_msg=f"replay {i}")
+            g.trace(W, H, 0)                      # overwrite the framebuffer between replays
+            np.testing.assert_array_equal(g.read_framebuffer(), other)
+        assert g.stats()["graph_captures"] == 1
+
+
+def test_graph_replay_after_band_traces_and_other_sizes():
+    """A replay after a band trace on a caller stream (a frame in flight over the BVH the replay
+    rebuilds) and after a trace of another size: the replay waits for the frame in flight, and
+    read_framebuffer returns the replayed W x H frame."""
+    import torch
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    W, H = 320, 240
+    wvp, wv = rt.camera_reference(W, H)
+    stream = torch.cuda.Stream()
+    with rt.Context(device=0) as plain, rt.Context(device=0, flags=rt.FLAG_GRAPH) as g:
+        for c in (plain, g):
+            c.set_scene(s)
+            c.set_camera(wvp, wv)
+        plain.compute_bvh(W, H, 1)
+        want = plain.read_framebuffer()
+        g.compute_bvh(W, H, 1)
+        band = torch.full((H, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()
+        g.trace_band_async(W, H, 1, 0, 1, band.data_ptr(), stream_ptr=stream.cuda_stream)
+        g.compute_bvh(W, H, 1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(band.cpu().numpy(), want)
+        np.testing.assert_array_equal(g.read_framebuffer(), want)
+        g.trace(200, 100, 2)                       # another size in between
+        g.compute_bvh(W, H, 1)
+        assert g.read_framebuffer().shape == (H, W, 4)
+        np.testing.assert_array_equal(g.read_framebuffer(), want)
+
+
+@pytest.mark.parametrize("mode", ["reference", "nearest", "packet", "nearest+packet", "nearest+packet+refill",
+                                  "nearest+packet+wide", "refill+sort"])
+def test_stack_limit_reports_overflow(mode):
+    """rtbvh_config.stack_limit: a ray whose stack would exceed the limit ends early and the
+    synchronising call returns RTBVH_ERR_STACK_OVERFLOW once (the frame is complete); with the
+    compiled capacity, and with the reference's 32 entries on its own mesh, nothing overflows."""
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    W, H = 320, 240
+    frames = {}
+    for limit in (0, 32, 2):
+        with rt.Context(device=0, flags=TRACE_MODES[mode], stack_limit=limit) as c:
+            c.set_scene(s)
+            c.set_camera(*rt.camera_reference(W, H))
+            c.build()
+            if limit == 2:
+                with pytest.raises(rt.RtbvhError) as e:
+                    c.trace(W, H, 1)
+                assert e.value.status == rt._lib.ERR_STACK_OVERFLOW
+                assert "stack" in str(e.value)
+                assert c.stats()["stack_overflows"] > 0
+                c.synchronize()   # reported once
+            else:
+                c.trace(W, H, 1)
+                assert c.stats()["stack_overflows"] == 0
+            c.width, c.height = W, H
+            frames[limit] = c.read_framebuffer()
+    np.testing.assert_array_equal(frames[32], frames[0])
+    assert not np.array_equal(frames[2], frames[0])
+
+
+def test_verify_walk_and_auto_walk():
+    """rtbvh_verify_walk: the fast walks render the reference-order frame (0 differing pixels);
+    RTBVH_FLAG_AUTO_WALK takes the reference-order kernels on small scenes and the 4-wide
+    nearest-first walks on large ones, with the same frames."""
+    d = load_scene_fixture("Test")
+    small = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    big = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    W, H = 960, 540
+    for s, walk in ((small, 0), (big, WALK_FLAGS)):
+        with rt.Context(device=0) as ref, rt.Context(device=0, flags=rt.FLAG_AUTO_WALK) as auto, \
+                rt.Context(device=0, flags=TRACE_MODES["nearest+packet+wide"]) as fast:
+            for c in (ref, auto, fast):
+                c.set_scene(s)
+                c.set_camera(*rt.camera_reference(W, H))
+                c.compute_bvh(W, H, 1)
+            assert auto.stats()["walk_flags"] == walk
+            np.testing.assert_array_equal(auto.read_framebuffer(), ref.read_framebuffer())
+            assert fast.verify_walk(W, H, 1) == 0
+            np.testing.assert_array_equal(fast.read_framebuffer(), ref.read_framebuffer())
+            assert auto.verify_walk(W, H, 1) == 0
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
