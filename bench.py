@@ -18,8 +18,15 @@ fills the GPU while frame i's bounce walk drains its last long walks; two band b
 gathered and assembled before the timed region closes.  The one-frame latency (one
 context, frames back to back on one stream) is reported beside it.  The BVH is built once before the timed
 loop (the scene is static; replicated build throughput is measured separately and
-reported under "build").  value = all rays of the frame (W*H primary + every
-live bounce ray, summed over ranks) / max-over-ranks time per step.
+reported under "build"); the reference's own per-frame semantics -- Graphics.cpp:56 rebuilds
+the BVH and traces every frame, behind a fence -- is measured beside it at N = 1
+("c5_frame_rebuild").  value = all rays of the frame (W*H primary + every live bounce ray,
+summed over ranks) / max-over-ranks time per step.
+
+Parity at the headline size (N = 1, rank 0, inside the cpu_baseline leg): the oracle builds
+its own tree of the same 10M triangles (compared with the GPU tree field by field) and traces
+the whole 3840x2160 frame on it (OpenMP over rows), which is compared with the GPU frame of
+the reported mode pixel for pixel ("parity").
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c3]
        (N > 1 under `torch.distributed.run --nproc-per-node N`).
@@ -30,11 +37,18 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# algorithmic bytes per unit, SURVEY.md §8(d) (the reference's data per unit of work)
+# algorithmic bytes per unit of THIS layout (the bytes each walk step requests):
+L_REC = 64                       # one 64-B record per step: a QNode / child-pair record / leaf record
+L_BOUNCE_RAY = 32 + 8            # bounce walk per ray: the 32-B queue entry read + the 8-B hit record write
+L_PRIMARY_PIXEL = 16 + 4         # primary per pixel: colour (16 B) + intensity (4 B) written
+L_QUEUE = 32                     # primary per live bounce ray: the queue entry written
+# SURVEY.md §8(d) figures (the reference's data per unit of work; the frame_roofline below)
 S_INT = 56                       # internal visit: children ids 8 B + two child AABBs 48 B
 S_LEAF = 120                     # leaf visit: ids 8 + index 4 + 3 indices 12 + 3 Vertex 96
 S_PRIMARY = 56                   # reflectRay record write per primary ray
@@ -68,17 +82,19 @@ def make_scene(rt, wl):
     return rt.synthetic(wl["ntris"], seed=wl["seed"], half_extent=wl["half"])
 
 
-def trace_bytes(st, kernel, wide=False):
-    """Algorithmic bytes of one launch: SURVEY §8(d) per-unit figures x the units that
-    launch processes (its own visit counts).  A 4-wide visit tests the four grandchild
-    boxes = two binary child-pair records (2 x S_INT)."""
+def layout_bytes(st, kernel, wide_primary=False):
+    """Algorithmic bytes of one launch in this layout: the records its walk requests (one 64-B
+    record per lane step in the per-lane bounce walk; one 64-B record -- two for a 4-wide
+    step -- per WAVE step in the packet primary walk, which fetches a record once for its 64
+    rays) plus its per-ray inputs and outputs.  Counted with RTBVH_FLAG_COUNT_VISITS."""
     if kernel == "k_primary":
-        return (S_INT * st["internal_visits"][0] + S_LEAF * st["leaf_visits"][0] + S_PRIMARY * st["primary_rays"]
-                + S_HIT * st["hits"][0] + S_TEX * st["textured_hits"])
+        steps_int, steps_leaf = st["packet_steps"]
+        return ((2 if wide_primary else 1) * L_REC * steps_int + L_REC * steps_leaf
+                + L_PRIMARY_PIXEL * st["primary_rays"] + L_QUEUE * st["bounce_rays"])
     if kernel == "k_bounce_trav":
-        return (2 if wide else 1) * S_INT * st["internal_visits"][1] + S_LEAF * st["leaf_visits"][1]
-    # k_bounce_shade
-    return S_BOUNCE * st["bounce_rays"] + S_HIT * st["hits"][1]
+        return L_REC * (st["internal_visits"][1] + st["leaf_visits"][1]) + L_BOUNCE_RAY * st["bounce_rays"]
+    # k_bounce_shade: queue entry + hit record in, colour read + written, the hit's shading data
+    return (32 + 8 + 32) * st["bounce_rays"] + S_HIT * st["hits"][1]
 
 
 def frame_bytes(st):
@@ -87,17 +103,37 @@ def frame_bytes(st):
             + S_BOUNCE * st["bounce_rays"] + S_HIT * sum(st["hits"]) + S_TEX * st["textured_hits"])
 
 
-def load_pmc(workload, mode, kernel, counters=False):
-    """Per-launch HBM bytes of `kernel` (or its raw counters) from the PMC passes of the same
-    traversal mode (profiles/pmc_<workload>_<mode>.json, written by scripts/make_pmc_json.py)."""
+def load_pmc(workload, mode, kernel):
+    """The PMC record of `kernel` (per-launch HBM bytes, raw counters and the launch's record
+    fetches) from the rocprofv3 passes of the same traversal mode at N = 1
+    (profiles/pmc_<workload>_<mode>.json, scripts/make_pmc_json.py), or None."""
     path = os.path.join(REPO, "profiles", f"pmc_{workload}_{mode}.json")
     if not os.path.exists(path):
         return None
     try:
-        k = json.load(open(path))["kernels"][kernel]
-        return k["counters"] if counters else k["hbm_bytes_per_launch"]
+        return json.load(open(path))["kernels"][kernel]
     except Exception:
         return None
+
+
+def build_pmc(workload, mode):
+    """Summed per-launch HBM bytes of the build kernels in the same PMC profile, or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_{workload}_{mode}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        ks = json.load(open(path))["kernels"]
+    except Exception:
+        return None
+    names = [k for k in ks if k in BUILD_KERNELS]
+    if not names:
+        return None
+    return {"hbm_bytes": sum(ks[k]["hbm_bytes_per_launch"] for k in names),
+            "per_kernel_gb": {k: round(ks[k]["hbm_bytes_per_launch"] / 1e9, 3) for k in names}}
+
+
+BUILD_KERNELS = ("k_bounds", "k_bounds_final", "k_morton", "k_upsweep", "k_scan_rows", "k_downsweep",
+                 "k_leaf_karras", "k_refit", "k_qnodes", "k_build_small")
 
 
 def cpu_model() -> str:
@@ -110,35 +146,58 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(rt, scene, ctx, wl, W, H):
-    """Oracle (single-thread C++ restatement of the reference path) on a bounded sample."""
+NODE_FIELDS = ("parent", "child_l", "child_r", "code", "index", "bb_min", "bb_max")
+
+
+def cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame):
+    """The oracle (C++ restatement of the reference path, oracle/) on the GPU box's host cores:
+    its own BVH of the bench scene (the parity check of the tree), a single-thread trace
+    sample (the timed baseline), the whole frame on all cores (the timed all-cores baseline
+    and the pixel parity check of the headline frame), and the reference-faithful 32-pass
+    split-sort build on a 1M-triangle sample."""
     from oracle import lib as orc
     wvp, wv = rt.camera_reference(W, H)
-    nodes = ctx.read_bvh()
+    gnodes = ctx.read_bvh()
     osc = orc.Scene(scene.vertices, scene.indices, scene.mat_indices, scene.material_blob)
+    parity = {"tolerance_rgb": 1e-4}
+    t0 = time.perf_counter()
+    onodes = orc.build(osc, wvp)
+    parity["tree_nodes"] = int(len(onodes))
+    parity["tree_bit_identical"] = bool(all(np.array_equal(gnodes[f], onodes[f]) for f in NODE_FIELDS))
+    parity["tree_oracle_s"] = round(time.perf_counter() - t0, 2)
+    del gnodes
     step = 8 if W * H > 4_000_000 else 4
     t0 = time.perf_counter()
-    _, _, st = orc.trace(osc, nodes, wvp, wv, W, H, wl["bounces"], 0, H, step)
+    fb1, _, st = orc.trace(osc, onodes, wvp, wv, W, H, wl["bounces"], 0, H, step)
     dt = time.perf_counter() - t0
     rays = st["primary"] + st["bounce"]
     res = {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-           "sample": f"oracle/liboracle.so orc_trace of 1 row in {step} of the same frame and BVH "
-                     f"({st['primary']} primary + {st['bounce']} bounce rays, {dt:.1f} s, 1 thread)",
+           "sample": f"oracle/liboracle.so orc_trace of 1 row in {step} of the same frame, on the oracle's own BVH "
+                     f"of the same scene ({st['primary']} primary + {st['bounce']} bounce rays, {dt:.1f} s, 1 thread)",
            "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
     # BASELINE.md's all-cores variant: the same code, OpenMP over rows, on this process's CPU
-    # share (OMP_NUM_THREADS, 16 on the GPU boxes), on a 4x larger sample
+    # share (OMP_NUM_THREADS, 16 on the GPU boxes), over the WHOLE frame (the parity check)
     threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
-    step_all = max(1, step // 4)
     orc.set_threads(threads)
     try:
         t0 = time.perf_counter()
-        _, _, st2 = orc.trace(osc, nodes, wvp, wv, W, H, wl["bounces"], 0, H, step_all)
+        fb, _, st2 = orc.trace(osc, onodes, wvp, wv, W, H, wl["bounces"], 0, H, 1)
         dt2 = time.perf_counter() - t0
     finally:
         orc.set_threads(1)
     res["all_cores"] = {"value": (st2["primary"] + st2["bounce"]) / dt2 / 1e6, "unit": "Mrays/s", "cores": threads,
-                        "sample": f"1 row in {step_all}, {st2['primary']} primary + {st2['bounce']} bounce rays, "
+                        "sample": f"every row, {st2['primary']} primary + {st2['bounce']} bounce rays, "
                                   f"{dt2:.1f} s, OpenMP over rows"}
+    del onodes
+    if gpu_frame is not None:
+        diff = np.abs(fb - gpu_frame)
+        parity.update({"rows_checked": int(H), "pixels_checked": int(W * H),
+                       "frame_bit_identical": bool(np.array_equal(fb, gpu_frame)),
+                       "sample_rows_bit_identical": bool(np.array_equal(fb1, gpu_frame[0:H:step])),
+                       "pixels_differing": int(np.count_nonzero((fb != gpu_frame).any(axis=2))),
+                       "max_abs_diff": float(np.nanmax(diff)) if diff.size else 0.0,
+                       "within_tolerance": bool(np.allclose(fb, gpu_frame, atol=1e-4, rtol=0)),
+                       "oracle_rays": int(st2["primary"] + st2["bounce"])})
     # build baseline: reference-faithful 32 x 1-bit split sort + Karras + refit on a 1M-triangle sample
     n_s = 1_000_000
     sub = rt.Scene(scene.vertices[: 3 * n_s], scene.indices[: 3 * n_s], scene.mat_indices[:n_s], scene.materials)
@@ -150,7 +209,7 @@ def cpu_baseline(rt, scene, ctx, wl, W, H):
     dt = time.perf_counter() - t0
     res["build_mtris_s"] = sub.num_tris / dt / 1e6
     res["build_sample"] = f"orc_build (32 split passes + Karras + refit) on {sub.num_tris} triangles, {dt:.2f} s, 1 thread"
-    return res
+    return res, parity
 
 
 def main():
@@ -176,7 +235,6 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -350,39 +408,65 @@ def main():
     cst = counts(mode_flags)
     rst = counts(modes["reference-order"])
     ctx.set_flags(rt.FLAG_TIMING)
-    kern = {"k_primary": dict(ms=tst["ms_stage"][5], bytes=trace_bytes(cst, "k_primary"))}
+    wide = use_name.endswith("wide")
+    kern = {"k_primary": dict(ms=tst["ms_stage"][5], bytes=layout_bytes(cst, "k_primary", wide_primary=wide))}
     if bounces:   # 1 bounce: the first pass's traversal kernel has its own events
-        kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7],
-                                     bytes=trace_bytes(cst, "k_bounce_trav", wide=use_name.endswith("wide")))
+        kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7], bytes=layout_bytes(cst, "k_bounce_trav"))
         kern["k_bounce_shade"] = dict(ms=tst["ms_stage"][6] - tst["ms_stage"][7],
-                                      bytes=trace_bytes(cst, "k_bounce_shade"))
+                                      bytes=layout_bytes(cst, "k_bounce_shade"))
     dom = max(kern, key=lambda k: kern[k]["ms"])
+    # HBM traffic: the PMC bytes of each kernel from the rocprofv3 passes of the same mode at N = 1
+    # (profiles/pmc_c5_<mode>.json), per record fetch x this launch's record fetches (at N = 1 the
+    # profiled launch itself; at N > 1 a rank's launch fetches fewer records)
+    recs = {"k_primary": sum(cst["packet_steps"]) or (cst["internal_visits"][0] + cst["leaf_visits"][0]),
+            "k_bounce_trav": cst["internal_visits"][1] + cst["leaf_visits"][1],
+            "k_bounce_shade": cst["bounce_rays"]}
     for k, v in kern.items():
         v["achieved_gbs"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
-    traffic = load_pmc(args.workload, use_name, dom)
-    roofline = {"bound": "hbm", "achieved": round(kern[dom]["achieved_gbs"], 1), "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": round(kern[dom]["achieved_gbs"] / PEAK_HBM_GBS, 4),
-                "traffic": traffic, "kernel": dom, "kernel_ms": round(kern[dom]["ms"], 4),
-                "algorithmic_bytes": int(kern[dom]["bytes"])}
-    if traffic:
-        # the algorithmic bytes are node/leaf bytes per visit; the upper tree levels stay in
-        # L2, so the measured HBM rate (PMC bytes of the same kernel) is the second number
-        tg = traffic / (kern[dom]["ms"] * 1e-3) / 1e9
-        roofline.update({"traffic_gbs": round(tg, 1), "traffic_frac": round(tg / PEAK_HBM_GBS, 4),
-                         "cache_served_frac": round(max(0.0, 1.0 - traffic / kern[dom]["bytes"]), 4)})
-    if dom == "k_bounce_trav":
-        # the roofline of a dependent-gather walk: one 64-B record per step (QNode or leaf), at
-        # the measured random-record rates of L2 and of HBM/Infinity Cache, split by the L2 hit
-        # fraction of the same kernel (PMC); frac = model time / measured time
-        pc = load_pmc(args.workload, use_name, dom, counters=True)
-        recs = cst["internal_visits"][1] + cst["leaf_visits"][1]
-        if pc and pc.get("TCC_HIT_sum") is not None and pc.get("TCC_MISS_sum"):
-            h = pc["TCC_HIT_sum"] / (pc["TCC_HIT_sum"] + pc["TCC_MISS_sum"])
-            model_ms = recs * (h / GATHER_L2_RPS + (1 - h) / GATHER_HBM_RPS) * 1e3
-            roofline["gather"] = {"records": int(recs), "l2_hit_frac": round(h, 4),
-                                  "peak_records_per_s": {"l2": GATHER_L2_RPS, "hbm": GATHER_HBM_RPS},
-                                  "model_ms": round(model_ms, 4), "kernel_ms": round(kern[dom]["ms"], 4),
-                                  "frac": round(model_ms / kern[dom]["ms"], 4)}
+        v["frac"] = v["achieved_gbs"] / PEAK_HBM_GBS
+        pm = load_pmc(args.workload, use_name, k)
+        v["traffic"] = None
+        if pm and pm.get("records_per_launch") and recs.get(k):
+            v["traffic"] = pm["hbm_bytes_per_launch"] / pm["records_per_launch"] * recs[k]
+            v["traffic_gbs"] = v["traffic"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
+            v["traffic_frac"] = v["traffic_gbs"] / PEAK_HBM_GBS
+    kd = kern[dom]
+    roofline = {"bound": "hbm", "achieved": round(kd["achieved_gbs"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(kd["frac"], 4),
+                "traffic": kd["traffic"], "kernel": dom, "kernel_ms": round(kd["ms"], 4),
+                "algorithmic_bytes": int(kd["bytes"]),
+                "bytes_model": "layout bytes: 64 B per record fetch (QNode, child-pair record, leaf record; "
+                               "a 4-wide primary step = 2) + per-ray queue/hit/colour bytes (DESIGN.md 7.1)",
+                "traffic_source": f"PMC profiles/pmc_{args.workload}_{use_name}.json (N=1), per record fetch x "
+                                  f"this launch's {recs[dom]} record fetches" if kd["traffic"] else None}
+    if kd["traffic"]:
+        roofline.update({"traffic_gbs": round(kd["traffic_gbs"], 1), "traffic_frac": round(kd["traffic_frac"], 4),
+                         "cache_served_frac": round(max(0.0, 1.0 - kd["traffic"] / kd["bytes"]), 4)})
+    pm = load_pmc(args.workload, use_name, dom)
+    if dom == "k_bounce_trav" and pm and pm.get("counters", {}).get("TCC_HIT_sum") is not None \
+            and pm.get("records_per_launch"):
+        # the roofline of a dependent-gather walk, per L2 REQUEST: the measured random-record
+        # request rates of L2 and of HBM/Infinity Cache (scripts/gather_roofline.hip) x the PMC
+        # L2 hits and misses of the same kernel, scaled to this launch's record fetches
+        c = pm["counters"]
+        scale = recs[dom] / pm["records_per_launch"]
+        hits, miss = c["TCC_HIT_sum"] * scale, c["TCC_MISS_sum"] * scale
+        model_ms = (hits / GATHER_L2_RPS + miss / GATHER_HBM_RPS) * 1e3
+        roofline["gather"] = {"l2_requests": int(hits + miss), "record_fetches": int(recs[dom]),
+                              "l2_hit_frac": round(hits / (hits + miss), 4),
+                              "peak_requests_per_s": {"l2": GATHER_L2_RPS, "hbm": GATHER_HBM_RPS},
+                              "model_ms": round(model_ms, 4), "kernel_ms": round(kd["ms"], 4),
+                              "frac": round(model_ms / kd["ms"], 4)}
+    # the build's roofline: SURVEY 8(d)'s 348 B per triangle, and the PMC bytes of its kernels
+    bp = build_pmc(args.workload, use_name)
+    build_roofline = {"bound": "hbm", "bytes_model": "SURVEY 8(d) B_build = 348 B per triangle",
+                      "algorithmic_bytes": int(S_BUILD_PER_TRI * scene.num_tris), "ms": round(bst["ms_build"], 4),
+                      "achieved": round(S_BUILD_PER_TRI * scene.num_tris / (bst["ms_build"] * 1e-3) / 1e9, 1),
+                      "peak": PEAK_HBM_GBS, "unit": "GB/s"}
+    build_roofline["frac"] = round(build_roofline["achieved"] / PEAK_HBM_GBS, 4)
+    if bp:
+        build_roofline.update({"traffic": bp["hbm_bytes"], "traffic_per_kernel_gb": bp["per_kernel_gb"],
+                               "traffic_vs_algorithmic": round(bp["hbm_bytes"] / build_roofline["algorithmic_bytes"], 3)})
     fb = frame_bytes(rst)
     # SURVEY 8(d)'s whole-frame figure prices the REFERENCE-ORDER walk's visits; a traversal
     # that visits fewer nodes than that walk can exceed 1 here, so it is reported beside the
@@ -396,6 +480,28 @@ def main():
     result = None
     if rank == 0:
         extras = {}
+        if world == 1 and not args.no_extras:
+            # the reference's frame (Graphics.cpp:56, :667-831): rebuild the BVH and trace, one frame
+            # at a time behind a fence (rtbvh_compute_bvh is synchronous), in the reported mode;
+            # then the same frame replayed as one hipGraph (RTBVH_FLAG_GRAPH)
+            reb = {"workload": wl["name"] + ", BVH rebuilt every frame", "mode": use_name}
+            for key, fl in (("", rt.FLAG_TIMING), ("_graph", rt.FLAG_GRAPH)):
+                ctx.set_flags(fl | mode_flags)
+                ctx.compute_bvh(W, H, bounces)
+                ctx.compute_bvh(W, H, bounces)
+                nfr = max(5, args.steps // 2)
+                t0 = time.perf_counter()
+                for _ in range(nfr):
+                    ctx.compute_bvh(W, H, bounces)
+                dt = (time.perf_counter() - t0) / nfr
+                q = ctx.stats()
+                rk = q["primary_rays"] + q["bounce_rays"]
+                reb["ms_per_frame" + key] = round(dt * 1e3, 4)
+                reb["mrays_s" + key] = round(rk / dt / 1e6, 1)
+                reb["frames" + key] = nfr
+            reb["rays_per_frame"] = int(rk)
+            extras["c5_frame_rebuild" if args.workload == "c5" else "frame_rebuild"] = reb
+            ctx.set_flags(rt.FLAG_TIMING | mode_flags)
         if world == 1 and not args.no_extras and args.workload == "c5":
             # C4: 10M synthetic (seed 0x5EED0004, +-50) build only; C3: Test.obj 1080p primary+1 bounce
             c4 = rt.synthetic(10_000_000, seed=0x5EED0004, half_extent=(50.0, 50.0, 50.0))
@@ -445,10 +551,12 @@ def main():
                                           "mrays_s_build_plus_trace_wall": round(rk / dt / 1e6, 1),
                                           "mrays_s_build_plus_trace_wall_graph": round(rk / dtg / 1e6, 1),
                                           "ms_build": round(q2["ms_build"], 4), "ms_trace": round(q2["ms_trace"], 4)}
-        cpu = None
+        cpu = parity = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline (oracle, bounded sample) ...")
-            cpu = cpu_baseline(rt, scene, ctx, wl, W, H)
+            gpu_frame = use["frame"].cpu().numpy() if use["frame"] is not None else None
+            cpu, parity = cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame)
+            del gpu_frame
         result = {
             "metric": "Mrays/s primary+1-bounce (C5 frame); BVH build Mtris/s under build",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
@@ -459,9 +567,12 @@ def main():
                        "triangles": scene.num_tris, "rays_per_step": int(rays_per_step),
                        "parallelism": f"image bands x{world} + RCCL gather" if world > 1 else "single GPU"},
             "roofline": roofline,
+            "build_roofline": build_roofline,
+            "parity": parity,
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kern.items()},
             "visits": {"internal": cst["internal_visits"], "leaf": cst["leaf_visits"], "hits": cst["hits"],
+                       "primary_packet_steps": cst["packet_steps"],
                        "reference_order_internal": rst["internal_visits"], "reference_order_leaf": rst["leaf_visits"]},
             "frame_roofline": frame_roofline,
             "traversal": traversal,

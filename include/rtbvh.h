@@ -179,6 +179,9 @@ typedef struct {
     uint64_t graph_captures;   /* RTBVH_FLAG_GRAPH: frames captured so far (a replay captures nothing) */
     uint32_t walk_flags;       /* the walk flags the next trace uses (after RTBVH_FLAG_AUTO_WALK) */
     uint32_t reserved;
+    /* RTBVH_FLAG_COUNT_VISITS, wave-packet primary walks: wave steps (one record fetch for the
+     * wave each) at internal nodes [0] and at leaves [1] */
+    uint64_t packet_steps[2];
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 

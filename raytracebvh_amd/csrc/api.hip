@@ -1166,6 +1166,12 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         out->trav_active_lanes = cnt[12];
     }
     out->graph_captures = c->graph_captures;
+    if (c->traced && c->d_counters) {
+        unsigned long long w[2];
+        HIPC(c, hipMemcpy(w, c->d_counters + 64 * c->last_slot + 14, sizeof(w), hipMemcpyDeviceToHost));
+        out->packet_steps[0] = w[0];
+        out->packet_steps[1] = w[1];
+    }
     out->walk_flags = effective_flags(c) & WALK_FLAGS;
     return RTBVH_OK;
 }

@@ -34,7 +34,7 @@ namespace {
 constexpr uint32_t BLOCK = 256;
 constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
 
-struct Counts { uint32_t internal, leaf, overflow; };
+struct Counts { uint32_t internal, leaf, overflow, wint, wleaf; };   // w*: packet wave steps (lane 0)
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -206,6 +206,7 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
             const v16f q = sload16(leaf + 4 * (size_t)j);
+            if (COUNT && lane == 0) c.wleaf++;
             if (mask & lanebit) {
                 if (COUNT) c.leaf++;
                 const float t = ray_triangle(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]));
@@ -218,6 +219,7 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
             pop = true;
         } else {
             const v16f q = sload16(inner + node);
+            if (COUNT && lane == 0) c.wint++;
             const uint32_t own = __float_as_uint(q[14]);
             const uint32_t cl = child_slot(__float_as_uint(q[12]), own, 0), cr = child_slot(__float_as_uint(q[13]), own, 1);
             bool lh = false, rh = false;
@@ -313,6 +315,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
             const v16f q = sload16(leaf + 4 * (size_t)j);
+            if (COUNT && lane == 0) c.wleaf++;
             if (mask & lanebit) {
                 if (COUNT) c.leaf++;
                 const float t = ray_triangle(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]));
@@ -327,6 +330,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
         } else {
             const v16f A = sload16(inner4 + 2 * (size_t)node);
             const v16f B = sload16(inner4 + 2 * (size_t)node + 1);
+            if (COUNT && lane == 0) c.wint++;
             uint32_t id[4] = {__float_as_uint(A[12]), __float_as_uint(A[13]), __float_as_uint(B[12]),
                               __float_as_uint(B[13])};
             if (COUNT && (mask & lanebit)) c.internal++;
@@ -523,13 +527,14 @@ __device__ __forceinline__ uint32_t wave_append(bool active, uint32_t* counter) 
 }
 
 // counters: [base] internal visits, [base+1] leaf visits, [base+2] hits (base 2 primary,
-// 5 bounce), [8] stack overflows / guard trips (also added to *overflow), [9] textured hits
+// 5 bounce), [8] stack overflows / guard trips (also added to *overflow), [9] textured hits,
+// [14] / [15] internal / leaf wave steps of the primary packet walks (one record fetch each)
 template <bool COUNT>
 __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c, uint32_t hits, uint32_t tex,
                                              int base) {
-    unsigned long long v[5] = {c.internal, c.leaf, hits, c.overflow, tex};
+    unsigned long long v[7] = {c.internal, c.leaf, hits, c.overflow, tex, c.wint, c.wleaf};
 #pragma unroll
-    for (int k = 0; k < 5; k++)
+    for (int k = 0; k < 7; k++)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
     if (lane_id() == 0) {
@@ -538,6 +543,10 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
             atomicAdd(&a.counters[base + 1], v[1]);
             atomicAdd(&a.counters[base + 2], v[2]);
             atomicAdd(&a.counters[9], v[4]);
+            if (v[5] | v[6]) {   // wave steps of the primary packet walks
+                atomicAdd(&a.counters[14], v[5]);
+                atomicAdd(&a.counters[15], v[6]);
+            }
         }
         if (v[3]) {
             atomicAdd(&a.counters[8], v[3]);
@@ -560,7 +569,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     const uint32_t y = band * 8 + (lane >> 3);
     const bool valid = x < a.W && y < a.H;
     const size_t out = ((size_t)k * 8 + (lane >> 3)) * a.W + x;
-    Counts c = {0, 0, 0};
+    Counts c = {0, 0, 0, 0, 0};
     uint32_t hits = 0, tex = 0;
     bool live = false;
     RayQ e;
@@ -629,7 +638,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __
                                                      const uint32_t* __restrict__ perm, RayQ* __restrict__ qout,
                                                      uint32_t* __restrict__ qout_count, int emit) {
     const uint32_t n = *qin_count;
-    Counts c = {0, 0, 0};
+    Counts c = {0, 0, 0, 0, 0};
     uint32_t hits = 0, tex = 0;
     for (uint32_t base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
         const uint32_t i = base + threadIdx.x;
@@ -728,7 +737,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     const uint32_t n = *qin_count;
     const uint32_t lane = lane_id();
-    Counts c = {0, 0, 0};
+    Counts c = {0, 0, 0, 0, 0};
     bool has = false, hit = false;
     uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
     int sp = 0;
@@ -1012,7 +1021,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
     const uint32_t slot = wave_append(emit && live, qout_count);
     if (emit && live) qout[slot] = e;
     if (COUNT) {
-        Counts c = {0, 0, 0};
+        Counts c = {0, 0, 0, 0, 0};
         flush_counts<COUNT>(a, c, hits, tex, 5);
     }
 }

@@ -17,6 +17,8 @@ if [ -z "$SKIP_PROF" ]; then
   echo "prof ok"
 fi
 if [ -n "$PMC_MODE" ]; then
+  PROF_MODE=$PMC_MODE PROF_ITERS=1 PROF_COUNTS=$R/gpurun_out/counts_round.json timeout -k 10 300 python3 scripts/profile_trace.py > gpurun_out/counts_round.log 2>&1 || { echo "COUNTS FAILED"; tail -5 gpurun_out/counts_round.log; exit 1; }
   PMC_OUT=pmc_round MODES="$PMC_MODE" SETS="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum;TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_DRAM_sum;TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum;FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU;SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" bash scripts/gpu_pmc.sh || exit 1
+  python3 scripts/make_pmc_json.py gpurun_out/pmc_round "$PMC_MODE" c5 gpurun_out/pmc_c5_round.json gpurun_out/counts_round.json || exit 1
 fi
 echo "round ok"

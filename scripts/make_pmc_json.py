@@ -10,7 +10,9 @@ guide says) and a permutation gather of 64-B records (the traversal's node-recor
 pattern) issues one 128-B request per record, i.e. 2x the record bytes, while
 FETCH_SIZE (= RDREQ x 64 B) reports exactly the record bytes.  Counters are summed
 over the TCC channels and averaged over the profiled dispatches of each kernel.
-Usage: make_pmc_json.py PMC_DIR MODE WORKLOAD OUT.json"""
+records_per_launch (optional COUNTS.json: the stats of one PROF_COUNTS trace of the same mode)
+is each kernel's record fetches, so bench.py can scale the bytes to another launch's fetches.
+Usage: make_pmc_json.py PMC_DIR MODE WORKLOAD OUT.json [COUNTS.json]"""
 import collections
 import csv
 import glob
@@ -19,6 +21,7 @@ import os
 import sys
 
 d, mode, workload, out = sys.argv[1:5]
+counts = json.load(open(sys.argv[5])) if len(sys.argv) > 5 else None
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(d, f"p*_{mode}", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
@@ -35,6 +38,11 @@ for k, cs in acc.items():
     base = k.split("<")[0]
     e = {"instance": k, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
          "hbm_bytes_per_launch": rd + wr, "counters": m}
+    if counts:
+        e["records_per_launch"] = {
+            "k_primary": sum(counts["packet_steps"]) or counts["internal_visits"][0] + counts["leaf_visits"][0],
+            "k_bounce_trav": counts["internal_visits"][1] + counts["leaf_visits"][1],
+            "k_bounce_shade": counts["bounce_rays"]}.get(base)
     if base not in kern or e["hbm_bytes_per_launch"] > kern[base]["hbm_bytes_per_launch"]:
         kern[base] = e
 json.dump({"workload": workload, "mode": mode, "source": d,

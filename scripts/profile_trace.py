@@ -25,4 +25,10 @@ with rt.Context(device=0, flags=flags) as c:
         c.trace(W, H, 1)
     if flags & rt.FLAG_COUNT_VISITS:
         print(c.stats())
+    out = os.environ.get("PROF_COUNTS")   # one more trace with visit counts (run this outside rocprofv3)
+    if out:
+        import json
+        c.set_flags(flags | rt.FLAG_COUNT_VISITS)
+        c.trace(W, H, 1)
+        json.dump(c.stats(), open(out, "w"))
 print("done", mode)

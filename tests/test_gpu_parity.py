@@ -363,6 +363,59 @@ def test_trace_synthetic_sampled_rows(mode):
     np.testing.assert_array_equal(inten, oint)
 
 
+C5_SCENE = dict(ntris=10_000_000, seed=0x5EED0005, half=(100, 100, 50))
+C4_SCENE = dict(ntris=10_000_000, seed=0x5EED0004, half=(50, 50, 50))
+
+
+def _oracle_threads():
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)))
+
+
+@pytest.mark.parametrize("cfg", ["C4", "C5"])
+def test_10m_tree_matches_oracle(cfg):
+    """BASELINE C4 / C5 at full size (10M triangles): the GPU tree equals the oracle's own build
+    of the same scene in every field of every one of the 2n-1 nodes (Morton codes, sorted
+    order, Karras links, refit boxes)."""
+    p = C4_SCENE if cfg == "C4" else C5_SCENE
+    s = rt.synthetic(p["ntris"], seed=p["seed"], half_extent=p["half"])
+    wvp, wv = rt.camera_reference(1920, 1080) if cfg == "C4" else rt.camera_reference(3840, 2160)
+    with rt.Context(device=0) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.build()
+        nodes = c.read_bvh()
+    onodes = orc.build(_oscene(s), wvp)
+    for f in ("parent", "child_l", "child_r", "code", "index", "bb_min", "bb_max"):
+        assert np.array_equal(nodes[f], onodes[f]), f
+
+
+@pytest.mark.parametrize("mode", ["nearest+packet+wide", "auto"])
+def test_c5_frame_matches_oracle_sampled_rows(mode):
+    """The headline frame at full size (C5: 10M triangles, 3840x2160, primary + 1 bounce) in the
+    bench's walk, against the oracle tracing 1 row in 4 on its OWN tree (OpenMP over rows):
+    bit-identical pixels and intensities (tolerance 1e-4 stated)."""
+    s = rt.synthetic(C5_SCENE["ntris"], seed=C5_SCENE["seed"], half_extent=C5_SCENE["half"])
+    W, H = 3840, 2160
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=TRACE_MODES[mode]) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        fb = c.read_framebuffer()
+        inten = c.read_intensity()
+    os_ = _oscene(s)
+    onodes = orc.build(os_, wvp)
+    orc.set_threads(_oracle_threads())
+    try:
+        ofb, oint, ost = orc.trace(os_, onodes, wvp, wv, W, H, 1, 1, H, 4, want_intensity=True)
+    finally:
+        orc.set_threads(1)
+    np.testing.assert_allclose(fb[1::4], ofb, atol=RGB_TOL, rtol=0)
+    assert np.array_equal(fb[1::4], ofb)
+    np.testing.assert_array_equal(inten[1::4], oint)
+    assert ost["hits"] > 100_000 and ost["bounce"] > 100_000
+
+
 def test_trace_c5_full_frame_modes_agree():
     """C5 at full size (10M triangles, 3840x2160, primary + 1 bounce): every traversal
     mode renders the identical frame (the reference-order mode is bit-exact vs the
