@@ -281,6 +281,7 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     const uint32_t lim = c->cfg.stack_limit;
     a.stack_limit = lim && lim < (uint32_t)STACK_SIZE ? (int)lim : STACK_SIZE;
     a.stack_limit4 = lim && lim < (uint32_t)STACK4 ? (int)lim : STACK4;
+    a.limited = lim != 0 && lim < (uint32_t)STACK4;
     return a;
 }
 

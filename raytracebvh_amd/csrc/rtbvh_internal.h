@@ -90,6 +90,7 @@ struct TraceArgs {
     unsigned long long* counters;   // [64] per trace: see flush_counts (trace.hip) and rtbvh_get_stats
     unsigned long long* overflow;   // stack overflows / guard trips, accumulated over every trace (never reset)
     int stack_limit, stack_limit4;  // stack entries the binary / 4-wide walks may use (<= STACK_SIZE / STACK4)
+    bool limited;                   // a limit below a capacity: the kernels read the limits (else constants)
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)

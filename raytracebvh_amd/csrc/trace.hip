@@ -555,11 +555,14 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
     }
 }
 
-// RayTraceLaunch.hlsl:6-93
-template <bool COUNT, int K>
+// RayTraceLaunch.hlsl:6-93.  LIM: a run-time stack limit (rtbvh_config.stack_limit); without
+// it the limit is the compiled capacity, a constant (a run-time limit kept in the walk loop
+// costs the SGPR-bound packet walks a kernel-argument reload per step)
+template <bool COUNT, int K, bool LIM>
 __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restrict__ q, uint32_t* __restrict__ qcount,
                                                       int emit) {
     using PW = PrimaryWalk<K>;
+    const int lim = LIM ? a.stack_limit : STACK_SIZE, lim4 = LIM ? a.stack_limit4 : STACK4;
     constexpr int PST = PW::WIDE ? 3 * STACK4 : 3 * STACK_SIZE;   // per-wave packet stack words
     __shared__ uint32_t s_pst[PW::PACKET ? 4 * PST : 1];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -581,16 +584,15 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     uint32_t bl = 0;
     bool phit = false;
     if (PW::WIDE)     // whole wave, before any divergence
-        phit = traverse_packet4<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, a.stack_limit4, best, bl, c,
-                                       s_pst + w * PST);
+        phit = traverse_packet4<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c, s_pst + w * PST);
     else if (PW::PACKET)
-        phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, a.stack_limit, best, bl,
-                                                   c, s_pst + w * PST);
+        phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, lim, best, bl, c,
+                                                   s_pst + w * PST);
     if (valid) {
         float4 color;
         float intensity = 0.f;
         if (PW::PACKET ? phit
-                       : traverse<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, a.stack_limit, best, bl, c)) {
+                       : traverse<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, lim, best, bl, c)) {
             hits = 1;
             const HitInfo h = shade_hit(a, bl, o, d, best);
             tex = h.textured;
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
 
 // RayTraceReflection.hlsl:6-62 over the compacted queue of live rays (in `perm`
 // order when the queue was sorted for coherence), one ray per lane
-template <bool COUNT, bool NEAREST>
+template <bool COUNT, bool NEAREST, bool LIM>
 __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __restrict__ qin,
                                                      const uint32_t* __restrict__ qin_count,
                                                      const uint32_t* __restrict__ perm, RayQ* __restrict__ qout,
@@ -652,7 +654,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __
             uint32_t bl;
             float4 col = a.color[e.idx];
             float intensity = e.intensity;
-            if (traverse<COUNT, NEAREST>(a.inner, a.leaf, a.T, o, d, inv, a.stack_limit, best, bl, c)) {
+            if (traverse<COUNT, NEAREST>(a.inner, a.leaf, a.T, o, d, inv, LIM ? a.stack_limit : STACK_SIZE, best, bl,
+                                         c)) {
                 hits++;
                 const HitInfo h = shade_hit(a, bl, o, d, best);
                 tex += h.textured;
@@ -724,7 +727,7 @@ __device__ __forceinline__ float bf16_up(uint16_t h) { return __uint_as_float((u
 constexpr int SB = 16;   // 16 x 4 B x 256 lanes = 16 KB per block
 constexpr int SW = 12;   // 12 x 6 B x 256 lanes = 18 KB per block (8 blocks per CU)
 
-template <bool COUNT, int MODE>
+template <bool COUNT, int MODE, bool LIM>
 __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
@@ -733,8 +736,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          unsigned long long* __restrict__ overflow, int limit) {
+                                                          unsigned long long* __restrict__ overflow, int stack_limit) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
+    const int limit = LIM ? stack_limit : WIDE ? STACK4 : STACK_SIZE;
     const uint32_t n = *qin_count;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0, 0, 0};
@@ -1098,7 +1102,8 @@ __global__ __launch_bounds__(BLOCK) void k_count_diff(const uint4* __restrict__ 
 
 template <bool COUNT, int K>
 void launch_primary_t(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool emit, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_primary<COUNT, K>), grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
+    if (a.limited) hipLaunchKernelGGL((k_primary<COUNT, K, true>), grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
+    else hipLaunchKernelGGL((k_primary<COUNT, K, false>), grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
 }
 template <int K>
 void launch_primary_c(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, dim3 grid, hipStream_t s) {
@@ -1109,9 +1114,13 @@ void launch_primary_c(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count,
 template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           float2* hitrec, uint32_t* next, uint32_t blocks, hipStream_t s) {
-    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, a.T,
-                       qin, qin_count, perm, hitrec, next, a.counters, a.overflow,
-                       MODE == 2 ? a.stack_limit4 : a.stack_limit);
+    const int lim = MODE == 2 ? a.stack_limit4 : a.stack_limit;
+    if (a.limited)
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, true>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf,
+                           a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim);
+    else
+        hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, false>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode,
+                           a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim);
 }
 
 }  // namespace
@@ -1135,9 +1144,15 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
                    uint32_t* qout_count, bool count, bool emit, bool nearest, hipStream_t s) {
     const uint32_t blocks = 2048;   // 8 waves/SIMD x 1024 SIMDs / 4 waves per block; grid-stride over the queue
-#define RTBVH_BNC(C, N)                                                                                            \
-    hipLaunchKernelGGL((k_bounce<C, N>), dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, perm, qout, qout_count, \
-                       (int)emit)
+#define RTBVH_BNC(C, N)                                                                                          \
+    do {                                                                                                           \
+        if (a.limited)                                                                                             \
+            hipLaunchKernelGGL((k_bounce<C, N, true>), dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, perm, qout, \
+                               qout_count, (int)emit);                                                           \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_bounce<C, N, false>), dim3(blocks), dim3(BLOCK), 0, s, a, qin, qin_count, perm,     \
+                               qout, qout_count, (int)emit);                                                     \
+    } while (0)
     if (count) { if (nearest) RTBVH_BNC(true, true); else RTBVH_BNC(true, false); }
     else { if (nearest) RTBVH_BNC(false, true); else RTBVH_BNC(false, false); }
 #undef RTBVH_BNC
