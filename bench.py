@@ -281,7 +281,7 @@ def main():
     build = {"workload": f"{scene.num_tris} tris (bench scene)", "ms": bst["ms_build"],
              "mtris_s": scene.num_tris / (bst["ms_build"] * 1e-3) / 1e6,
              "achieved_gbs": round(S_BUILD_PER_TRI * scene.num_tris / (bst["ms_build"] * 1e-3) / 1e9, 1),
-             "stages_ms": dict(zip(["bounds", "morton", "sort", "leaf_karras", "refit"],
+             "stages_ms": dict(zip(["bounds", "morton", "sort", "karras", "refit"],
                                    [round(x, 4) for x in bst["ms_stage"][:5]]))}
 
     # ---- frames in flight: frame i is traced on streams[i % inflight] (stream 0 is the

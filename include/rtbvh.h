@@ -167,7 +167,8 @@ typedef struct {
      * the context stream since rtbvh_reset_stats (the most recent 32 of each) */
     uint32_t timed_builds, timed_traces;
     float ms_build, ms_trace;
-    float ms_stage[8];   /* bounds, morton, sort, leaf+karras, refit, primary, bounce (all passes),
+    float ms_stage[8];   /* 0 (the mesh box is computed by set_scene), morton, sort, karras, refit (+ leaf and node
+                            records, QNodes), primary, bounce (all passes),
                             first bounce pass's traversal kernel (RTBVH_FLAG_REFILL_BOUNCE) */
     /* RTBVH_FLAG_COUNT_VISITS with RTBVH_FLAG_REFILL_BOUNCE: wave iterations of the bounce
      * traversal, those with both a leaf lane and an internal-node lane, and active lanes

@@ -52,6 +52,7 @@ struct rtbvh_ctx {
     float* d_refr_rec = nullptr;             //   RayPresent records, 14 floats per traced pixel
     size_t cap_rec = 0, rec_P = 0;           // record capacity; pixels of the last records trace
     uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr;
+    uint32_t *d_cross = nullptr, *d_cross_count = nullptr;   // k_refit's list of block-crossing nodes
     unsigned long long* d_ovf = nullptr;     // stack overflows + guard trips of every trace (never reset)
     unsigned long long* h_ovf = nullptr;     // pinned: a snapshot of *d_ovf copied at the end of each trace,
                                              //   one word per slot; ovf_seen: the value last reported
@@ -166,6 +167,8 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
     HIPC(c, dalloc(c->d_cnt, ni));
+    HIPC(c, dalloc(c->d_cross, ni));
+    HIPC(c, dalloc(c->d_cross_count, 1));
     HIPC(c, dalloc(c->d_bounds, BOUNDS_WORDS));
     HIPC(c, dalloc(c->d_rootbox, 8));
     c->cap_T = T;
@@ -249,6 +252,8 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.refit_cnt = c->d_cnt;
     a.rootbox = c->d_rootbox;
     a.qnode = c->d_qnode;
+    a.cross = c->d_cross;
+    a.cross_count = c->d_cross_count;
     return a;
 }
 
@@ -578,6 +583,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode);
     dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_bounds); dfree(c->d_rootbox);
+    dfree(c->d_cross); dfree(c->d_cross_count);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
     dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);
@@ -661,6 +667,16 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
     c->nmat = nmats;
     rtbvh_status st = ensure_build_capacity(c, T);
     if (st) return st;
+    if (c->cfg.morton_mode == RTBVH_MORTON_CPUTESTS) {
+        // the object-space mesh box the CPUTests Morton codes are normalised by: a property of
+        // the scene, computed once after loading as ShaderSim does (ShaderSim/main.cpp:277-285),
+        // not per build (it does not depend on the camera)
+        BuildArgs a = build_args(c);
+        launch_bounds(a, c->stream);
+        st = check_launch(c, "mesh bounds");
+        if (st) return st;
+        HIPC(c, hipStreamSynchronize(c->stream));
+    }
     c->have_scene = true;
     c->built = false;
     return RTBVH_OK;
@@ -707,10 +723,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         c->built = true;
         return check_launch(c, "build kernel");
     }
-    if (c->cfg.morton_mode == RTBVH_MORTON_CPUTESTS) {
-        launch_bounds(a, s);
-    }
-    if (timing) HIPC(c, hipEventRecord(ev[1], s));
+    if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
     launch_morton(a, s);
     if (timing) HIPC(c, hipEventRecord(ev[2], s));
     c->sorted = radix_sort_pairs(c->d_codes, c->d_ids, c->d_ka, c->d_va, c->d_kb, c->d_vb, c->T, 30,
@@ -718,11 +731,11 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (timing) HIPC(c, hipEventRecord(ev[3], s));
     a.sorted_keys = c->sorted.keys;
     a.sorted_vals = c->sorted.vals;
-    launch_leaf_karras(a, s);
+    launch_karras(a, s);
     if (timing) HIPC(c, hipEventRecord(ev[4], s));
     if (c->T > 1) HIPC(c, hipMemsetAsync(c->d_cnt, 0, sizeof(uint32_t) * (c->T - 1), s));
-    launch_refit(a, s);
-    launch_qnodes(a, s);   // timed with the refit stage
+    HIPC(c, hipMemsetAsync(c->d_cross_count, 0, sizeof(uint32_t), s));
+    launch_refit(a, s);   // leaf records, boxes, node records and QNodes
     if (timing) HIPC(c, hipEventRecord(ev[5], s));
     if (timing) c->n_builds++;
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));

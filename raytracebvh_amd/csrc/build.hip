@@ -201,13 +201,14 @@ __device__ void karras_node(const C& c, uint32_t n, uint32_t i, uint4* __restric
 // leaf record of sorted position i: gather the clip-space triangle once, store
 // (v0, e1, e2) for the triangle test (the reference's edge1/edge2, :43-44) and
 // the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
-__device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i) {
+__device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i, f3& lo, f3& hi) {
     const uint32_t t = a.sorted_vals[i];
     const float4* src = a.tclip + 3 * (size_t)t;
     const float4 s0 = src[0], s1 = src[1], s2 = src[2];
     const f3 v0 = mk(s0.x, s0.y, s0.z), v1 = mk(s1.x, s1.y, s1.z), v2 = mk(s2.x, s2.y, s2.z);
     const f3 e1 = sub(v1, v0), e2 = sub(v2, v0);
-    f3 lo = vmin(v0, v1), hi = vmax(v0, v1);
+    lo = vmin(v0, v1);
+    hi = vmax(v0, v1);
     lo = vmin(lo, v2);
     hi = vmax(hi, v2);
     float4* dst = a.leaf + 4 * (size_t)i;
@@ -216,18 +217,11 @@ __device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i) {
     dst[2] = make_float4(e2.z, __uint_as_float(t), lo.x, lo.y);
     dst[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
 }
+// BVHConstructP1.hlsl:167-188: internal node i for every i < T-1 (topology only: child ids,
+// leaf range, parent links); the root's parent is UINT_MAX (:186-187).  The leaf records are
+// written by the refit (k_refit), which gathers each leaf's triangle once.
 template <int MODE>
-__global__ __launch_bounds__(BLOCK) void k_leaf_karras(BuildArgs a) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= a.T) return;
-    leaf_record(a, i);
-    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
-    if (i == 0 && a.T > 1) a.pint[0] = INVALID;   // root (BVHConstructP1.hlsl:186-187)
-}
-
-// Karras only (for rtbvh_build_from_codes): leaf boxes come from the caller
-template <int MODE>
-__global__ __launch_bounds__(BLOCK) void k_karras_only(BuildArgs a) {
+__global__ __launch_bounds__(BLOCK) void k_karras(BuildArgs a) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
     if (i == 0 && a.T > 1) a.pint[0] = INVALID;
@@ -292,112 +286,44 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t parent_code, uint32_t T) {
     return parent_code == INVALID ? 2 * T - 2 : parent_code;
 }
 
-__device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, Inner* __restrict__ inner,
-                                            const uint4* __restrict__ topo,
-                                            const uint32_t* __restrict__ pint, uint32_t* __restrict__ cnt,
-                                            float* __restrict__ rootbox, Inner* __restrict__ rec, uint32_t T) {
+// the pseudo-record of leaf j, child `side` of node p (rtbvh_device.h: the 4-wide walks read a
+// leaf child's slot as a record whose two children are the leaf itself and nothing)
+__device__ __forceinline__ void store_leaf_record(Inner* rec, uint32_t p, uint32_t side, uint32_t leaf_id, f3 lo,
+                                                  f3 hi) {
+    store_record(rec + 2 * (size_t)p + side, lo, hi, lo, hi, leaf_id, INVALID, leaf_id);
+}
+
+// The global part of the climb, for the nodes whose leaf range crosses a refit workgroup:
+// the child box is handed over through inner[p] (sc1) and the second arriver writes p's
+// record (and the pseudo-records of p's leaf children), lists p for k_qnodes_list, and goes on.
+__device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, const BuildArgs& a) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
     for (int level = 0; level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
-        st_box_sc1(side ? inner[p].rmin : inner[p].lmin, lo, hi);
+        st_box_sc1(side ? a.inner[p].rmin : a.inner[p].lmin, lo, hi);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the box stores before the ticket
-        const uint32_t old = __hip_atomic_fetch_add(&cnt[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t old = __hip_atomic_fetch_add(&a.refit_cnt[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == 0) return;
         asm volatile("" ::: "memory");
         f3 smin, smax;
-        ld_box_sc1(side ? inner[p].lmin : inner[p].rmin, smin, smax);
-        e = pint[p];
-        const uint4 ids = topo[p];
-        if (side) store_record(rec + slot_of(e, T), smin, smax, lo, hi, ids.x, ids.y, p);
-        else      store_record(rec + slot_of(e, T), lo, hi, smin, smax, ids.x, ids.y, p);
+        ld_box_sc1(side ? a.inner[p].lmin : a.inner[p].rmin, smin, smax);
+        e = a.pint[p];
+        const uint4 ids = a.topo[p];
+        const f3 l0 = side ? smin : lo, l1 = side ? smax : hi, r0 = side ? lo : smin, r1 = side ? hi : smax;
+        store_record(a.rec + slot_of(e, a.T), l0, l1, r0, r1, ids.x, ids.y, p);
+        if (ids.x & LEAF_BIT) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
+        if (ids.y & LEAF_BIT) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
+        a.cross[atomicAdd(a.cross_count, 1u)] = p;
         // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
-        if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
-        else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
-        if (e == INVALID) {
-            rootbox[0] = lo.x; rootbox[1] = lo.y; rootbox[2] = lo.z;
-            rootbox[3] = hi.x; rootbox[4] = hi.y; rootbox[5] = hi.z;
-            return;
-        }
-    }
-}
-
-// Block-local refit: the workgroup of leaves [a, a + BLOCK) joins every internal node
-// whose leaf range lies inside that block through LDS (ticket + both child boxes), so
-// only nodes whose range crosses a block boundary -- about log2(T / BLOCK) per leaf
-// path's top -- use the global sc1 hand-off of refit_climb.  Both children of a node
-// are climbed by threads of the same block exactly when the node's range is inside
-// the block, so a node takes one protocol for both of its arrivals.  The boxes still
-// go to the node's 64-B record in HBM (plain stores: read by later kernels only).
-__global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
-    __shared__ uint32_t s_cnt[BLOCK];
-    __shared__ float s_box[BLOCK][2][6];
-    __shared__ uint4 s_topo[BLOCK];   // the block's nodes [base, base + BLOCK): ids, leaf range
-    __shared__ uint32_t s_pint[BLOCK];
-    const uint32_t base = blockIdx.x * BLOCK;
-    const uint32_t i = base + threadIdx.x;
-    s_cnt[threadIdx.x] = 0;
-    if (i + 1 < a.T) {   // coalesced, so the in-block climb makes no dependent global loads
-        s_topo[threadIdx.x] = a.topo[i];
-        s_pint[threadIdx.x] = a.pint[i];
-    }
-    __syncthreads();
-    if (i >= a.T) return;
-    const float4* r = a.leaf + 4 * (size_t)i;
-    const float4 b0 = r[2], b1 = r[3];
-    f3 lo = mk(b0.z, b0.w, b1.x), hi = mk(b1.y, b1.z, b1.w);
-    if (a.T == 1) {
-        a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
-        a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
-        return;
-    }
-    uint32_t e = a.pleaf[i];
-    store_record(a.rec + e, lo, hi, lo, hi, LEAF_BIT | i, INVALID, LEAF_BIT | i);   // leaf pseudo-record
-    const uint32_t end = base + BLOCK;
-    for (int level = 0; level < 2 * STACK_SIZE; level++) {
-        const uint32_t p = e >> 1, side = e & 1u;
-        if (!(p >= base && p < end)) {   // leaves the block
-            refit_climb(lo, hi, e, a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
-            return;
-        }
-        const uint4 q3 = s_topo[p - base];   // ids, leaf range
-        const uint32_t pe = s_pint[p - base];
-        if (!(q3.z >= base && q3.w < end)) {   // p's range crosses the block
-            refit_climb(lo, hi, e, a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
-            return;
-        }
-        float* sb = s_box[p - base][side];
-        sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the LDS box lands before the ticket
-        const uint32_t old = atomicAdd(&s_cnt[p - base], 1u);
-        if (old == 0) return;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const float* ob = s_box[p - base][side ^ 1u];
-        const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
-        if (side) store_record(a.rec + slot_of(pe, a.T), smin, smax, lo, hi, q3.x, q3.y, p);
-        else      store_record(a.rec + slot_of(pe, a.T), lo, hi, smin, smax, q3.x, q3.y, p);
-        // union in (childL, childR) order, as the reference
-        if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
-        else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
-        e = pe;
+        lo = vmin(l0, r0);
+        hi = vmax(l1, r1);
         if (e == INVALID) {
             a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
             a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
             return;
         }
     }
-}
-
-__global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= a.T) return;
-    const float* b = boxes + 6 * (size_t)i;
-    const f3 lo = mk(b[0], b[1], b[2]), hi = mk(b[3], b[4], b[5]);
-    if (a.T == 1) {
-        for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
-        return;
-    }
-    refit_climb(lo, hi, a.pleaf[i], a.inner, a.topo, a.pint, a.refit_cnt, a.rootbox, a.rec, a.T);
 }
 
 // ---- quantized 4-wide nodes (rtbvh_device.h QNode) ---------------------------------
@@ -408,7 +334,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
 // pair).  Division-free: s and 1/s are built from exponent bits (both normal: s is in
 // [2^-120, 2^116] for |corners| <= 1e37), so (x - o) * (1/s) is exactly (x - o) / s.
 // PMC: the first form (correctly rounded divisions, frexpf/ldexpf) ran ~3,500 VALU per
-// node and made k_qnodes VALU-bound (0.90 ms at 10M nodes).
+// node and made the QNode pass VALU-bound (0.90 ms at 10M nodes).
 __device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
 __device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float (&hi)[4], float& org, float& scl,
                                               uint32_t& wlo, uint32_t& whi) {
@@ -442,13 +368,44 @@ __device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float 
     return true;
 }
 
+// the QNode of a node from its four grandchild boxes (x/y/z min and max per grandchild c) and
+// ids, written as four 16-B stores
+__device__ __forceinline__ void store_qnode(QNode* dst, const float (&lx)[4], const float (&ly)[4],
+                                            const float (&lz)[4], const float (&hx)[4], const float (&hy)[4],
+                                            const float (&hz)[4], uint4 ids) {
+    QNode q;
+    bool ok = quantize_axis(lx, hx, q.org[0], q.scl[0], q.lo[0], q.hi[0]);
+    ok = quantize_axis(ly, hy, q.org[1], q.scl[1], q.lo[1], q.hi[1]) && ok;
+    ok = quantize_axis(lz, hz, q.org[2], q.scl[2], q.lo[2], q.hi[2]) && ok;
+    if (!ok) q.scl[0] = 0.f;   // the traversal reads the exact pair for this node
+    q.id[0] = ids.x; q.id[1] = ids.y; q.id[2] = ids.z; q.id[3] = ids.w;
+    const float4* qs = reinterpret_cast<const float4*>(&q);
+    float4* d = reinterpret_cast<float4*>(dst);
+    d[0] = qs[0]; d[1] = qs[1]; d[2] = qs[2]; d[3] = qs[3];
+}
+
 // The QNode of internal node k from its record pair (slots 2k, 2k+1: the four grandchild
 // boxes and ids), written at k's own slot pint[k] (the root's: 2T-2), so that siblings'
-// nodes share a 128-B line as the records do.  Internal grandchild ids become their
-// slots (2 * their parent + side; the parent's index is word 14 of its record).  One
-// workgroup takes 256 consecutive pairs: coalesced loads into LDS (one float4 of padding
-// per pair: the per-node ds_read_b128 at a 144-B stride is bank-conflict free), then
-// one node per thread.
+// nodes share a 128-B line as the records do.  Internal grandchild ids become their slots
+// (2 * their parent + side; the parent's index is word 14 of its record).
+__device__ __forceinline__ void qnode_from_pair(const float4 (&r)[8], QNode* dst) {
+    const float4 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], b0 = r[4], b1 = r[5], b2 = r[6], b3 = r[7];
+    // record words (rtbvh_device.h): 0-1 l.min.xy 2-3 l.max.xy 4-5 r.min.xy 6-7 r.max.xy
+    // 8 l.min.z 9 l.max.z 10 r.min.z 11 r.max.z 12 id_l 13 id_r 14 own
+    const float lx[4] = {a0.x, a1.x, b0.x, b1.x}, ly[4] = {a0.y, a1.y, b0.y, b1.y}, lz[4] = {a2.x, a2.z, b2.x, b2.z};
+    const float hx[4] = {a0.z, a1.z, b0.z, b1.z}, hy[4] = {a0.w, a1.w, b0.w, b1.w}, hz[4] = {a2.y, a2.w, b2.y, b2.w};
+    const uint32_t ownl = __float_as_uint(a3.z), ownr = __float_as_uint(b3.z);
+    auto gslot = [](uint32_t id, uint32_t own, uint32_t side) {
+        return (id == INVALID || (id & LEAF_BIT)) ? id : 2 * own + side;
+    };
+    const uint4 ids = make_uint4(gslot(__float_as_uint(a3.x), ownl, 0), gslot(__float_as_uint(a3.y), ownl, 1),
+                                 gslot(__float_as_uint(b3.x), ownr, 0), gslot(__float_as_uint(b3.y), ownr, 1));
+    store_qnode(dst, lx, ly, lz, hx, hy, hz, ids);
+}
+
+// QNodes of internal nodes [k0, k0 + BLOCK) from their record pairs (the one-workgroup
+// build and rtbvh_build_from_codes): coalesced loads into LDS (one float4 of padding per
+// pair: the per-node ds_read_b128 at a 144-B stride is bank-conflict free), one node per thread.
 __global__ __launch_bounds__(BLOCK) void k_qnodes(const Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
                                                   QNode* __restrict__ qn, uint32_t T) {
     __shared__ float4 s_pair[BLOCK * 9];
@@ -458,29 +415,147 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes(const Inner* __restrict__ rec,
     for (uint32_t j = tid; j < 8 * nn; j += BLOCK) s_pair[j + j / 8] = src[j];
     __syncthreads();
     if (tid >= nn) return;
-    const uint32_t k = k0 + tid;
-    const float4* r = s_pair + 9 * tid;
-    const float4 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], b0 = r[4], b1 = r[5], b2 = r[6], b3 = r[7];
-    // record words (rtbvh_device.h): 0-1 l.min.xy 2-3 l.max.xy 4-5 r.min.xy 6-7 r.max.xy
-    // 8 l.min.z 9 l.max.z 10 r.min.z 11 r.max.z 12 id_l 13 id_r 14 own
-    const float lx[4] = {a0.x, a1.x, b0.x, b1.x}, ly[4] = {a0.y, a1.y, b0.y, b1.y}, lz[4] = {a2.x, a2.z, b2.x, b2.z};
-    const float hx[4] = {a0.z, a1.z, b0.z, b1.z}, hy[4] = {a0.w, a1.w, b0.w, b1.w}, hz[4] = {a2.y, a2.w, b2.y, b2.w};
-    QNode q;
-    bool ok = quantize_axis(lx, hx, q.org[0], q.scl[0], q.lo[0], q.hi[0]);
-    ok = quantize_axis(ly, hy, q.org[1], q.scl[1], q.lo[1], q.hi[1]) && ok;
-    ok = quantize_axis(lz, hz, q.org[2], q.scl[2], q.lo[2], q.hi[2]) && ok;
-    if (!ok) q.scl[0] = 0.f;   // the traversal reads the exact pair for this node
-    const uint32_t ownl = __float_as_uint(a3.z), ownr = __float_as_uint(b3.z);
-    auto gslot = [](uint32_t id, uint32_t own, uint32_t side) {
-        return (id == INVALID || (id & LEAF_BIT)) ? id : 2 * own + side;
-    };
-    q.id[0] = gslot(__float_as_uint(a3.x), ownl, 0);
-    q.id[1] = gslot(__float_as_uint(a3.y), ownl, 1);
-    q.id[2] = gslot(__float_as_uint(b3.x), ownr, 0);
-    q.id[3] = gslot(__float_as_uint(b3.y), ownr, 1);
-    const float4* qs = reinterpret_cast<const float4*>(&q);
-    float4* dst = reinterpret_cast<float4*>(qn + slot_of(pint[k], T));   // pint[0] = INVALID: the root
-    dst[0] = qs[0]; dst[1] = qs[1]; dst[2] = qs[2]; dst[3] = qs[3];
+    float4 r[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) r[w] = s_pair[9 * tid + w];
+    qnode_from_pair(r, qn + slot_of(pint[k0 + tid], T));   // pint[0] = INVALID: the root
+}
+
+// QNodes of the nodes k_refit lists (their leaf range crosses a refit workgroup)
+__global__ __launch_bounds__(BLOCK) void k_qnodes_list(const Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
+                                                       const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ count, QNode* __restrict__ qn,
+                                                       uint32_t T) {
+    const uint32_t n = *count;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
+        const uint32_t k = list[j];
+        const float4* src = reinterpret_cast<const float4*>(rec + 2 * (size_t)k);
+        float4 r[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) r[w] = src[w];
+        qnode_from_pair(r, qn + slot_of(pint[k], T));
+    }
+}
+
+// Refit (BVHConstructP2.hlsl:8-37) fused with the leaf records and the node outputs.  One
+// workgroup per 256 sorted leaves [base, base + 256):
+//  1. each thread gathers its leaf's clip-space triangle once and writes the 64-B leaf record
+//     (MortonCodes.hlsl:87-96 box; the reference's edge1/edge2, RayTraceTraversal.hlsl:43-44);
+//  2. it climbs from its leaf as BVHConstructP2 does (a per-node ticket; the second arriver
+//     unions both children in (childL, childR) order): the nodes whose leaf range lies inside
+//     the block join in LDS (both children are climbed by this block exactly then), the few
+//     whose range crosses the block through refit_climb's global sc1 hand-off;
+//  3. after a barrier every node of the block with an in-block range has both children's
+//     boxes in LDS, and so have its internal children: one thread per node writes its record,
+//     the pseudo-records of its leaf children and its QNode, all lanes busy.
+// Against one pass per stage (round 1: records written during the divergent climb, then a
+// QNode pass re-reading every record pair) this writes each output once and reads no record
+// back except for the listed crossing nodes.
+__global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
+    __shared__ uint32_t s_cnt[BLOCK];
+    __shared__ float s_box[BLOCK][2][6];   // node base + k: the boxes of its children (side 0, 1)
+    __shared__ uint4 s_topo[BLOCK];        // the block's nodes [base, base + BLOCK): ids, leaf range
+    __shared__ uint32_t s_pint[BLOCK];
+    const uint32_t T = a.T;
+    const uint32_t base = blockIdx.x * BLOCK, tid = threadIdx.x;
+    const uint32_t i = base + tid;
+    const uint32_t end = base + BLOCK;
+    s_cnt[tid] = 0;
+    if (i + 1 < T) {   // coalesced, so the in-block climb makes no dependent global loads
+        s_topo[tid] = a.topo[i];
+        s_pint[tid] = a.pint[i];
+    }
+    f3 lo = mk(0.f, 0.f, 0.f), hi = lo;
+    uint32_t e = INVALID;
+    if (i < T) {
+        leaf_record(a, i, lo, hi);
+        if (T == 1) {
+            a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
+            a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+        } else {
+            e = a.pleaf[i];
+        }
+    }
+    __syncthreads();
+    for (int level = 0; e != INVALID && level < 2 * STACK_SIZE; level++) {
+        const uint32_t p = e >> 1, side = e & 1u;
+        bool cross = !(p >= base && p < end);   // p's index is outside the block: so is its range
+        uint4 q3;
+        if (!cross) {
+            q3 = s_topo[p - base];   // ids, leaf range
+            cross = !(q3.z >= base && q3.w < end);
+        }
+        if (cross) {
+            refit_climb(lo, hi, e, a);
+            break;
+        }
+        float* sb = s_box[p - base][side];
+        sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the LDS box lands before the ticket
+        if (atomicAdd(&s_cnt[p - base], 1u) == 0) break;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const float* ob = s_box[p - base][side ^ 1u];
+        const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
+        // union in (childL, childR) order, as the reference
+        if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
+        else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
+        e = s_pint[p - base];
+        if (e == INVALID) {
+            a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
+            a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+        }
+    }
+    __syncthreads();
+    // 3. the block's in-block nodes: record, leaf pseudo-records, QNode
+    if (i + 1 >= T) return;
+    const uint4 q = s_topo[tid];
+    if (!(q.z >= base && q.w < end)) return;   // crossing: refit_climb wrote it, k_qnodes_list quantizes it
+    const float* L = s_box[tid][0];
+    const float* R = s_box[tid][1];
+    const f3 l0 = mk(L[0], L[1], L[2]), l1 = mk(L[3], L[4], L[5]);
+    const f3 r0 = mk(R[0], R[1], R[2]), r1 = mk(R[3], R[4], R[5]);
+    const uint32_t slot = slot_of(s_pint[tid], T);
+    store_record(a.rec + slot, l0, l1, r0, r1, q.x, q.y, i);
+    float gx[4], gy[4], gz[4], hx[4], hy[4], hz[4];
+    uint32_t gid[4];
+#pragma unroll
+    for (int sd = 0; sd < 2; sd++) {
+        const uint32_t c = sd ? q.y : q.x;
+        if (c & LEAF_BIT) {   // a leaf child: itself, and no second grandchild (as its pseudo-record)
+            store_leaf_record(a.rec, i, sd, c, sd ? r0 : l0, sd ? r1 : l1);
+            const float* b = sd ? R : L;
+#pragma unroll
+            for (int g = 0; g < 2; g++) {
+                gx[2 * sd + g] = b[0]; gy[2 * sd + g] = b[1]; gz[2 * sd + g] = b[2];
+                hx[2 * sd + g] = b[3]; hy[2 * sd + g] = b[4]; hz[2 * sd + g] = b[5];
+            }
+            gid[2 * sd] = c;
+            gid[2 * sd + 1] = INVALID;
+        } else {              // an internal child: in-block too (its range is inside this node's)
+            const uint4 cq = s_topo[c - base];
+#pragma unroll
+            for (int g = 0; g < 2; g++) {
+                const float* b = s_box[c - base][g];
+                gx[2 * sd + g] = b[0]; gy[2 * sd + g] = b[1]; gz[2 * sd + g] = b[2];
+                hx[2 * sd + g] = b[3]; hy[2 * sd + g] = b[4]; hz[2 * sd + g] = b[5];
+                const uint32_t gcid = g ? cq.y : cq.x;
+                gid[2 * sd + g] = (gcid & LEAF_BIT) ? gcid : 2 * c + g;
+            }
+        }
+    }
+    store_qnode(a.qnode + slot, gx, gy, gz, hx, hy, hz, make_uint4(gid[0], gid[1], gid[2], gid[3]));
+}
+
+__global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= a.T) return;
+    const float* b = boxes + 6 * (size_t)i;
+    const f3 lo = mk(b[0], b[1], b[2]), hi = mk(b[3], b[4], b[5]);
+    if (a.T == 1) {
+        for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
+        return;
+    }
+    refit_climb(lo, hi, a.pleaf[i], a);
 }
 
 // ---- small scenes: the whole build in one workgroup ------------------------------
@@ -571,7 +646,8 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
     __syncthreads();   // sorted ids (leaf_record) and clip triangles visible to the block
     const LdsCodes codes{s_kv};
     for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
-        leaf_record(a, i);
+        f3 lo, hi;
+        leaf_record(a, i, lo, hi);
         if (i + 1 < T) karras_node<MODE>(codes, T, i, a.topo, a.pleaf, a.pint);
     }
     if (tid == 0 && T > 1) a.pint[0] = INVALID;
@@ -671,9 +747,10 @@ void launch_bounds(const BuildArgs& a, hipStream_t s) {
 void launch_morton(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_morton, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
 }
-void launch_leaf_karras(const BuildArgs& a, hipStream_t s) {
-    if (a.delta_mode == 0) hipLaunchKernelGGL(k_leaf_karras<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
-    else hipLaunchKernelGGL(k_leaf_karras<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+void launch_karras(const BuildArgs& a, hipStream_t s) {
+    if (a.T < 2) return;
+    if (a.delta_mode == 0) hipLaunchKernelGGL(k_karras<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL(k_karras<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
 }
 uint32_t small_build_max() { return SMALL_T; }
 void launch_build_small(const BuildArgs& a, hipStream_t s) {
@@ -688,14 +765,18 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s) {
 }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    if (a.T > 1)   // the crossing nodes' QNodes: a few per workgroup of k_refit
+        hipLaunchKernelGGL(k_qnodes_list, dim3(256), dim3(BLOCK), 0, s, a.rec, a.pint, a.cross, a.cross_count, a.qnode,
+                           a.T);
 }
 void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
     hipLaunchKernelGGL(k_export, dim3(blocks_for(2 * (size_t)a.T - 1)), dim3(BLOCK), 0, s, a, (RefNode*)out);
 }
 void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t s) {
-    if (a.delta_mode == 0) hipLaunchKernelGGL(k_karras_only<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
-    else hipLaunchKernelGGL(k_karras_only<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    if (a.delta_mode == 0) hipLaunchKernelGGL(k_karras<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL(k_karras<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
     if (a.T > 1) (void)hipMemsetAsync(a.refit_cnt, 0, sizeof(uint32_t) * (a.T - 1), s);
+    (void)hipMemsetAsync(a.cross_count, 0, sizeof(uint32_t), s);
     hipLaunchKernelGGL(k_refit_boxes, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a, leaf_boxes);
     launch_qnodes(a, s);
 }
