@@ -295,7 +295,8 @@ __device__ __forceinline__ void store_leaf_record(Inner* rec, uint32_t p, uint32
 
 // The global part of the climb, for the nodes whose leaf range crosses a refit workgroup:
 // the child box is handed over through inner[p] (sc1) and the second arriver writes p's
-// record (and the pseudo-records of p's leaf children), lists p for k_qnodes_list, and goes on.
+// record (and the pseudo-records of p's leaf children) and goes on; k_qnodes_cross
+// quantizes these nodes afterwards.
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, const BuildArgs& a) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
@@ -314,7 +315,6 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, const Buil
         store_record(a.rec + slot_of(e, a.T), l0, l1, r0, r1, ids.x, ids.y, p);
         if (ids.x & LEAF_BIT) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
         if (ids.y & LEAF_BIT) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
-        a.cross[atomicAdd(a.cross_count, 1u)] = p;
         // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
         lo = vmin(l0, r0);
         hi = vmax(l1, r1);
@@ -421,20 +421,22 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes(const Inner* __restrict__ rec,
     qnode_from_pair(r, qn + slot_of(pint[k0 + tid], T));   // pint[0] = INVALID: the root
 }
 
-// QNodes of the nodes k_refit lists (their leaf range crosses a refit workgroup)
-__global__ __launch_bounds__(BLOCK) void k_qnodes_list(const Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
-                                                       const uint32_t* __restrict__ list,
-                                                       const uint32_t* __restrict__ count, QNode* __restrict__ qn,
-                                                       uint32_t T) {
-    const uint32_t n = *count;
-    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
-        const uint32_t k = list[j];
-        const float4* src = reinterpret_cast<const float4*>(rec + 2 * (size_t)k);
-        float4 r[8];
+// QNodes of the nodes whose leaf range crosses a refit workgroup (k_refit quantizes the
+// others): a scan of the 16-B topology records, the pair loads for the crossing ones only.
+// (A list appended by the climbing threads serialised on its one counter: ~88 adds per us.)
+__global__ __launch_bounds__(BLOCK) void k_qnodes_cross(const Inner* __restrict__ rec, const uint4* __restrict__ topo,
+                                                        const uint32_t* __restrict__ pint, QNode* __restrict__ qn,
+                                                        uint32_t T) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k + 1 >= T) return;
+    const uint4 q = topo[k];
+    const uint32_t base = k & ~(BLOCK - 1);
+    if (q.z >= base && q.w < base + BLOCK) return;
+    const float4* src = reinterpret_cast<const float4*>(rec + 2 * (size_t)k);
+    float4 r[8];
 #pragma unroll
-        for (int w = 0; w < 8; w++) r[w] = src[w];
-        qnode_from_pair(r, qn + slot_of(pint[k], T));
-    }
+    for (int w = 0; w < 8; w++) r[w] = src[w];
+    qnode_from_pair(r, qn + slot_of(pint[k], T));
 }
 
 // Refit (BVHConstructP2.hlsl:8-37) fused with the leaf records and the node outputs.  One
@@ -509,7 +511,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
     // 3. the block's in-block nodes: record, leaf pseudo-records, QNode
     if (i + 1 >= T) return;
     const uint4 q = s_topo[tid];
-    if (!(q.z >= base && q.w < end)) return;   // crossing: refit_climb wrote it, k_qnodes_list quantizes it
+    if (!(q.z >= base && q.w < end)) return;   // crossing: refit_climb wrote it, k_qnodes_cross quantizes it
     const float* L = s_box[tid][0];
     const float* R = s_box[tid][1];
     const f3 l0 = mk(L[0], L[1], L[2]), l1 = mk(L[3], L[4], L[5]);
@@ -766,7 +768,7 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s) {
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
     if (a.T > 1)   // the crossing nodes' QNodes: a few per workgroup of k_refit
-        hipLaunchKernelGGL(k_qnodes_list, dim3(256), dim3(BLOCK), 0, s, a.rec, a.pint, a.cross, a.cross_count, a.qnode,
+        hipLaunchKernelGGL(k_qnodes_cross, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a.rec, a.topo, a.pint, a.qnode,
                            a.T);
 }
 void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
@@ -776,7 +778,6 @@ void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t 
     if (a.delta_mode == 0) hipLaunchKernelGGL(k_karras<0>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
     else hipLaunchKernelGGL(k_karras<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
     if (a.T > 1) (void)hipMemsetAsync(a.refit_cnt, 0, sizeof(uint32_t) * (a.T - 1), s);
-    (void)hipMemsetAsync(a.cross_count, 0, sizeof(uint32_t), s);
     hipLaunchKernelGGL(k_refit_boxes, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a, leaf_boxes);
     launch_qnodes(a, s);
 }

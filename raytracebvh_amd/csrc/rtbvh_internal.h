@@ -53,14 +53,12 @@ struct BuildArgs {
     uint32_t* refit_cnt;      // [T-1]
     float* rootbox;           // [6]
     QNode* qnode;             // [2T-1] quantized 4-wide nodes in slots (rtbvh_device.h), from rec
-    uint32_t* cross;          // [T-1] nodes whose leaf range crosses a refit workgroup (their QNodes come last)
-    uint32_t* cross_count;    // [1]
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
 // Karras topology (topo, pleaf, pint)
 void launch_karras(const BuildArgs& a, hipStream_t s);
-// leaf records + refit + node records + QNodes (refit_cnt and *cross_count zeroed first)
+// leaf records + refit + node records + QNodes (refit_cnt zeroed first)
 void launch_refit(const BuildArgs& a, hipStream_t s);
 // qnode[k] of every internal node from the record pairs
 void launch_qnodes(const BuildArgs& a, hipStream_t s);
