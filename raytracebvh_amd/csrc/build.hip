@@ -293,14 +293,31 @@ __device__ __forceinline__ void store_leaf_record(Inner* rec, uint32_t p, uint32
     store_record(rec + 2 * (size_t)p + side, lo, hi, lo, hi, leaf_id, INVALID, leaf_id);
 }
 
-// The global part of the climb, for the nodes whose leaf range crosses a refit workgroup:
-// the child box is handed over through inner[p] (sc1) and the second arriver writes p's
-// record (and the pseudo-records of p's leaf children) and goes on; k_qnodes_cross
+// A node of the climb is complete: its record (both children's boxes) at its slot, the
+// pseudo-records of its leaf children; returns its box, the union in (childL, childR)
+// order as the reference's min(L.bbMin, R.bbMin).
+__device__ __forceinline__ void complete_node(const BuildArgs& a, uint32_t p, uint32_t e, f3 l0, f3 l1, f3 r0, f3 r1,
+                                              f3& lo, f3& hi) {
+    const uint4 ids = a.topo[p];
+    store_record(a.rec + slot_of(e, a.T), l0, l1, r0, r1, ids.x, ids.y, p);
+    if (ids.x & LEAF_BIT) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
+    if (ids.y & LEAF_BIT) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
+    lo = vmin(l0, r0);
+    hi = vmax(l1, r1);
+    if (e == INVALID) {
+        a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
+        a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+    }
+}
+
+// The global climb, for the nodes whose leaf range crosses a refit workgroup: from a complete
+// node (box lo, hi; e = its parent link) upward, the child box handed over through inner[p]
+// (sc1) and a per-node ticket; the second arriver completes p and goes on.  k_qnodes_cross
 // quantizes these nodes afterwards.
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, const BuildArgs& a) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
-    for (int level = 0; level < 2 * STACK_SIZE; level++) {
+    for (int level = 0; e != INVALID && level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
         st_box_sc1(side ? a.inner[p].rmin : a.inner[p].lmin, lo, hi);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the box stores before the ticket
@@ -310,20 +327,15 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, const Buil
         f3 smin, smax;
         ld_box_sc1(side ? a.inner[p].lmin : a.inner[p].rmin, smin, smax);
         e = a.pint[p];
-        const uint4 ids = a.topo[p];
-        const f3 l0 = side ? smin : lo, l1 = side ? smax : hi, r0 = side ? lo : smin, r1 = side ? hi : smax;
-        store_record(a.rec + slot_of(e, a.T), l0, l1, r0, r1, ids.x, ids.y, p);
-        if (ids.x & LEAF_BIT) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
-        if (ids.y & LEAF_BIT) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
-        // union in (childL, childR) order, as the reference: min(L.bbMin, R.bbMin)
-        lo = vmin(l0, r0);
-        hi = vmax(l1, r1);
-        if (e == INVALID) {
-            a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
-            a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
-            return;
-        }
+        if (side) complete_node(a, p, e, smin, smax, lo, hi, lo, hi);
+        else      complete_node(a, p, e, lo, hi, smin, smax, lo, hi);
     }
+}
+
+// crossing: node k's leaf range is not inside the refit workgroup of its index (k_refit's block)
+__device__ __forceinline__ bool crossing(uint4 topo_k, uint32_t k) {
+    const uint32_t base = k & ~(BLOCK - 1);
+    return !(topo_k.z >= base && topo_k.w < base + BLOCK);
 }
 
 // ---- quantized 4-wide nodes (rtbvh_device.h QNode) ---------------------------------
@@ -429,9 +441,7 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(const Inner* __restrict_
                                                         uint32_t T) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k + 1 >= T) return;
-    const uint4 q = topo[k];
-    const uint32_t base = k & ~(BLOCK - 1);
-    if (q.z >= base && q.w < base + BLOCK) return;
+    if (!crossing(topo[k], k)) return;
     const float4* src = reinterpret_cast<const float4*>(rec + 2 * (size_t)k);
     float4 r[8];
 #pragma unroll
@@ -487,8 +497,9 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
             q3 = s_topo[p - base];   // ids, leaf range
             cross = !(q3.z >= base && q3.w < end);
         }
-        if (cross) {
-            refit_climb(lo, hi, e, a);
+        if (cross) {   // k_refit_top takes it from here (kernel boundary: plain stores)
+            float* hb = side ? a.inner[p].rmin : a.inner[p].lmin;
+            hb[0] = lo.x; hb[1] = lo.y; hb[2] = lo.z; hb[3] = hi.x; hb[4] = hi.y; hb[5] = hi.z;
             break;
         }
         float* sb = s_box[p - base][side];
@@ -511,7 +522,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
     // 3. the block's in-block nodes: record, leaf pseudo-records, QNode
     if (i + 1 >= T) return;
     const uint4 q = s_topo[tid];
-    if (!(q.z >= base && q.w < end)) return;   // crossing: refit_climb wrote it, k_qnodes_cross quantizes it
+    if (!(q.z >= base && q.w < end)) return;   // crossing: k_refit_top completes it, k_qnodes_cross quantizes it
     const float* L = s_box[tid][0];
     const float* R = s_box[tid][1];
     const f3 l0 = mk(L[0], L[1], L[2]), l1 = mk(L[3], L[4], L[5]);
@@ -546,6 +557,41 @@ __global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
         }
     }
     store_qnode(a.qnode + slot, gx, gy, gz, hx, hy, hz, make_uint4(gid[0], gid[1], gid[2], gid[3]));
+}
+
+// The crossing nodes (a few per k_refit workgroup, the top of the tree among them): k_refit
+// left the box of every non-crossing child of a crossing node in inner[node] (leaf or in-block
+// subtree).  Node k's thread: both children non-crossing -> k is complete, climb from it; one
+// -> arrive at k's ticket for that child (the other arrives by a climb); none -> nothing.  A
+// separate launch, so that k_refit's workgroups never wait on the global climb's latency.
+__global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k + 1 >= a.T) return;
+    const uint4 q = a.topo[k];
+    if (!crossing(q, k)) return;
+    const bool ncl = (q.x & LEAF_BIT) || !crossing(a.topo[q.x], q.x);
+    const bool ncr = (q.y & LEAF_BIT) || !crossing(a.topo[q.y], q.y);
+    if (!ncl && !ncr) return;
+    const float* L = a.inner[k].lmin;
+    const float* R = a.inner[k].rmin;
+    f3 lo, hi;
+    uint32_t e = a.pint[k];
+    if (ncl && ncr) {
+        complete_node(a, k, e, mk(L[0], L[1], L[2]), mk(L[3], L[4], L[5]), mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]),
+                      lo, hi);
+    } else {   // one child here: its arrival at k's ticket (the other side's box comes sc1)
+        const uint32_t side = ncl ? 0u : 1u;
+        const float* B = side ? R : L;
+        const f3 blo = mk(B[0], B[1], B[2]), bhi = mk(B[3], B[4], B[5]);
+        const uint32_t old = __hip_atomic_fetch_add(&a.refit_cnt[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == 0) return;
+        asm volatile("" ::: "memory");
+        f3 smin, smax;
+        ld_box_sc1(side ? a.inner[k].lmin : a.inner[k].rmin, smin, smax);
+        if (side) complete_node(a, k, e, smin, smax, blo, bhi, lo, hi);
+        else      complete_node(a, k, e, blo, bhi, smin, smax, lo, hi);
+    }
+    refit_climb(lo, hi, e, a);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
@@ -767,7 +813,8 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s) {
 }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
-    if (a.T > 1)   // the crossing nodes' QNodes: a few per workgroup of k_refit
+    if (a.T > BLOCK) hipLaunchKernelGGL(k_refit_top, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    if (a.T > BLOCK)   // the crossing nodes' QNodes: a few per workgroup of k_refit
         hipLaunchKernelGGL(k_qnodes_cross, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a.rec, a.topo, a.pint, a.qnode,
                            a.T);
 }
