@@ -128,12 +128,14 @@ def build_pmc(workload, mode):
     names = [k for k in ks if k in BUILD_KERNELS]
     if not names:
         return None
-    return {"hbm_bytes": sum(ks[k]["hbm_bytes_per_launch"] for k in names),
-            "per_kernel_gb": {k: round(ks[k]["hbm_bytes_per_launch"] / 1e9, 3) for k in names}}
+    per = {k: ks[k]["hbm_bytes_per_launch"] * BUILD_KERNELS[k] for k in names}
+    return {"hbm_bytes": sum(per.values()), "per_kernel_gb": {k: round(v / 1e9, 3) for k, v in per.items()}}
 
 
-BUILD_KERNELS = ("k_bounds", "k_bounds_final", "k_morton", "k_upsweep", "k_scan_rows", "k_downsweep",
-                 "k_leaf_karras", "k_refit", "k_qnodes", "k_build_small")
+# the build's kernels and their launches per build (the 30-bit sort: 4 passes of 8-bit digits);
+# the mesh box (k_bounds) is computed once per scene by rtbvh_set_scene
+BUILD_KERNELS = {"k_morton": 1, "k_upsweep": 4, "k_scan_rows": 4, "k_downsweep": 4, "k_karras": 1, "k_refit": 1,
+                 "k_refit_top": 1, "k_qnodes_cross": 1}
 
 
 def cpu_model() -> str:

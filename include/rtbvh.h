@@ -335,6 +335,16 @@ rtbvh_status rtbvh_build_from_codes(rtbvh_ctx* ctx, const uint32_t* sorted_codes
  * file order (bottom row first for the usual positive height), as DevIL hands them to
  * Image.cpp:48-49.  Free with rtbvh_texture_free. */
 rtbvh_status rtbvh_texture_load_bmp(const char* path, rtbvh_texture* out);
+/* Decode a baseline (sequential DCT, Huffman, 8-bit, 1 or 3 components, sampling up to 2x2)
+ * JPEG file / memory buffer into RGBA8 rows, top row first, as DevIL hands them to
+ * Image.cpp:48-49 (Test.mtl:12 binds Balls.jpg).  The arithmetic of libjpeg's default
+ * decompression (islow IDCT, fancy upsampling, fixed-point YCbCr -> RGB), restated: bit-exact
+ * against libjpeg-turbo on the reference's files.  RTBVH_ERR_IO for other or malformed files.
+ * Free with rtbvh_texture_free. */
+rtbvh_status rtbvh_texture_load_jpeg(const char* path, rtbvh_texture* out);
+rtbvh_status rtbvh_texture_decode_jpeg(const uint8_t* data, size_t size, rtbvh_texture* out);
+/* BMP or JPEG by the file's magic bytes (ObjLoader's map_Kd files, Image::loadImage). */
+rtbvh_status rtbvh_texture_load(const char* path, rtbvh_texture* out);
 void rtbvh_texture_free(rtbvh_texture* tex);
 /* The 256-entry sRGB -> linear table the texture sampling uses (IEC 61966-2-1, in double). */
 void rtbvh_srgb_table(float out[256]);

@@ -38,7 +38,8 @@ EXPORTS = [
     "rtbvh_scene_synthetic", "rtbvh_scene_free", "rtbvh_scene_num_vertices", "rtbvh_scene_num_indices",
     "rtbvh_scene_num_materials", "rtbvh_scene_num_textures", "rtbvh_scene_vertices", "rtbvh_scene_indices",
     "rtbvh_scene_mat_indices", "rtbvh_scene_materials", "rtbvh_scene_texture_path", "rtbvh_set_scene_obj",
-    "rtbvh_camera_reference", "rtbvh_texture_load_bmp", "rtbvh_texture_free", "rtbvh_srgb_table",
+    "rtbvh_camera_reference", "rtbvh_texture_load_bmp", "rtbvh_texture_load_jpeg", "rtbvh_texture_decode_jpeg",
+    "rtbvh_texture_load", "rtbvh_texture_free", "rtbvh_srgb_table",
     "rtbvh_present", "rtbvh_save_bmp", "rtbvh_assemble_bands", "rtbvh_comm_unique_id", "rtbvh_comm_init",
     "rtbvh_comm_destroy", "rtbvh_trace_tiles",
 ]
@@ -163,6 +164,9 @@ def lib() -> ctypes.CDLL:
         "rtbvh_set_scene_obj": (i32, [vp, vp, vp, u32]),
         "rtbvh_camera_reference": (None, [u32, u32, vp, vp]),
         "rtbvh_texture_load_bmp": (i32, [ctypes.c_char_p, vp]),
+        "rtbvh_texture_load_jpeg": (i32, [ctypes.c_char_p, vp]),
+        "rtbvh_texture_decode_jpeg": (i32, [vp, ctypes.c_size_t, vp]),
+        "rtbvh_texture_load": (i32, [ctypes.c_char_p, vp]),
         "rtbvh_texture_free": (None, [vp]),
         "rtbvh_srgb_table": (None, [vp]),
         "rtbvh_present": (i32, [vp, vp]),

@@ -76,20 +76,29 @@ def _from_native(handle) -> Scene:
 
 def load_texture(path: str) -> np.ndarray:
     """Image::loadImage (Image.cpp:35-61): RGBA8 rows in the order DevIL hands them over
-    without IL_ORIGIN_SET -- the file's own order (BMP: bottom row first, native decoder
-    rtbvh_texture_load_bmp; other formats: PIL, top row first)."""
-    if path.lower().endswith(".bmp"):
-        L = _L.lib()
-        t = _L.Texture()
-        _L.check(L.rtbvh_texture_load_bmp(os.fsencode(path), ctypes.byref(t)))
-        try:
-            return np.ctypeslib.as_array(ctypes.cast(t.rgba8, ctypes.POINTER(ctypes.c_uint8)),
-                                         shape=(t.height, t.width, 4)).copy()
-        finally:
-            L.rtbvh_texture_free(ctypes.byref(t))
-    from PIL import Image   # JPEG etc. (DevIL is not available; PIL is host-side image I/O)
-    with Image.open(path) as im:
-        return np.asarray(im.convert("RGBA"), dtype=np.uint8).copy()
+    without IL_ORIGIN_SET -- the file's own order (BMP: bottom row first; JPEG: top row
+    first), decoded natively by librtbvh (rtbvh_texture_load: BMP or baseline JPEG)."""
+    L = _L.lib()
+    t = _L.Texture()
+    _L.check(L.rtbvh_texture_load(os.fsencode(path), ctypes.byref(t)))
+    try:
+        return np.ctypeslib.as_array(ctypes.cast(t.rgba8, ctypes.POINTER(ctypes.c_uint8)),
+                                     shape=(t.height, t.width, 4)).copy()
+    finally:
+        L.rtbvh_texture_free(ctypes.byref(t))
+
+
+def decode_jpeg(data: bytes) -> np.ndarray:
+    """rtbvh_texture_decode_jpeg on an in-memory file: (H, W, 4) uint8, top row first."""
+    L = _L.lib()
+    t = _L.Texture()
+    buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+    _L.check(L.rtbvh_texture_decode_jpeg(buf, len(data), ctypes.byref(t)))
+    try:
+        return np.ctypeslib.as_array(ctypes.cast(t.rgba8, ctypes.POINTER(ctypes.c_uint8)),
+                                     shape=(t.height, t.width, 4)).copy()
+    finally:
+        L.rtbvh_texture_free(ctypes.byref(t))
 
 
 def load_obj(path: str, load_textures: bool = True) -> Scene:
