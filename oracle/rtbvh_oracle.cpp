@@ -292,7 +292,7 @@ void orc_karras(int mode, const uint32_t* c, uint32_t n, uint32_t* parent, uint3
         parent[left] = (uint32_t)(n + i);
         parent[right] = (uint32_t)(n + i);
     }
-    parent[n] = 0xFFFFFFFFu;   // BVHConstructP1.hlsl:186-187 (root; n == 1: the single leaf)
+    if (n > 1) parent[n] = 0xFFFFFFFFu;   // BVHConstructP1.hlsl:186-187 (the root; n == 1: leaf 0, set above)
 }
 
 /* BVHConstructP2.hlsl:8-37 emulated thread by thread (RadixBVHCombo/main.cpp:535-574) */

@@ -300,6 +300,40 @@ def test_textured_frames_match_oracle(name, W, H, bounces):
     assert not np.array_equal(white, ofb)
 
 
+def _reference_textures():
+    """Test.obj's own textures (Test.mtl: Balls.jpg, Map__1_Composite.bmp), decoded by librtbvh
+    (the files are the reference's CPUTests data, committed under tests/golden/textures)."""
+    from raytracebvh_amd.scene import load_texture
+    d = load_scene_fixture("Test")
+    return [load_texture(os.path.join(GOLDEN, "textures", str(n))) for n in d["texture_names"]]
+
+
+@pytest.mark.parametrize("mode", ["reference", "nearest+packet+wide", "auto"])
+def test_reference_scene_with_its_own_textures(mode):
+    """The reference's default scene as Graphics::onInit loads it (Graphics.cpp:364: Obj/Test.obj
+    with Balls.jpg and Map__1_Composite.bmp), 1920x1080, primary + 1 bounce: GPU frame equals the
+    oracle's with the same texels, bit for bit, and the textures change the frame."""
+    d = load_scene_fixture("Test")
+    tex = _reference_textures()
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"], textures=tex)
+    os_ = orc.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"], textures=tex)
+    W, H = 1920, 1080
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=TRACE_MODES[mode] | rt.FLAG_COUNT_VISITS) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        fb = c.read_framebuffer()
+        st = c.stats()
+        nodes = c.read_bvh()
+    ofb, _, ost = orc.trace(os_, nodes, wvp, wv, W, H, 1)
+    np.testing.assert_allclose(fb, ofb, atol=RGB_TOL, rtol=0)
+    assert np.array_equal(fb, ofb)
+    assert st["textured_hits"] == ost["textured_hits"] > 0
+    white, _, _ = orc.trace(_oscene(s), nodes, wvp, wv, W, H, 1)
+    assert not np.array_equal(white, ofb)
+
+
 def test_present_is_flipped_unorm8_framebuffer():
     """RayTraceBVHPS.hlsl:13-16 into R8G8B8A8_UNORM: screen row y = framebuffer row H-1-y."""
     d = load_scene_fixture("Test")

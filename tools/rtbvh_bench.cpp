@@ -36,13 +36,6 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
     const char* v = std::getenv(name);
     return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
 }
-bool ends_with_ci(const std::string& s, const char* suf) {
-    const size_t n = std::strlen(suf);
-    if (s.size() < n) return false;
-    for (size_t i = 0; i < n; i++)
-        if (std::tolower((unsigned char)s[s.size() - n + i]) != suf[i]) return false;
-    return true;
-}
 double median(std::vector<double> v) {
     std::sort(v.begin(), v.end());
     return v.empty() ? 0.0 : v[v.size() / 2];
@@ -103,8 +96,8 @@ int main(int argc, char** argv) {
     rtbvh_scene* scene = nullptr;
     if (!obj.empty()) check(rtbvh_scene_load_obj(obj.c_str(), &scene), "load " + obj);
     else check(rtbvh_scene_synthetic(seed, ntris, half, &scene), "synthetic scene");
-    // textures t4-t5: BMP decoded natively; other formats fall back to white (as a texture
-    // that fails to load does in the Python loader)
+    // textures t4-t5 (Image::loadImage, Image.cpp:35-61): BMP and baseline JPEG decoded natively;
+    // a file that cannot be decoded falls back to one white texel (as in the Python loader)
     std::vector<rtbvh_texture> tex(rtbvh_scene_num_textures(scene));
     std::vector<bool> owned(tex.size(), false);
     static const uint8_t white[4] = {255, 255, 255, 255};
@@ -116,7 +109,7 @@ int main(int argc, char** argv) {
             if (slash != std::string::npos) path = obj.substr(0, slash + 1) + path;
         }
         const char* p = name ? path.c_str() : nullptr;
-        if (p && ends_with_ci(path, ".bmp") && rtbvh_texture_load_bmp(p, &tex[k]) == RTBVH_OK) {
+        if (p && rtbvh_texture_load(p, &tex[k]) == RTBVH_OK) {
             owned[k] = true;
             continue;
         }
