@@ -14,6 +14,12 @@ namespace rtbvh {
 namespace {
 
 constexpr uint32_t BLOCK = 256;
+#ifndef RTBVH_REFIT_BLOCK
+#define RTBVH_REFIT_BLOCK 512
+#endif
+// leaves (and node indices) per k_refit workgroup: the nodes whose leaf range lies inside
+// one join in LDS; the others ("crossing") climb in k_refit_top
+constexpr uint32_t RBLOCK = RTBVH_REFIT_BLOCK;
 
 __device__ __forceinline__ uint32_t expand_bits(uint32_t var) {   // MortonCodes.hlsl:13-31
     var &= 0x000003ffu; var |= var << 16;
@@ -220,10 +226,34 @@ __device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i, f3& 
 // BVHConstructP1.hlsl:167-188: internal node i for every i < T-1 (topology only: child ids,
 // leaf range, parent links); the root's parent is UINT_MAX (:186-187).  The leaf records are
 // written by the refit (k_refit), which gathers each leaf's triangle once.
+#ifndef RTBVH_KARRAS_WIN
+#define RTBVH_KARRAS_WIN 256
+#endif
+// The sorted codes a workgroup's searches touch most -- the neighbourhood of its 256 nodes:
+// the deep nodes' ranges are short -- are staged in LDS (a window of KWIN codes either side);
+// codes outside the window come from global memory.
+constexpr int64_t KWIN = RTBVH_KARRAS_WIN;
+struct WindowCodes {
+    const uint32_t* g;
+    const uint32_t* s;
+    int64_t lo, hi;   // the window [lo, hi) of the code sequence held in s
+    __device__ uint32_t operator[](int64_t j) const { return (j >= lo && j < hi) ? s[j - lo] : g[j]; }
+};
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_karras(BuildArgs a) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
+    if (KWIN > 0) {
+        __shared__ uint32_t s_codes[KWIN > 0 ? BLOCK + 2 * KWIN : 1];
+        const int64_t base = (int64_t)blockIdx.x * BLOCK;
+        const int64_t lo = base - KWIN > 0 ? base - KWIN : 0;
+        const int64_t hi = base + BLOCK + KWIN < (int64_t)a.T ? base + BLOCK + KWIN : (int64_t)a.T;
+        for (int64_t j = lo + threadIdx.x; j < hi; j += BLOCK) s_codes[j - lo] = a.sorted_keys[j];
+        __syncthreads();
+        const WindowCodes codes{a.sorted_keys, s_codes, lo, hi};
+        if (i + 1 < a.T) karras_node<MODE>(codes, a.T, i, a.topo, a.pleaf, a.pint);
+    } else {
+        if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
+    }
     if (i == 0 && a.T > 1) a.pint[0] = INVALID;
 }
 
@@ -334,8 +364,8 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, const Buil
 
 // crossing: node k's leaf range is not inside the refit workgroup of its index (k_refit's block)
 __device__ __forceinline__ bool crossing(uint4 topo_k, uint32_t k) {
-    const uint32_t base = k & ~(BLOCK - 1);
-    return !(topo_k.z >= base && topo_k.w < base + BLOCK);
+    const uint32_t base = k & ~(RBLOCK - 1);
+    return !(topo_k.z >= base && topo_k.w < base + RBLOCK);
 }
 
 // ---- quantized 4-wide nodes (rtbvh_device.h QNode) ---------------------------------
@@ -463,15 +493,15 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(const Inner* __restrict_
 // Against one pass per stage (round 1: records written during the divergent climb, then a
 // QNode pass re-reading every record pair) this writes each output once and reads no record
 // back except for the listed crossing nodes.
-__global__ __launch_bounds__(BLOCK) void k_refit(BuildArgs a) {
-    __shared__ uint32_t s_cnt[BLOCK];
-    __shared__ float s_box[BLOCK][2][6];   // node base + k: the boxes of its children (side 0, 1)
-    __shared__ uint4 s_topo[BLOCK];        // the block's nodes [base, base + BLOCK): ids, leaf range
-    __shared__ uint32_t s_pint[BLOCK];
+__global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
+    __shared__ uint32_t s_cnt[RBLOCK];
+    __shared__ float s_box[RBLOCK][2][6];   // node base + k: the boxes of its children (side 0, 1)
+    __shared__ uint4 s_topo[RBLOCK];        // the block's nodes [base, base + BLOCK): ids, leaf range
+    __shared__ uint32_t s_pint[RBLOCK];
     const uint32_t T = a.T;
-    const uint32_t base = blockIdx.x * BLOCK, tid = threadIdx.x;
+    const uint32_t base = blockIdx.x * RBLOCK, tid = threadIdx.x;
     const uint32_t i = base + tid;
-    const uint32_t end = base + BLOCK;
+    const uint32_t end = base + RBLOCK;
     s_cnt[tid] = 0;
     if (i + 1 < T) {   // coalesced, so the in-block climb makes no dependent global loads
         s_topo[tid] = a.topo[i];
@@ -812,9 +842,9 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_qnodes, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.rec, a.pint, a.qnode, a.T);
 }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_refit, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
-    if (a.T > BLOCK) hipLaunchKernelGGL(k_refit_top, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
-    if (a.T > BLOCK)   // the crossing nodes' QNodes: a few per workgroup of k_refit
+    hipLaunchKernelGGL(k_refit, dim3((a.T + RBLOCK - 1) / RBLOCK), dim3(RBLOCK), 0, s, a);
+    if (a.T > RBLOCK) hipLaunchKernelGGL(k_refit_top, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
+    if (a.T > RBLOCK)   // the crossing nodes' QNodes: a few per workgroup of k_refit
         hipLaunchKernelGGL(k_qnodes_cross, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a.rec, a.topo, a.pint, a.qnode,
                            a.T);
 }
