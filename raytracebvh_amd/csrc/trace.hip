@@ -33,6 +33,9 @@ namespace {
 
 constexpr uint32_t BLOCK = 256;
 constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
+#ifndef RTBVH_PACKET_PUSH
+#define RTBVH_PACKET_PUSH 2
+#endif
 
 struct Counts { uint32_t internal, leaf, overflow, wint, wleaf; };   // w*: packet wave steps (lane 0)
 
@@ -360,6 +363,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
 #pragma unroll
                 for (int k = 0; k < 4; k++) m[k] = __ballot(h[k]);
             }
+#if RTBVH_PACKET_PUSH == 0
             // children left to right (compile-time indices only: no private arrays)
             const uint32_t* oi = id;
             const uint64_t* om = m;
@@ -384,6 +388,40 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
                 node = first == 0 ? oi[0] : first == 1 ? oi[1] : first == 2 ? oi[2] : oi[3];
                 mask = first == 0 ? om[0] : first == 1 ? om[1] : first == 2 ? om[2] : om[3];
             }
+#else
+            // The children as a 4-bit set; lanes 0..3 hold child k's (id, lane mask), so the
+            // next node is a v_readlane at the first child and the pushes are ONE vector store
+            // per word from the lanes of the other hit children (the later a child, the deeper its
+            // entry: popped left to right), instead of one branchy lane-0 region per child:
+            // the walk is bound by the CU's one scalar unit.
+            const uint32_t hs = (m[0] != 0 ? 1u : 0u) | (m[1] != 0 ? 2u : 0u) | (m[2] != 0 ? 4u : 0u) |
+                                (m[3] != 0 ? 8u : 0u);
+            if (hs == 0) {
+                pop = true;
+            } else {
+                const uint32_t rest = hs & (hs - 1);
+                const int npush = __builtin_popcount(rest);
+                if (sp + npush > limit) {
+                    c.overflow++;
+                    pop = true;
+                } else {
+                    const uint32_t first = (uint32_t)__builtin_ctz(hs);
+                    const uint32_t vid = lane == 0 ? id[0] : lane == 1 ? id[1] : lane == 2 ? id[2] : id[3];
+                    const uint64_t vm = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
+                    const uint32_t vlo = (uint32_t)vm, vhi = (uint32_t)(vm >> 32);
+                    node = __builtin_amdgcn_readlane(vid, first);
+                    mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, first) << 32 |
+                           (uint32_t)__builtin_amdgcn_readlane(vlo, first);
+                    if (lane < 4 && ((rest >> lane) & 1u)) {
+                        const int pos = sp + __builtin_popcount(rest >> (lane + 1));
+                        s_st[3 * pos] = vid;
+                        s_st[3 * pos + 1] = vlo;
+                        s_st[3 * pos + 2] = vhi;
+                    }
+                    sp += npush;
+                }
+            }
+#endif
         }
         if (pop) {
             if (sp == 0) break;
@@ -394,6 +432,166 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             mask = ((uint64_t)hi << 32) | lo;
         }
     }
+    return hit;
+}
+
+// ray_triangle without early exits, for the packet walk's leaf step: every lane evaluates
+// the same operations, and each rejection of the reference's order becomes a select of -1
+// (pinned, so the six tests stay VALU selects rather than lane masks combined on the SALU).
+// The same floats and the same accept predicate: the same result.  `in` false also gives -1.
+__device__ __forceinline__ float ray_triangle_flat(f3 o, f3 d, f3 p0, f3 e1, f3 e2, bool in) {
+    const f3 tmp = cross(d, e2);
+    const float dx = dot(e1, tmp);
+    const float idx = 1.f / dx;
+    const f3 rt = sub(o, p0);
+    const float u = dot(rt, tmp) * idx;
+    const f3 q = cross(rt, e1);
+    const float v = dot(d, q) * idx;
+    const float t = dot(e2, q) * idx;
+    float r = EPSILON < t ? t : -1.f;
+    pin(r);
+    r = fabsf(dx) < EPSILON ? -1.f : r;
+    pin(r);
+    r = u < .0f ? -1.f : r;
+    pin(r);
+    r = 1.f < u ? -1.f : r;
+    pin(r);
+    r = v < .0f ? -1.f : r;
+    pin(r);
+    r = 1.f < u + v ? -1.f : r;
+    pin(r);
+    return in ? r : -1.f;
+}
+
+// v_writelane_b32: lane K of v := the wave-uniform s (a VALU op, no scalar work)
+template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t s) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "i"(K));
+}
+
+// traverse_packet4 with the per-step scalar work cut (the walk is bound by the CU's one
+// scalar unit):
+//  * lanes 0..3 of (vid, vlo, vhi) hold child k's id and lane mask (v_writelane), so the hit
+//    set is one ballot, the next node a v_readlane and the pushes one vector store per word;
+//  * the fast box test needs no AND with the parent's lanes: a box whose bit is clear lies
+//    inside its parent's box, so a lane that passes it passed the parent's test (at a bound
+//    >= today's) -- lanes outside the frame get a NaN origin, which fails every fast test;
+//  * the leaf test runs on every lane without branches (ray_triangle_flat) and the (t, leaf)
+//    minimum is one u64 compare.
+template <bool COUNT>
+__device__ __forceinline__ bool traverse_packet4_flat(const Inner* __restrict__ inner4,
+                                                      const float4* __restrict__ leaf, uint32_t T, f3 o, f3 d,
+                                                      f3 inv, bool valid, int limit, float& best,
+                                                      uint32_t& best_leaf, Counts& c, uint32_t* s_st) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t mask = __ballot(valid);
+    best = 0.f;
+    best_leaf = 0;
+    if (mask == 0) return false;
+    const float qnan = __builtin_nanf("");
+    const f2v oxy = valid ? f2v{o.x, o.y} : f2v{qnan, qnan};
+    // (t, leaf) of the best hit as one u64 key, t's bits above: t > EPSILON > 0, so the u64
+    // order is the (t, leaf) order; before any hit (+inf, ~0), which every hit beats
+    constexpr uint64_t NO_HIT = 0x7F800000FFFFFFFFull;
+    uint64_t key = NO_HIT;
+    uint32_t vid = 0, vlo = 0, vhi = 0;
+    int sp = 0;
+    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
+    uint32_t guard = 2 * T + 2;
+    while (true) {
+        if (--guard == 0) { c.overflow++; break; }
+        node = __builtin_amdgcn_readfirstlane(node);
+        if (node & LEAF_BIT) {
+            const uint32_t j = node & ~LEAF_BIT;
+            const v16f q = sload16(leaf + 4 * (size_t)j);
+            if (COUNT && lane == 0) c.wleaf++;
+            const bool in = (mask >> lane) & 1u;
+            if (COUNT) c.leaf += in;
+            const float t =
+                ray_triangle_flat(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]), in);
+            const uint64_t k = t == -1.f ? ~0ull : (uint64_t)__float_as_uint(t) << 32 | j;
+            key = k < key ? k : key;
+        } else {
+            const v16f A = sload16(inner4 + 2 * (size_t)node);
+            const v16f B = sload16(inner4 + 2 * (size_t)node + 1);
+            if (COUNT && lane == 0) c.wint++;
+            if (COUNT) c.internal += (mask >> lane) & 1u;
+            const uint32_t id0 = __float_as_uint(A[12]), id1 = __float_as_uint(A[13]);
+            const uint32_t id2 = __float_as_uint(B[12]), id3 = __float_as_uint(B[13]);
+            uint64_t m0, m1, m2, m3;
+            const float bound = __uint_as_float((uint32_t)(key >> 32));
+            if ((__float_as_uint(A[15]) | __float_as_uint(B[15])) == 0) {   // wave-uniform
+                // min(o - lo, hi - o) > 0 with lz <= bound folded in as a select (pinned, so the
+                // compiler keeps it a VALU select instead of ANDing two lane masks on the SALU)
+                const auto lanes = [&](f2v lo, f2v hi, float lz) {
+                    const f2v d0 = oxy - lo, d1 = hi - oxy;
+                    float m = fminf(fminf(d0.x, d0.y), fminf(d1.x, d1.y));
+                    m = lz <= bound ? m : -1.f;   // bound: +inf before the first hit
+                    pin(m);
+                    return __builtin_amdgcn_ballot_w64(m > 0.f);
+                };
+                m0 = lanes(A.s01, A.s23, A[8]);
+                m1 = lanes(A.s45, A.s67, A[10]);
+                m2 = lanes(B.s01, B.s23, B[8]);
+                m3 = lanes(B.s45, B.s67, B[10]);
+            } else {
+                const bool hit = key != NO_HIT;
+                const float bst = hit ? bound : 0.f;
+                bool h0 = false, h1 = false, h2 = false, h3 = false;
+                float t0, t1, t2, t3;
+                if ((mask >> lane) & 1u) {
+                    h0 = ray_box_xy(o, inv, A.s01, A.s23, A[8], A[9], hit, bst, t0);
+                    h1 = ray_box_xy(o, inv, A.s45, A.s67, A[10], A[11], hit, bst, t1) & (id1 != INVALID);
+                    h2 = ray_box_xy(o, inv, B.s01, B.s23, B[8], B[9], hit, bst, t2);
+                    h3 = ray_box_xy(o, inv, B.s45, B.s67, B[10], B[11], hit, bst, t3) & (id3 != INVALID);
+                }
+                m0 = __ballot(h0); m1 = __ballot(h1); m2 = __ballot(h2); m3 = __ballot(h3);
+            }
+            writelane<0>(vid, id0);
+            writelane<1>(vid, id1);
+            writelane<2>(vid, id2);
+            writelane<3>(vid, id3);
+            writelane<0>(vlo, (uint32_t)m0);
+            writelane<1>(vlo, (uint32_t)m1);
+            writelane<2>(vlo, (uint32_t)m2);
+            writelane<3>(vlo, (uint32_t)m3);
+            writelane<0>(vhi, (uint32_t)(m0 >> 32));
+            writelane<1>(vhi, (uint32_t)(m1 >> 32));
+            writelane<2>(vhi, (uint32_t)(m2 >> 32));
+            writelane<3>(vhi, (uint32_t)(m3 >> 32));
+            // an absent second child (INVALID id: a leaf's pseudo-record) hits no lane
+            const bool absent = vid == INVALID;
+            vlo = absent ? 0u : vlo;
+            vhi = absent ? 0u : vhi;
+            const uint32_t hs = (uint32_t)__builtin_amdgcn_ballot_w64((vlo | vhi) != 0);   // lanes >= 4 stay 0
+            if (hs != 0) {
+                const uint32_t rest = hs & (hs - 1);
+                const int npush = __builtin_popcount(rest);
+                if (sp + npush <= limit) {
+                    const uint32_t first = (uint32_t)__builtin_ctz(hs);
+                    node = __builtin_amdgcn_readlane(vid, first);
+                    mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, first) << 32 |
+                           (uint32_t)__builtin_amdgcn_readlane(vlo, first);
+                    if (((uint64_t)rest >> lane) & 1u) {   // the later a child, the deeper its entry
+                        const int pos = sp + __builtin_popcount(rest >> (lane + 1));
+                        s_st[3 * pos] = vid;
+                        s_st[3 * pos + 1] = vlo;
+                        s_st[3 * pos + 2] = vhi;
+                    }
+                    sp += npush;
+                    continue;
+                }
+                c.overflow++;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
+        mask = ((uint64_t)hi << 32) | lo;
+    }
+    const bool hit = key != NO_HIT;
+    if (hit) { best = __uint_as_float((uint32_t)(key >> 32)); best_leaf = (uint32_t)key; }
     return hit;
 }
 
@@ -584,7 +782,12 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     uint32_t bl = 0;
     bool phit = false;
     if (PW::WIDE)     // whole wave, before any divergence
+#if RTBVH_PACKET_PUSH == 2
+        phit = traverse_packet4_flat<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c,
+                                            s_pst + w * PST);
+#else
         phit = traverse_packet4<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c, s_pst + w * PST);
+#endif
     else if (PW::PACKET)
         phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, lim, best, bl, c,
                                                    s_pst + w * PST);
