@@ -316,11 +316,22 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t parent_code, uint32_t T) {
     return parent_code == INVALID ? 2 * T - 2 : parent_code;
 }
 
-// the pseudo-record of leaf j, child `side` of node p (rtbvh_device.h: the 4-wide walks read a
-// leaf child's slot as a record whose two children are the leaf itself and nothing)
+// The pseudo-record of leaf j (rtbvh_device.h: the 4-wide walks read a leaf child's slot as a
+// record whose two children are the leaf itself and nothing).  The absent second child repeats
+// the box with a NaN min.z, which fails the primary walk's fast test (min.z <= bound) for every
+// lane, so that walk needs no id check; both bits of word 15 are the leaf box's own.
+__device__ __forceinline__ void store_pseudo_record(Inner* dst, uint32_t leaf_id, f3 lo, f3 hi) {
+    float4* d = reinterpret_cast<float4*>(dst);
+    const uint32_t gen = general_box(lo, hi) * 3u;
+    d[0] = make_float4(lo.x, lo.y, hi.x, hi.y);
+    d[1] = make_float4(lo.x, lo.y, hi.x, hi.y);
+    d[2] = make_float4(lo.z, hi.z, __uint_as_float(ABSENT_MINZ), hi.z);
+    d[3] = make_float4(__uint_as_float(leaf_id), __uint_as_float(INVALID), __uint_as_float(leaf_id),
+                       __uint_as_float(gen));
+}
 __device__ __forceinline__ void store_leaf_record(Inner* rec, uint32_t p, uint32_t side, uint32_t leaf_id, f3 lo,
                                                   f3 hi) {
-    store_record(rec + 2 * (size_t)p + side, lo, hi, lo, hi, leaf_id, INVALID, leaf_id);
+    store_pseudo_record(rec + 2 * (size_t)p + side, leaf_id, lo, hi);
 }
 
 // A node of the climb is complete: its record (both children's boxes) at its slot, the
@@ -434,7 +445,10 @@ __device__ __forceinline__ void qnode_from_pair(const float4 (&r)[8], QNode* dst
     const float4 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], b0 = r[4], b1 = r[5], b2 = r[6], b3 = r[7];
     // record words (rtbvh_device.h): 0-1 l.min.xy 2-3 l.max.xy 4-5 r.min.xy 6-7 r.max.xy
     // 8 l.min.z 9 l.max.z 10 r.min.z 11 r.max.z 12 id_l 13 id_r 14 own
-    const float lx[4] = {a0.x, a1.x, b0.x, b1.x}, ly[4] = {a0.y, a1.y, b0.y, b1.y}, lz[4] = {a2.x, a2.z, b2.x, b2.z};
+    // an absent grandchild (a pseudo-record's second box, NaN min.z) repeats the first box
+    const float lx[4] = {a0.x, a1.x, b0.x, b1.x}, ly[4] = {a0.y, a1.y, b0.y, b1.y};
+    const float lz[4] = {a2.x, __float_as_uint(a3.y) == INVALID ? a2.x : a2.z, b2.x,
+                         __float_as_uint(b3.y) == INVALID ? b2.x : b2.z};
     const float hx[4] = {a0.z, a1.z, b0.z, b1.z}, hy[4] = {a0.w, a1.w, b0.w, b1.w}, hz[4] = {a2.y, a2.w, b2.y, b2.w};
     const uint32_t ownl = __float_as_uint(a3.z), ownr = __float_as_uint(b3.z);
     auto gslot = [](uint32_t id, uint32_t own, uint32_t side) {
@@ -749,7 +763,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
             continue;
         }
         uint32_t e = s_pleaf[i];
-        store_record(a.rec + e, lo, hi, lo, hi, LEAF_BIT | i, INVALID, LEAF_BIT | i);
+        store_pseudo_record(a.rec + e, LEAF_BIT | i, lo, hi);
         for (int level = 0; level < 2 * STACK_SIZE; level++) {   // k_refit's in-block protocol
             const uint32_t p = e >> 1, side = e & 1u;
             float* sb = s_box[p][side];

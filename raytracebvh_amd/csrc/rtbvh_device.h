@@ -11,7 +11,8 @@
 //                        names): the record of internal node k (the boxes and ids of its
 //                        two children, and k itself) sits at slot
 //                        pint[k] = 2*parent + side, the root's at slot 2T-2; slot pleaf[j]
-//                        holds a pseudo-record {box_j, box_j, LEAF_BIT|j, INVALID} for leaf j.
+//                        holds a pseudo-record {box_j, box_j with min.z NaN, LEAF_BIT|j, INVALID}
+//                        for leaf j (build.hip store_pseudo_record).
 //                        So the records of two siblings share one 128-B line: the binary
 //                        walks step to slot 2k+side, the 4-wide walks read slots 2k, 2k+1
 //                        (the four grandchild boxes of k) in one line.
@@ -33,6 +34,7 @@ namespace rtbvh {
 
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t INVALID = 0xFFFFFFFFu;
+constexpr uint32_t ABSENT_MINZ = 0x7FC00000u;   // min.z (a quiet NaN) of a pseudo-record's absent child
 constexpr int STACK_SIZE = 66;   // binary walks: >= 64 levels of a clz64 Karras tree + sentinel
 constexpr int STACK4 = 100;      // 4-wide walks: <= 3 pushes per level of a <= 32-level 4-wide tree
 

@@ -33,9 +33,6 @@ namespace {
 
 constexpr uint32_t BLOCK = 256;
 constexpr float EPSILON = 0.01f;   // RayTraceTraversal.hlsl:7
-#ifndef RTBVH_PACKET_PUSH
-#define RTBVH_PACKET_PUSH 2
-#endif
 
 struct Counts { uint32_t internal, leaf, overflow, wint, wleaf; };   // w*: packet wave steps (lane 0)
 
@@ -279,162 +276,6 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
     return hit;
 }
 
-// ---- wave-packet traversal on the 4-wide view (primary rays) -------------------
-// As traverse_packet, but one step reads the 128-B record pair inner4[2p], inner4[2p+1]
-// (two s_load_dwordx16 of one line): the boxes of p's four grandchildren.  Children
-// are taken left to right (the left-first DFS's order LL, LR, RL, RR).  The per-lane
-// result is the (t, leaf) minimum, as for the 4-wide bounce walk.  (A front-to-back
-// order lost the compiler's wave-uniform tracking of the node id: DESIGN.md §6.)
-//
-// Axis-parallel box test: the rays run along d = (0, 0, 1) from z = 0 (k_primary), so
-// inv = (inf, inf, 1) and each x/y slab of ray_box_xy yields [-inf, inf] (or NaNs that
-// fminf/fmaxf drop) exactly when min < o < max, and an empty slab otherwise.  For a box
-// whose record bit (word 15, build.hip general_box) is clear -- min < max in x and y,
-// min.z <= max.z, 0 <= max.z < inf -- the test is therefore exactly
-//     min.x < o.x < max.x  &&  min.y < o.y < max.y  &&  (!hit || min.z <= best)
-// (denormals are kept, so min < o has the sign of min - o), evaluated as o - min and
-// max - o as packed differences and min(...) > 0: 6 VALU + 2 lane-mask ANDs per box.  A
-// node with any bit set takes the general test.
-template <bool COUNT>
-__device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
-                                                 uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
-                                                 uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*STACK4] */) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t lanebit = 1ull << lane;
-    bool hit = false;
-    best = 0.f;
-    best_leaf = 0;
-    uint64_t mask = __ballot(valid);
-    int sp = 0;
-    uint32_t node = (T == 1) ? LEAF_BIT : 0u;
-    if (mask == 0) return false;
-    float bound = INFINITY;   // best once hit, +inf before (min.z <= bound == !hit || min.z <= best)
-    // The stack is lane 0's LDS words, one lane-0 region per push (alternatives: DESIGN.md §6).
-    uint32_t guard = 2 * T + 2;
-    while (true) {
-        if (--guard == 0) { c.overflow++; break; }
-        node = __builtin_amdgcn_readfirstlane(node);   // wave-uniform: keeps the record fetch on s_load
-        bool pop = false;
-        if (node & LEAF_BIT) {
-            const uint32_t j = node & ~LEAF_BIT;
-            const v16f q = sload16(leaf + 4 * (size_t)j);
-            if (COUNT && lane == 0) c.wleaf++;
-            if (mask & lanebit) {
-                if (COUNT) c.leaf++;
-                const float t = ray_triangle(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]));
-                if (t != -1.f && (!hit || t < best || (t == best && j < best_leaf))) {
-                    best = t;
-                    bound = t;
-                    best_leaf = j;
-                    hit = true;
-                }
-            }
-            pop = true;
-        } else {
-            const v16f A = sload16(inner4 + 2 * (size_t)node);
-            const v16f B = sload16(inner4 + 2 * (size_t)node + 1);
-            if (COUNT && lane == 0) c.wint++;
-            uint32_t id[4] = {__float_as_uint(A[12]), __float_as_uint(A[13]), __float_as_uint(B[12]),
-                              __float_as_uint(B[13])};
-            if (COUNT && (mask & lanebit)) c.internal++;
-            uint64_t m[4];
-            if ((__float_as_uint(A[15]) | __float_as_uint(B[15])) == 0) {   // wave-uniform
-                const f2v oxy = {o.x, o.y};
-                const auto lanes = [&](f2v lo, f2v hi, float lz) {
-                    const f2v d0 = oxy - lo, d1 = hi - oxy;
-                    const float m = fminf(fminf(d0.x, d0.y), fminf(d1.x, d1.y));
-                    return __builtin_amdgcn_ballot_w64(m > 0.f) & __builtin_amdgcn_ballot_w64(lz <= bound);
-                };
-                m[0] = lanes(A.s01, A.s23, A[8]) & mask;
-                m[1] = lanes(A.s45, A.s67, A[10]) & mask;
-                m[2] = lanes(B.s01, B.s23, B[8]) & mask;
-                m[3] = lanes(B.s45, B.s67, B[10]) & mask;
-                if (id[1] == INVALID) m[1] = 0;
-                if (id[3] == INVALID) m[3] = 0;
-            } else {
-                bool h[4] = {false, false, false, false};
-                float t[4] = {0.f, 0.f, 0.f, 0.f};
-                if (mask & lanebit) {
-                    h[0] = ray_box_xy(o, inv, A.s01, A.s23, A[8], A[9], hit, best, t[0]);
-                    h[1] = ray_box_xy(o, inv, A.s45, A.s67, A[10], A[11], hit, best, t[1]) & (id[1] != INVALID);
-                    h[2] = ray_box_xy(o, inv, B.s01, B.s23, B[8], B[9], hit, best, t[2]);
-                    h[3] = ray_box_xy(o, inv, B.s45, B.s67, B[10], B[11], hit, best, t[3]) & (id[3] != INVALID);
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++) m[k] = __ballot(h[k]);
-            }
-#if RTBVH_PACKET_PUSH == 0
-            // children left to right (compile-time indices only: no private arrays)
-            const uint32_t* oi = id;
-            const uint64_t* om = m;
-            const int first = om[0] ? 0 : om[1] ? 1 : om[2] ? 2 : om[3] ? 3 : -1;
-            if (first < 0) {
-                pop = true;
-            } else if (sp + 3 > limit) {
-                c.overflow++;
-                pop = true;
-            } else {
-#pragma unroll
-                for (int k = 3; k >= 1; --k) {   // push the later children, farthest first
-                    if (k > first && om[k]) {
-                        if (lane == 0) {
-                            s_st[3 * sp] = oi[k];
-                            s_st[3 * sp + 1] = (uint32_t)om[k];
-                            s_st[3 * sp + 2] = (uint32_t)(om[k] >> 32);
-                        }
-                        ++sp;
-                    }
-                }
-                node = first == 0 ? oi[0] : first == 1 ? oi[1] : first == 2 ? oi[2] : oi[3];
-                mask = first == 0 ? om[0] : first == 1 ? om[1] : first == 2 ? om[2] : om[3];
-            }
-#else
-            // The children as a 4-bit set; lanes 0..3 hold child k's (id, lane mask), so the
-            // next node is a v_readlane at the first child and the pushes are ONE vector store
-            // per word from the lanes of the other hit children (the later a child, the deeper its
-            // entry: popped left to right), instead of one branchy lane-0 region per child:
-            // the walk is bound by the CU's one scalar unit.
-            const uint32_t hs = (m[0] != 0 ? 1u : 0u) | (m[1] != 0 ? 2u : 0u) | (m[2] != 0 ? 4u : 0u) |
-                                (m[3] != 0 ? 8u : 0u);
-            if (hs == 0) {
-                pop = true;
-            } else {
-                const uint32_t rest = hs & (hs - 1);
-                const int npush = __builtin_popcount(rest);
-                if (sp + npush > limit) {
-                    c.overflow++;
-                    pop = true;
-                } else {
-                    const uint32_t first = (uint32_t)__builtin_ctz(hs);
-                    const uint32_t vid = lane == 0 ? id[0] : lane == 1 ? id[1] : lane == 2 ? id[2] : id[3];
-                    const uint64_t vm = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
-                    const uint32_t vlo = (uint32_t)vm, vhi = (uint32_t)(vm >> 32);
-                    node = __builtin_amdgcn_readlane(vid, first);
-                    mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, first) << 32 |
-                           (uint32_t)__builtin_amdgcn_readlane(vlo, first);
-                    if (lane < 4 && ((rest >> lane) & 1u)) {
-                        const int pos = sp + __builtin_popcount(rest >> (lane + 1));
-                        s_st[3 * pos] = vid;
-                        s_st[3 * pos + 1] = vlo;
-                        s_st[3 * pos + 2] = vhi;
-                    }
-                    sp += npush;
-                }
-            }
-#endif
-        }
-        if (pop) {
-            if (sp == 0) break;
-            --sp;
-            node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
-            const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
-            const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
-            mask = ((uint64_t)hi << 32) | lo;
-        }
-    }
-    return hit;
-}
-
 // ray_triangle without early exits, for the packet walk's leaf step: every lane evaluates
 // the same operations, and each rejection of the reference's order becomes a select of -1
 // (pinned, so the six tests stay VALU selects rather than lane masks combined on the SALU).
@@ -468,20 +309,41 @@ template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t
     asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "i"(K));
 }
 
-// traverse_packet4 with the per-step scalar work cut (the walk is bound by the CU's one
-// scalar unit, DESIGN.md 7.3):
+// ---- wave-packet traversal on the 4-wide view (primary rays) -------------------
+// As traverse_packet, but one step reads the 128-B record pair inner4[2p], inner4[2p+1]
+// (two s_load_dwordx16 of one line): the boxes of p's four grandchildren.  Children are
+// taken left to right (the left-first DFS's order LL, LR, RL, RR); the per-lane result is
+// the (t, leaf) minimum, as for the 4-wide bounce walk.
+//
+// Axis-parallel box test: the rays run along d = (0, 0, 1) from z = 0 (k_primary), so
+// inv = (inf, inf, 1) and each x/y slab of ray_box_xy yields [-inf, inf] (or NaNs that
+// fminf/fmaxf drop) exactly when min < o < max, and an empty slab otherwise.  For a box
+// whose record bit (word 15, build.hip general_box) is clear -- min < max in x and y,
+// min.z <= max.z, 0 <= max.z < inf -- the test is therefore exactly
+//     min.x < o.x < max.x  &&  min.y < o.y < max.y  &&  (!hit || min.z <= best)
+// (denormals are kept, so min < o has the sign of min - o), evaluated as o - min and
+// max - o as packed differences and min(...) > 0.  A node with any bit set takes the
+// general test.
+//
+// Per-step work (one wave step is ~100 instructions, and 32 waves share the CU's one
+// scalar unit; DESIGN.md 7.3):
 //  * lanes 0..3 of (vid, vlo, vhi) hold child k's id and lane mask (v_writelane), so the hit
 //    set is one ballot, the next node a v_readlane and the pushes one vector store per word;
 //  * the fast box test needs no AND with the parent's lanes: a box whose bit is clear lies
 //    inside its parent's box, so a lane that passes it passed the parent's test (at a bound
-//    >= today's) -- lanes outside the frame get a NaN origin, which fails every fast test;
+//    >= today's) -- lanes outside the frame get a NaN origin, which fails every fast test,
+//    and a pseudo-record's absent child has a NaN min.z (build.hip store_pseudo_record);
 //  * the leaf test runs on every lane without branches (ray_triangle_flat) and the (t, leaf)
-//    minimum is one u64 compare.
+//    minimum is one u64 compare;
+//  * stack entry 0 is a sentinel, so a pop has no empty-stack test and the loop one exit.
+// A/B at C5 (10M triangles, 3840x2160, frame identical): 2.60 ms for the per-child lane-0
+// pushes with the parent-mask AND, 2.23 with the lanes-0..3 form, 2.20 with the sentinel and
+// the NaN min.z, 2.18 with the z test as its own lane mask (VALU -> SALU); a branchless tail
+// (descend or pop by selects, the stack top read at the step's start) ran 2.45.
 template <bool COUNT>
-__device__ __forceinline__ bool traverse_packet4_flat(const Inner* __restrict__ inner4,
-                                                      const float4* __restrict__ leaf, uint32_t T, f3 o, f3 d,
-                                                      f3 inv, bool valid, int limit, float& best,
-                                                      uint32_t& best_leaf, Counts& c, uint32_t* s_st) {
+__device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
+                                                 uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
+                                                 uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*(STACK4+1)] */) {
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t mask = __ballot(valid);
     best = 0.f;
@@ -494,11 +356,13 @@ __device__ __forceinline__ bool traverse_packet4_flat(const Inner* __restrict__ 
     constexpr uint64_t NO_HIT = 0x7F800000FFFFFFFFull;
     uint64_t key = NO_HIT;
     uint32_t vid = 0, vlo = 0, vhi = 0;
-    int sp = 0;
+    // entry 0 is a sentinel (node INVALID): popping it ends the walk, so a pop needs no
+    // empty-stack test and the loop has one exit
+    if (lane == 0) s_st[0] = INVALID;
+    int sp = 1;
     uint32_t node = (T == 1) ? LEAF_BIT : 0u;
     uint32_t guard = 2 * T + 2;
-    while (true) {
-        if (--guard == 0) { c.overflow++; break; }
+    do {
         node = __builtin_amdgcn_readfirstlane(node);
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
@@ -525,9 +389,7 @@ __device__ __forceinline__ bool traverse_packet4_flat(const Inner* __restrict__ 
                 const auto lanes = [&](f2v lo, f2v hi, float lz) {
                     const f2v d0 = oxy - lo, d1 = hi - oxy;
                     float m = fminf(fminf(d0.x, d0.y), fminf(d1.x, d1.y));
-                    m = lz <= bound ? m : -1.f;   // bound: +inf before the first hit
-                    pin(m);
-                    return __builtin_amdgcn_ballot_w64(m > 0.f);
+                    return __builtin_amdgcn_ballot_w64(m > 0.f) & __builtin_amdgcn_ballot_w64(lz <= bound);
                 };
                 m0 = lanes(A.s01, A.s23, A[8]);
                 m1 = lanes(A.s45, A.s67, A[10]);
@@ -558,15 +420,13 @@ __device__ __forceinline__ bool traverse_packet4_flat(const Inner* __restrict__ 
             writelane<1>(vhi, (uint32_t)(m1 >> 32));
             writelane<2>(vhi, (uint32_t)(m2 >> 32));
             writelane<3>(vhi, (uint32_t)(m3 >> 32));
-            // an absent second child (INVALID id: a leaf's pseudo-record) hits no lane
-            const bool absent = vid == INVALID;
-            vlo = absent ? 0u : vlo;
-            vhi = absent ? 0u : vhi;
+            // (an absent second child -- INVALID id, a leaf's pseudo-record -- has a NaN min.z and
+            // hits no lane in the fast test; the general test checks its id)
             const uint32_t hs = (uint32_t)__builtin_amdgcn_ballot_w64((vlo | vhi) != 0);   // lanes >= 4 stay 0
             if (hs != 0) {
                 const uint32_t rest = hs & (hs - 1);
                 const int npush = __builtin_popcount(rest);
-                if (sp + npush <= limit) {
+                if (sp + npush <= limit + 1) {
                     const uint32_t first = (uint32_t)__builtin_ctz(hs);
                     node = __builtin_amdgcn_readlane(vid, first);
                     mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, first) << 32 |
@@ -583,13 +443,13 @@ __device__ __forceinline__ bool traverse_packet4_flat(const Inner* __restrict__ 
                 c.overflow++;
             }
         }
-        if (sp == 0) break;
         --sp;
         node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
         const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
         const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
         mask = ((uint64_t)hi << 32) | lo;
-    }
+    } while (node != INVALID && --guard != 0);
+    if (guard == 0) c.overflow++;
     const bool hit = key != NO_HIT;
     if (hit) { best = __uint_as_float((uint32_t)(key >> 32)); best_leaf = (uint32_t)key; }
     return hit;
@@ -761,7 +621,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
                                                       int emit) {
     using PW = PrimaryWalk<K>;
     const int lim = LIM ? a.stack_limit : STACK_SIZE, lim4 = LIM ? a.stack_limit4 : STACK4;
-    constexpr int PST = PW::WIDE ? 3 * STACK4 : 3 * STACK_SIZE;   // per-wave packet stack words
+    constexpr int PST = PW::WIDE ? 3 * (STACK4 + 1) : 3 * STACK_SIZE;   // per-wave packet stack words (+ sentinel)
     __shared__ uint32_t s_pst[PW::PACKET ? 4 * PST : 1];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
@@ -782,12 +642,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     uint32_t bl = 0;
     bool phit = false;
     if (PW::WIDE)     // whole wave, before any divergence
-#if RTBVH_PACKET_PUSH == 2
-        phit = traverse_packet4_flat<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c,
+        phit = traverse_packet4<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c,
                                             s_pst + w * PST);
-#else
-        phit = traverse_packet4<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c, s_pst + w * PST);
-#endif
     else if (PW::PACKET)
         phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, lim, best, bl, c,
                                                    s_pst + w * PST);

@@ -2,6 +2,7 @@
 """A/B traversal walk flags (or, with AB_SET=base, two library builds via RTBVH_LIB) on the C5 frame in ONE process (interleaved
 rounds, cdna_hip_programming.md §5.4 rule 24).  Every variant's framebuffer must
 equal the baseline's bit for bit.  Prints one JSON line per variant."""
+import hashlib
 import json
 import os
 import sys
@@ -62,7 +63,8 @@ def main():
                 if ref is None:
                     ref = fb
                 ndiff = int((fb != ref).any(axis=-1).sum())
-                print(json.dumps({"variant": v, "pixels_differing_from_first": ndiff}), flush=True)
+                sha = hashlib.sha1(fb.tobytes()).hexdigest()[:16]   # compare across RTBVH_LIB builds
+                print(json.dumps({"variant": v, "pixels_differing_from_first": ndiff, "frame_sha1": sha}), flush=True)
     for (v, srt), xs in res.items():
         a = np.array(xs)
         print(json.dumps({"variant": v, "primary_ms_med": float(np.median(a[:, 0])),

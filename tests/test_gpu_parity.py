@@ -510,12 +510,13 @@ def test_wide_view_records_match_binary_tree():
         e = par[k] - T                       # parent internal index
         side = 0 if nodes["child_l"][par[k]] == k else 1
         rec, fr = w4[2 * e + side], f[2 * e + side]
-        if k < T:   # leaf
+        if k < T:   # leaf: its box, then the absent child's (the same box, min.z a quiet NaN)
             assert rec[12] == (0x80000000 | k) and rec[13] == 0xFFFFFFFF and rec[14] == (0x80000000 | k)
             lo, hi = box(fr, 0)
             np.testing.assert_array_equal(lo, nodes["bb_min"][k])
             np.testing.assert_array_equal(hi, nodes["bb_max"][k])
             assert rec[15] == 3 * _general_box(lo, hi)
+            assert list(rec[4:8]) == list(rec[0:4]) and rec[10] == 0x7FC00000 and rec[11] == rec[9]
         else:
             cl, cr = nodes["child_l"][k], nodes["child_r"][k]
             ids = [(0x80000000 | x) if x < T else x - T for x in (cl, cr)]
