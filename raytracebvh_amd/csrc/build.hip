@@ -477,20 +477,27 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes(const Inner* __restrict__ rec,
     qnode_from_pair(r, qn + slot_of(pint[k0 + tid], T));   // pint[0] = INVALID: the root
 }
 
+// The crossing nodes of refit workgroup b are xlist[b * RBLOCK, + xcnt[b]): one wave per
+// refit workgroup walks them (a few dozen typically; up to RBLOCK for a degenerate tree).
+constexpr uint32_t XWAVES = BLOCK / 64;
+template <class F>
+__device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f) {
+    const uint32_t b = blockIdx.x * XWAVES + (threadIdx.x >> 6);
+    if (b * RBLOCK >= a.T) return;
+    const uint32_t n = a.xcnt[b];
+    for (uint32_t j = threadIdx.x & 63u; j < n; j += 64) f(a.xlist[b * RBLOCK + j]);
+}
 // QNodes of the nodes whose leaf range crosses a refit workgroup (k_refit quantizes the
 // others): a scan of the 16-B topology records, the pair loads for the crossing ones only.
 // (A list appended by the climbing threads serialised on its one counter: ~88 adds per us.)
-__global__ __launch_bounds__(BLOCK) void k_qnodes_cross(const Inner* __restrict__ rec, const uint4* __restrict__ topo,
-                                                        const uint32_t* __restrict__ pint, QNode* __restrict__ qn,
-                                                        uint32_t T) {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k + 1 >= T) return;
-    if (!crossing(topo[k], k)) return;
-    const float4* src = reinterpret_cast<const float4*>(rec + 2 * (size_t)k);
-    float4 r[8];
+__global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
+    for_crossing(a, [&](uint32_t k) {
+        const float4* src = reinterpret_cast<const float4*>(a.rec + 2 * (size_t)k);
+        float4 r[8];
 #pragma unroll
-    for (int w = 0; w < 8; w++) r[w] = src[w];
-    qnode_from_pair(r, qn + slot_of(pint[k], T));
+        for (int w = 0; w < 8; w++) r[w] = src[w];
+        qnode_from_pair(r, a.qnode + slot_of(a.pint[k], a.T));
+    });
 }
 
 // Refit (BVHConstructP2.hlsl:8-37) fused with the leaf records and the node outputs.  One
@@ -512,11 +519,13 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     __shared__ float s_box[RBLOCK][2][6];   // node base + k: the boxes of its children (side 0, 1)
     __shared__ uint4 s_topo[RBLOCK];        // the block's nodes [base, base + BLOCK): ids, leaf range
     __shared__ uint32_t s_pint[RBLOCK];
+    __shared__ uint32_t s_xn;
     const uint32_t T = a.T;
     const uint32_t base = blockIdx.x * RBLOCK, tid = threadIdx.x;
     const uint32_t i = base + tid;
     const uint32_t end = base + RBLOCK;
     s_cnt[tid] = 0;
+    if (tid == 0) s_xn = 0;
     if (i + 1 < T) {   // coalesced, so the in-block climb makes no dependent global loads
         s_topo[tid] = a.topo[i];
         s_pint[tid] = a.pint[i];
@@ -563,10 +572,25 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
         }
     }
     __syncthreads();
-    // 3. the block's in-block nodes: record, leaf pseudo-records, QNode
-    if (i + 1 >= T) return;
+    // the block's crossing nodes (k_refit_top completes them, k_qnodes_cross quantizes them):
+    // listed at xlist[base, ...) in wave order, their tickets zeroed (no other ticket is used)
     const uint4 q = s_topo[tid];
-    if (!(q.z >= base && q.w < end)) return;   // crossing: k_refit_top completes it, k_qnodes_cross quantizes it
+    const bool xnode = i + 1 < T && !(q.z >= base && q.w < end);
+    const uint64_t xb = __ballot(xnode);
+    if (xb) {
+        const uint32_t lane = tid & 63u;
+        uint32_t wbase = 0;
+        if (lane == (uint32_t)(__ffsll((unsigned long long)xb) - 1)) wbase = atomicAdd(&s_xn, (uint32_t)__popcll(xb));
+        wbase = __shfl(wbase, __ffsll((unsigned long long)xb) - 1, 64);
+        if (xnode) {
+            a.xlist[base + wbase + (uint32_t)__popcll(xb & ((1ull << lane) - 1))] = i;
+            a.refit_cnt[i] = 0;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) a.xcnt[blockIdx.x] = s_xn;
+    // 3. the block's in-block nodes: record, leaf pseudo-records, QNode
+    if (i + 1 >= T || xnode) return;
     const float* L = s_box[tid][0];
     const float* R = s_box[tid][1];
     const f3 l0 = mk(L[0], L[1], L[2]), l1 = mk(L[3], L[4], L[5]);
@@ -608,11 +632,8 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
 // subtree).  Node k's thread: both children non-crossing -> k is complete, climb from it; one
 // -> arrive at k's ticket for that child (the other arrives by a climb); none -> nothing.  A
 // separate launch, so that k_refit's workgroups never wait on the global climb's latency.
-__global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k + 1 >= a.T) return;
+__device__ __forceinline__ void refit_top_node(const BuildArgs& a, uint32_t k) {
     const uint4 q = a.topo[k];
-    if (!crossing(q, k)) return;
     const bool ncl = (q.x & LEAF_BIT) || !crossing(a.topo[q.x], q.x);
     const bool ncr = (q.y & LEAF_BIT) || !crossing(a.topo[q.y], q.y);
     if (!ncl && !ncr) return;
@@ -636,6 +657,9 @@ __global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
         else      complete_node(a, k, e, blo, bhi, smin, smax, lo, hi);
     }
     refit_climb(lo, hi, e, a);
+}
+__global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
+    for_crossing(a, [&](uint32_t k) { refit_top_node(a, k); });
 }
 
 __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
@@ -855,12 +879,14 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s) {
     if (a.T > 1)
         hipLaunchKernelGGL(k_qnodes, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.rec, a.pint, a.qnode, a.T);
 }
+uint32_t refit_blocks(uint32_t T) { return (T + RBLOCK - 1) / RBLOCK; }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_refit, dim3((a.T + RBLOCK - 1) / RBLOCK), dim3(RBLOCK), 0, s, a);
-    if (a.T > RBLOCK) hipLaunchKernelGGL(k_refit_top, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
-    if (a.T > RBLOCK)   // the crossing nodes' QNodes: a few per workgroup of k_refit
-        hipLaunchKernelGGL(k_qnodes_cross, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a.rec, a.topo, a.pint, a.qnode,
-                           a.T);
+    const uint32_t nb = refit_blocks(a.T);
+    hipLaunchKernelGGL(k_refit, dim3(nb), dim3(RBLOCK), 0, s, a);
+    if (a.T > RBLOCK) {   // the crossing nodes: climbed, then quantized (a few per workgroup of k_refit)
+        hipLaunchKernelGGL(k_refit_top, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL(k_qnodes_cross, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
+    }
 }
 void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
     hipLaunchKernelGGL(k_export, dim3(blocks_for(2 * (size_t)a.T - 1)), dim3(BLOCK), 0, s, a, (RefNode*)out);

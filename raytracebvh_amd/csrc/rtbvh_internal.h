@@ -51,6 +51,8 @@ struct BuildArgs {
     uint32_t* pleaf;          // [T]
     uint32_t* pint;           // [T-1]
     uint32_t* refit_cnt;      // [T-1]
+    uint32_t* xlist;          // [T] k_refit workgroup b's crossing nodes at [b * RBLOCK, ...)
+    uint32_t* xcnt;           // [T / RBLOCK + 1] their counts
     float* rootbox;           // [6]
     QNode* qnode;             // [2T-1] quantized 4-wide nodes in slots (rtbvh_device.h), from rec
 };
@@ -58,8 +60,10 @@ void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
 // Karras topology (topo, pleaf, pint)
 void launch_karras(const BuildArgs& a, hipStream_t s);
-// leaf records + refit + node records + QNodes (refit_cnt zeroed first)
+// leaf records + refit + node records + QNodes (zeroes the tickets it uses)
 void launch_refit(const BuildArgs& a, hipStream_t s);
+// size of BuildArgs::xcnt for T leaves
+uint32_t refit_blocks(uint32_t T);
 // qnode[k] of every internal node from the record pairs
 void launch_qnodes(const BuildArgs& a, hipStream_t s);
 // the whole build in one workgroup for T <= small_build_max() (sorted pairs into
