@@ -72,6 +72,7 @@ struct rtbvh_ctx {
     uint32_t* d_qcount = nullptr;             // [32 x MAXSPLIT]: per pipeline, queue counts [0..15] and
                                               //   bounce work counters [16..31]
     float2* d_hit = nullptr;                  // per queued bounce ray: (t, leaf | INVALID)
+    uint32_t* d_next = nullptr;               // [NEXT_WORDS x MAXSPLIT]: segmented bounce work counters
     // pipelines 1.. of a split trace (pipeline 0 = d_q / d_hit on the context stream): a
     // rank's bands dealt over `nsplit` independent primary -> bounce chains on their own
     // streams, so one chain's kernel tail overlaps the others' work
@@ -190,6 +191,7 @@ rtbvh_status ensure_trace_capacity(rtbvh_ctx* c, size_t P) {
     HIPC(c, dalloc(c->d_bscratch, sort_scratch_words((uint32_t)P)));
     HIPC(c, dalloc(c->d_hit, P));
     if (!c->d_qcount) HIPC(c, dalloc(c->d_qcount, 32 * rtbvh_ctx::MAXSPLIT));
+    if (!c->d_next) HIPC(c, dalloc(c->d_next, (size_t)NEXT_WORDS * rtbvh_ctx::MAXSPLIT));
     if (!c->d_counters) HIPC(c, dalloc(c->d_counters, 64 * rtbvh_ctx::MAXSPLIT));
     c->cap_P = P;
     return RTBVH_OK;
@@ -429,6 +431,9 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
     HIPC(c, hipMemsetAsync(c->d_qcount + 32 * slot, 0, 32 * nsplit * sizeof(uint32_t), s));
+    if (refill && bounces)
+        HIPC(c, hipMemsetAsync(c->d_next + (size_t)NEXT_WORDS * slot, 0,
+                               (size_t)NEXT_WORDS * nsplit * sizeof(uint32_t), s));
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (nsplit > 1) HIPC(c, hipEventRecord(c->ev_fork, s));
     for (uint32_t g = 0; g < nsplit; g++) {
@@ -441,6 +446,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         RayQ* q[2] = {b ? c->d_qs[b][0] : c->d_q[0], b ? c->d_qs[b][1] : c->d_q[1]};
         float2* hit = b ? c->d_hits[b] : c->d_hit;
         uint32_t* qc = c->d_qcount + 32 * b;
+        uint32_t* nx = c->d_next + (size_t)NEXT_WORDS * b;
         const bool tg = timing && g == 0;   // stage events: chain 0's kernels
         launch_primary(ag, q[0], &qc[0], count, bounces > 0, wk.primary, sg);
         if (tg) HIPC(c, hipEventRecord(ev[1], sg));
@@ -453,7 +459,8 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             }
             if (refill) {
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[3], sg));
-                launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, wk.bounce, hit, &qc[16 + b], tblocks, sg);
+                launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, wk.bounce, hit,
+                                       nx + (size_t)NEXT_SEGS * NEXT_STRIDE * b, tblocks, sg);
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[4], sg));
                 launch_bounce_shade(ag, q[b & 1], &qc[b], hit, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
                                     Pg, sg);
@@ -583,7 +590,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode);
     dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox);
-    dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_hit);
+    dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
     dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);
     dfree(c->d_texels); dfree(c->d_texinfo); dfree(c->d_srgb);

@@ -111,8 +111,15 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 // one ray per lane bounce pass (reference order or nearest-first), shading included
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
                    uint32_t* qout_count, bool count, bool emit, bool nearest, hipStream_t s);
-// bounce pass as persistent refill traversal (hit records) + shading kernel; `next` is a
-// zeroed work counter; `blocks` persistent workgroups (0: 2048)
+// bounce pass as persistent refill traversal (hit records) + shading kernel; `next` holds
+// NEXT_SEGS zeroed work counters NEXT_STRIDE words apart (one per queue segment);
+// `blocks` persistent workgroups (0: 2048)
+#ifndef RTBVH_NEXT_SEGS
+#define RTBVH_NEXT_SEGS 32
+#endif
+constexpr uint32_t NEXT_SEGS = RTBVH_NEXT_SEGS;
+constexpr uint32_t NEXT_STRIDE = 32;                          // one 128-B line per counter
+constexpr uint32_t NEXT_WORDS = 16 * NEXT_SEGS * NEXT_STRIDE;  // per buffer set: bounce passes 0..15
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
                             hipStream_t s);

@@ -752,7 +752,24 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __
 // A wave refills when at least REFILL_MIN lanes are idle.  A/B on C5 (bounce pass):
 // 4 -> 15.6 ms, 8 -> 9.2, 16 -> 5.5, 24 -> 4.13, 32 -> 3.87, 40 -> 3.84, 48 -> 3.90,
 // 64 -> 5.36 (the single work counter's atomic contention below 32).
-constexpr uint32_t REFILL_MIN = 32;
+// Work counters: the queue is cut into NEXT_SEGS contiguous segments, each with its own
+// counter on its own 128-B line.  Workgroup b runs on XCD b % 8 (round-robin dispatch); its
+// waves claim from the segments of their XCD first (starting at one picked by b / 8), then from
+// the other XCDs' in turn.  A single counter serialised the claims of all 8192 waves (~88 per
+// us), which is what kept REFILL_MIN from going lower; and an XCD's waves now walk rays of
+// neighbouring queue positions (neighbouring pixels), whose upper-tree nodes its L2 shares.
+#ifndef RTBVH_REFILL_MIN
+#define RTBVH_REFILL_MIN 16
+#endif
+constexpr uint32_t REFILL_MIN = RTBVH_REFILL_MIN;
+constexpr uint32_t XCDS = 8;
+constexpr uint32_t SEGS_PER_XCD = NEXT_SEGS >= XCDS ? NEXT_SEGS / XCDS : 1;
+__device__ __forceinline__ uint32_t claim_segment(uint32_t k) {   // the wave's k-th segment
+    if (NEXT_SEGS < XCDS) return k;
+    const uint32_t xcd = blockIdx.x % XCDS, sub = (blockIdx.x / XCDS) % SEGS_PER_XCD;
+    const uint32_t g = (xcd + k / SEGS_PER_XCD) % XCDS;
+    return g * SEGS_PER_XCD + (sub + k) % SEGS_PER_XCD;
+}
 
 __device__ __forceinline__ void sort2(float& ta, uint32_t& ia, float& tb, uint32_t& ib) {
     const bool sw = tb < ta;
@@ -799,6 +816,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     const int limit = LIM ? stack_limit : WIDE ? STACK4 : STACK_SIZE;
     const uint32_t n = *qin_count;
+    if (n == 0) return;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0, 0, 0};
     bool has = false, hit = false;
@@ -830,20 +848,24 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         ++sp;
     };
     bool drained = false;
+    uint32_t kseg = 0;   // segments claimed from so far (wave-uniform)
     unsigned long long wsteps = 0, mixed = 0, active_lanes = 0;
     while (true) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (!drained && (nidle >= REFILL_MIN || nidle == 64)) {
+            const uint32_t seg = claim_segment(kseg);
+            const uint32_t s0 = (uint32_t)((uint64_t)n * seg / NEXT_SEGS);
+            const uint32_t len = (uint32_t)((uint64_t)n * (seg + 1) / NEXT_SEGS) - s0;
             uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(next, nidle);
+            if (lane == 0) base = atomicAdd(next + NEXT_STRIDE * seg, nidle);
             base = __builtin_amdgcn_readfirstlane(base);
-            if (base + nidle >= n) drained = true;   // nothing left after these
+            if (base + nidle >= len && ++kseg == NEXT_SEGS) drained = true;   // segment (and the last) used up
             if (!has) {
                 const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
                 const uint32_t p = base + (uint32_t)__popcll(idle & lt);
-                if (p < n) {
-                    r = perm ? perm[p] : p;
+                if (p < len) {
+                    r = perm ? perm[s0 + p] : s0 + p;
                     const float4 q0 = reinterpret_cast<const float4*>(qin + r)[0];
                     const float4 q1 = reinterpret_cast<const float4*>(qin + r)[1];
                     o = mk(q0.z, q0.w, q1.x);
@@ -860,8 +882,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 }
             }
         }
-        // every refill either hands out rays or sets `drained`, so a wave with no ray left
-        // loops back to refill until the queue is drained
+        // every refill either hands out rays or moves on to the next segment (the last one
+        // sets `drained`), so a wave with no ray left loops back to refill until the queue is drained
         if (__ballot(has) == 0 && drained) break;
         if (COUNT) {   // wave-level divergence census (stats trav_*; all lanes converged here)
             const uint64_t act = __ballot(has);
