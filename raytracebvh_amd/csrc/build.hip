@@ -207,7 +207,7 @@ __device__ void karras_node(const C& c, uint32_t n, uint32_t i, uint4* __restric
 // leaf record of sorted position i: gather the clip-space triangle once, store
 // (v0, e1, e2) for the triangle test (the reference's edge1/edge2, :43-44) and
 // the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
-__device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i, f3& lo, f3& hi) {
+__device__ __forceinline__ void leaf_record_words(const BuildArgs& a, uint32_t i, f3& lo, f3& hi, float4 (&r)[4]) {
     const uint32_t t = a.sorted_vals[i];
     const float4* src = a.tclip + 3 * (size_t)t;
     const float4 s0 = src[0], s1 = src[1], s2 = src[2];
@@ -217,11 +217,39 @@ __device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i, f3& 
     hi = vmax(v0, v1);
     lo = vmin(lo, v2);
     hi = vmax(hi, v2);
+    r[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
+    r[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+    r[2] = make_float4(e2.z, __uint_as_float(t), lo.x, lo.y);
+    r[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
+}
+__device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i, f3& lo, f3& hi) {
+    float4 r[4];
+    leaf_record_words(a, i, lo, hi, r);
     float4* dst = a.leaf + 4 * (size_t)i;
-    dst[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
-    dst[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
-    dst[2] = make_float4(e2.z, __uint_as_float(t), lo.x, lo.y);
-    dst[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
+    dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2]; dst[3] = r[3];
+}
+// 64-B records of consecutive indices, one per lane, written with every store instruction of
+// the wave covering 1 KB contiguously (16 B per lane): each half-wave's records are staged in
+// LDS (`buf`: 128 float4 of this wave's own) and read back transposed.  MI355X (scripts/
+// write_roofline.hip): 16-B-per-lane stores stream at 4.1 TB/s, a 64-B record per lane at
+// 2.5-2.9 TB/s.  `n` records start at dst (lanes >= n hold none); the whole block calls it.
+__device__ __forceinline__ void staged_records(float4* __restrict__ dst, uint32_t n, const float4 (&r)[4],
+                                               float4* buf) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+        if ((lane >> 5) == h) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) buf[4 * (lane & 31u) + k] = r[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t m = 0; m < 2; m++) {
+            const uint32_t w = lane + 64 * m;                   // float4 w of this half-wave's 32 records
+            if (32 * h + (w >> 2) < n) dst[128 * h + w] = buf[w];
+        }
+        __syncthreads();
+    }
 }
 // BVHConstructP1.hlsl:167-188: internal node i for every i < T-1 (topology only: child ids,
 // leaf range, parent links); the root's parent is UINT_MAX (:186-187).  The leaf records are
@@ -516,7 +544,10 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
 // back except for the listed crossing nodes.
 __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     __shared__ uint32_t s_cnt[RBLOCK];
-    __shared__ float s_box[RBLOCK][2][6];   // node base + k: the boxes of its children (side 0, 1)
+    // node base + k: the boxes of its children (side 0, 1); before the climb, the staging
+    // buffer of the leaf-record stores (128 float4 per wave)
+    __shared__ __align__(16) float s_box[RBLOCK][2][6];
+    static_assert(sizeof(float) * 12 * RBLOCK >= 16 * 128 * (RBLOCK / 64), "leaf staging fits in s_box");
     __shared__ uint4 s_topo[RBLOCK];        // the block's nodes [base, base + BLOCK): ids, leaf range
     __shared__ uint32_t s_pint[RBLOCK];
     __shared__ uint32_t s_xn;
@@ -532,8 +563,14 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     }
     f3 lo = mk(0.f, 0.f, 0.f), hi = lo;
     uint32_t e = INVALID;
+    {
+        float4 r[4] = {};
+        if (i < T) leaf_record_words(a, i, lo, hi, r);
+        const uint32_t w0 = base + (tid & ~63u);   // this wave's first leaf
+        staged_records(a.leaf + 4 * (size_t)w0, T > w0 ? min(64u, T - w0) : 0u, r,
+                       reinterpret_cast<float4*>(&s_box[0][0][0]) + 128 * (tid >> 6));
+    }
     if (i < T) {
-        leaf_record(a, i, lo, hi);
         if (T == 1) {
             a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
             a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
