@@ -261,23 +261,33 @@ __device__ __forceinline__ void staged_records(float4* __restrict__ dst, uint32_
 // the deep nodes' ranges are short -- are staged in LDS (a window of KWIN codes either side);
 // codes outside the window come from global memory.
 constexpr int64_t KWIN = RTBVH_KARRAS_WIN;
+// the window lives in a file-scope LDS array so that its reads compile to ds_read (through a
+// generic pointer kept in the accessor they were flat loads, 8 per node)
+__shared__ uint32_t s_kwin[BLOCK + 2 * (KWIN > 0 ? KWIN : 0)];
 struct WindowCodes {
     const uint32_t* g;
-    const uint32_t* s;
-    int64_t lo, hi;   // the window [lo, hi) of the code sequence held in s
-    __device__ uint32_t operator[](int64_t j) const { return (j >= lo && j < hi) ? s[j - lo] : g[j]; }
+    int64_t lo, hi;   // the window [lo, hi) of the code sequence held in s_kwin
+    __device__ uint32_t operator[](int64_t j) const {
+        uint32_t v;
+        if (j >= lo && j < hi) {
+            v = s_kwin[j - lo];
+            asm volatile("" : "+v"(v));   // keeps the two loads apart (merged: one flat load of a selected pointer)
+        } else {
+            v = g[j];
+        }
+        return v;
+    }
 };
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_karras(BuildArgs a) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (KWIN > 0) {
-        __shared__ uint32_t s_codes[KWIN > 0 ? BLOCK + 2 * KWIN : 1];
         const int64_t base = (int64_t)blockIdx.x * BLOCK;
         const int64_t lo = base - KWIN > 0 ? base - KWIN : 0;
         const int64_t hi = base + BLOCK + KWIN < (int64_t)a.T ? base + BLOCK + KWIN : (int64_t)a.T;
-        for (int64_t j = lo + threadIdx.x; j < hi; j += BLOCK) s_codes[j - lo] = a.sorted_keys[j];
+        for (int64_t j = lo + threadIdx.x; j < hi; j += BLOCK) s_kwin[j - lo] = a.sorted_keys[j];
         __syncthreads();
-        const WindowCodes codes{a.sorted_keys, s_codes, lo, hi};
+        const WindowCodes codes{a.sorted_keys, lo, hi};
         if (i + 1 < a.T) karras_node<MODE>(codes, a.T, i, a.topo, a.pleaf, a.pint);
     } else {
         if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
