@@ -497,44 +497,102 @@ __device__ __forceinline__ void store_qnode(QNode* dst, const float (&lx)[4], co
     d[0] = qs[0]; d[1] = qs[1]; d[2] = qs[2]; d[3] = qs[3];
 }
 
-// The QNode of internal node k from its record pair (slots 2k, 2k+1: the four grandchild
-// boxes and ids), written at k's own slot pint[k] (the root's: 2T-2), so that siblings'
-// nodes share a 128-B line as the records do.  Internal grandchild ids become their slots
-// (2 * their parent + side; the parent's index is word 14 of its record).
-__device__ __forceinline__ void qnode_from_pair(const float4 (&r)[8], QNode* dst) {
-    const float4 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], b0 = r[4], b1 = r[5], b2 = r[6], b3 = r[7];
-    // record words (rtbvh_device.h): 0-1 l.min.xy 2-3 l.max.xy 4-5 r.min.xy 6-7 r.max.xy
-    // 8 l.min.z 9 l.max.z 10 r.min.z 11 r.max.z 12 id_l 13 id_r 14 own
-    // an absent grandchild (a pseudo-record's second box, NaN min.z) repeats the first box
-    const float lx[4] = {a0.x, a1.x, b0.x, b1.x}, ly[4] = {a0.y, a1.y, b0.y, b1.y};
-    const float lz[4] = {a2.x, __float_as_uint(a3.y) == INVALID ? a2.x : a2.z, b2.x,
-                         __float_as_uint(b3.y) == INVALID ? b2.x : b2.z};
-    const float hx[4] = {a0.z, a1.z, b0.z, b1.z}, hy[4] = {a0.w, a1.w, b0.w, b1.w}, hz[4] = {a2.y, a2.w, b2.y, b2.w};
-    const uint32_t ownl = __float_as_uint(a3.z), ownr = __float_as_uint(b3.z);
-    auto gslot = [](uint32_t id, uint32_t own, uint32_t side) {
-        return (id == INVALID || (id & LEAF_BIT)) ? id : 2 * own + side;
-    };
-    const uint4 ids = make_uint4(gslot(__float_as_uint(a3.x), ownl, 0), gslot(__float_as_uint(a3.y), ownl, 1),
-                                 gslot(__float_as_uint(b3.x), ownr, 0), gslot(__float_as_uint(b3.y), ownr, 1));
-    store_qnode(dst, lx, ly, lz, hx, hy, hz, ids);
+// ---- the grouping of a QNode (greedy collapse) ------------------------------------
+// A QNode holds up to four subtrees that partition its node's subtree.  Starting from the
+// node's two children, the internal entry with the largest box surface is replaced by its two
+// children, twice (fewer when the subtree runs out of internal nodes): the grouping a BVH4
+// collapse by largest area makes, so every QNode of a node with >= 4 leaves is full and the
+// entries are of similar size.  (The first form took the four grandchildren, a leaf child
+// counting once: ~half the QNodes near the leaves held 2-3 entries.)  The walk's result does
+// not depend on the grouping: every entry's box is the exact union of its subtree's leaves.
+struct QEnt {
+    uint32_t id;     // internal node index, or LEAF_BIT | j
+    uint32_t slot;   // where the entry's record / QNode lives (2 * parent + side)
+    float b[6];      // box: min xyz, max xyz
+};
+__device__ __forceinline__ float half_area(const float (&b)[6]) {
+    const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+    return dx * dy + dy * dz + dz * dx;   // NaN boxes compare false: never expanded
+}
+__device__ __forceinline__ void qent_sel(QEnt& d, const QEnt& s, bool take) {
+    d.id = take ? s.id : d.id;
+    d.slot = take ? s.slot : d.slot;
+#pragma unroll
+    for (int k = 0; k < 6; k++) d.b[k] = take ? s.b[k] : d.b[k];
+}
+// Kids(e, c0, c1): the two children of internal entry e
+template <class Kids>
+__device__ __forceinline__ void greedy_qnode(const QEnt& e0, const QEnt& e1, Kids&& kids, QNode* dst) {
+    QEnt E[4] = {e0, e1, e0, e0};
+    uint32_t n = 2;
+#pragma unroll
+    for (int step = 0; step < 2; step++) {
+        int pick = -1;
+        float best = -1.f;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if ((uint32_t)k < n && !(E[k].id & LEAF_BIT)) {
+                const float ar = half_area(E[k].b);
+                if (ar > best) { best = ar; pick = k; }
+            }
+        }
+        if (pick < 0) break;
+        QEnt sel = E[0];
+#pragma unroll
+        for (int k = 1; k < 3; k++) qent_sel(sel, E[k], k == pick);
+        QEnt c0, c1;
+        kids(sel, c0, c1);
+#pragma unroll
+        for (int k = 0; k < 3; k++) qent_sel(E[k], c0, k == pick);
+        qent_sel(E[2], c1, n == 2);
+        qent_sel(E[3], c1, n == 3);
+        ++n;
+    }
+    // positions: 4 entries in order; 3 -> the fourth absent; 2 -> at 0 and 2 (1 and 3 absent:
+    // the walk masks only positions 1 and 3 by their INVALID id).  An absent entry repeats box 0.
+    QEnt P[4] = {E[0], E[1], E[2], E[3]};
+    if (n == 2) { P[1] = E[0]; P[2] = E[1]; P[3] = E[0]; }
+    if (n == 3) P[3] = E[0];
+    const bool absent1 = n == 2, absent3 = n < 4;
+    float lx[4], ly[4], lz[4], hx[4], hy[4], hz[4];
+    uint32_t id[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        lx[k] = P[k].b[0]; ly[k] = P[k].b[1]; lz[k] = P[k].b[2];
+        hx[k] = P[k].b[3]; hy[k] = P[k].b[4]; hz[k] = P[k].b[5];
+        id[k] = (P[k].id & LEAF_BIT) ? P[k].id : P[k].slot;
+    }
+    if (absent1) id[1] = INVALID;
+    if (absent3) id[3] = INVALID;
+    store_qnode(dst, lx, ly, lz, hx, hy, hz, make_uint4(id[0], id[1], id[2], id[3]));
+}
+// entries from the node records in global memory (record words: rtbvh_device.h)
+__device__ __forceinline__ void record_kids(const Inner* __restrict__ rec, uint32_t slot, QEnt& c0, QEnt& c1) {
+    const float4* r = reinterpret_cast<const float4*>(rec + slot);
+    const float4 w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3];
+    const uint32_t own = __float_as_uint(w3.z);
+    c0.id = __float_as_uint(w3.x);
+    c1.id = __float_as_uint(w3.y);
+    c0.slot = 2 * own;
+    c1.slot = 2 * own + 1;
+    c0.b[0] = w0.x; c0.b[1] = w0.y; c0.b[2] = w2.x; c0.b[3] = w0.z; c0.b[4] = w0.w; c0.b[5] = w2.y;
+    c1.b[0] = w1.x; c1.b[1] = w1.y; c1.b[2] = w2.z; c1.b[3] = w1.z; c1.b[4] = w1.w; c1.b[5] = w2.w;
+}
+// the QNode of the node whose record is at `slot`, from the records (crossing nodes, small builds)
+__device__ __forceinline__ void qnode_from_records(const Inner* __restrict__ rec, uint32_t slot, QNode* dst) {
+    QEnt e0, e1;
+    record_kids(rec, slot, e0, e1);
+    greedy_qnode(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { record_kids(rec, e.slot, c0, c1); }, dst);
 }
 
-// QNodes of internal nodes [k0, k0 + BLOCK) from their record pairs (the one-workgroup
-// build and rtbvh_build_from_codes): coalesced loads into LDS (one float4 of padding per
-// pair: the per-node ds_read_b128 at a 144-B stride is bank-conflict free), one node per thread.
+// QNodes of every internal node from the records (the one-workgroup build and
+// rtbvh_build_from_codes), one node per thread.
 __global__ __launch_bounds__(BLOCK) void k_qnodes(const Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
                                                   QNode* __restrict__ qn, uint32_t T) {
-    __shared__ float4 s_pair[BLOCK * 9];
-    const uint32_t k0 = blockIdx.x * BLOCK, tid = threadIdx.x;
-    const uint32_t nn = min(BLOCK, T - 1 - k0);   // nodes of this workgroup
-    const float4* src = reinterpret_cast<const float4*>(rec + 2 * (size_t)k0);
-    for (uint32_t j = tid; j < 8 * nn; j += BLOCK) s_pair[j + j / 8] = src[j];
-    __syncthreads();
-    if (tid >= nn) return;
-    float4 r[8];
-#pragma unroll
-    for (int w = 0; w < 8; w++) r[w] = s_pair[9 * tid + w];
-    qnode_from_pair(r, qn + slot_of(pint[k0 + tid], T));   // pint[0] = INVALID: the root
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k + 1 >= T) return;
+    const uint32_t slot = slot_of(pint[k], T);   // pint[0] = INVALID: the root
+    qnode_from_records(rec, slot, qn + slot);
 }
 
 // The crossing nodes of refit workgroup b are xlist[b * RBLOCK, + xcnt[b]): one wave per
@@ -552,11 +610,8 @@ __device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f) {
 // (A list appended by the climbing threads serialised on its one counter: ~88 adds per us.)
 __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
     for_crossing(a, [&](uint32_t k) {
-        const float4* src = reinterpret_cast<const float4*>(a.rec + 2 * (size_t)k);
-        float4 r[8];
-#pragma unroll
-        for (int w = 0; w < 8; w++) r[w] = src[w];
-        qnode_from_pair(r, a.qnode + slot_of(a.pint[k], a.T));
+        const uint32_t slot = slot_of(a.pint[k], a.T);
+        qnode_from_records(a.rec, slot, a.qnode + slot);
     });
 }
 
@@ -666,34 +721,24 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     const f3 r0 = mk(R[0], R[1], R[2]), r1 = mk(R[3], R[4], R[5]);
     const uint32_t slot = slot_of(s_pint[tid], T);
     store_record(a.rec + slot, l0, l1, r0, r1, q.x, q.y, i);
-    float gx[4], gy[4], gz[4], hx[4], hy[4], hz[4];
-    uint32_t gid[4];
+    if (q.x & LEAF_BIT) store_leaf_record(a.rec, i, 0, q.x, l0, l1);
+    if (q.y & LEAF_BIT) store_leaf_record(a.rec, i, 1, q.y, r0, r1);
+    // the QNode: its entries' boxes are in LDS (an in-block node's subtree is in the block)
+    const auto lds_kids = [&](uint32_t x, QEnt& c0, QEnt& c1) {   // children of in-block node x
+        const uint4 xq = s_topo[x - base];
+        c0.id = xq.x;
+        c1.id = xq.y;
+        c0.slot = 2 * x;
+        c1.slot = 2 * x + 1;
 #pragma unroll
-    for (int sd = 0; sd < 2; sd++) {
-        const uint32_t c = sd ? q.y : q.x;
-        if (c & LEAF_BIT) {   // a leaf child: itself, and no second grandchild (as its pseudo-record)
-            store_leaf_record(a.rec, i, sd, c, sd ? r0 : l0, sd ? r1 : l1);
-            const float* b = sd ? R : L;
-#pragma unroll
-            for (int g = 0; g < 2; g++) {
-                gx[2 * sd + g] = b[0]; gy[2 * sd + g] = b[1]; gz[2 * sd + g] = b[2];
-                hx[2 * sd + g] = b[3]; hy[2 * sd + g] = b[4]; hz[2 * sd + g] = b[5];
-            }
-            gid[2 * sd] = c;
-            gid[2 * sd + 1] = INVALID;
-        } else {              // an internal child: in-block too (its range is inside this node's)
-            const uint4 cq = s_topo[c - base];
-#pragma unroll
-            for (int g = 0; g < 2; g++) {
-                const float* b = s_box[c - base][g];
-                gx[2 * sd + g] = b[0]; gy[2 * sd + g] = b[1]; gz[2 * sd + g] = b[2];
-                hx[2 * sd + g] = b[3]; hy[2 * sd + g] = b[4]; hz[2 * sd + g] = b[5];
-                const uint32_t gcid = g ? cq.y : cq.x;
-                gid[2 * sd + g] = (gcid & LEAF_BIT) ? gcid : 2 * c + g;
-            }
+        for (int k = 0; k < 6; k++) {
+            c0.b[k] = s_box[x - base][0][k];
+            c1.b[k] = s_box[x - base][1][k];
         }
-    }
-    store_qnode(a.qnode + slot, gx, gy, gz, hx, hy, hz, make_uint4(gid[0], gid[1], gid[2], gid[3]));
+    };
+    QEnt e0, e1;
+    lds_kids(i, e0, e1);
+    greedy_qnode(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, a.qnode + slot);
 }
 
 // The crossing nodes (a few per k_refit workgroup, the top of the tree among them): k_refit

@@ -533,9 +533,10 @@ def test_wide_view_records_match_binary_tree():
 @pytest.mark.parametrize("scene", ["synthetic", "general boxes", "Test"])
 def test_qnodes_contain_the_exact_boxes(scene):
     """Quantized node of internal node k (rtbvh_device.h QNode) at k's slot: power-of-two grid
-    steps, the grandchildren of the record pair at slots 2k, 2k+1 (internal ones by their
-    slots), and decoded corners (origin + q * step in fp32, the traversal's arithmetic)
-    that contain every grandchild's exact box."""
+    steps, the entries of the largest-area greedy collapse (build.hip greedy_qnode: from k's
+    two children, the internal entry with the largest box surface replaced by its children,
+    twice; internal entries by their slots), and decoded corners (origin + q * step in fp32,
+    the traversal's arithmetic) that contain every entry's exact box."""
     if scene == "synthetic":
         s = rt.synthetic(20_000, seed=7, half_extent=(30, 30, 20))
     elif scene == "general boxes":
@@ -570,10 +571,32 @@ def test_qnodes_contain_the_exact_boxes(scene):
     dlo = org[:, :, None] + lo * scl[:, :, None]   # q * step exact; one rounding in the add
     dhi = org[:, :, None] + hi * scl[:, :, None]
     top = np.full((T - 1, 3), -np.inf, dtype=np.float32)   # the exact max corner of the four boxes
+    bmin, bmax = nodes["bb_min"], nodes["bb_max"]
+
+    def area(g):   # fp32, the kernel's operation order
+        d = (bmax[g] - bmin[g]).astype(np.float32)
+        return (d[0] * d[1] + d[1] * d[2]) + d[2] * d[0]
+
+    def greedy(x):
+        ents = [cl[x], cr[x]]
+        for _ in range(2):
+            best, pick = np.float32(-1), -1
+            for idx in range(min(len(ents), 3)):
+                if ents[idx] >= T:
+                    ar = area(ents[idx])
+                    if ar > best:
+                        best, pick = ar, idx
+            if pick < 0:
+                break
+            g = ents[pick]
+            ents[pick] = cl[g]
+            ents.append(cr[g])
+        if len(ents) == 2:
+            return [ents[0], None, ents[1], None]
+        return ents + [None] * (4 - len(ents))
+
     for k in range(T - 1):
-        gc = []
-        for ch in (cl[T + k], cr[T + k]):
-            gc += [ch, None] if ch < T else [cl[ch], cr[ch]]
+        gc = greedy(T + k)
         ids = [0xFFFFFFFF if g is None else ((0x80000000 | g) if g < T else slot(g)) for g in gc]
         assert list(q[k, 12:16]) == ids, k
         for cidx, g in enumerate(gc):
