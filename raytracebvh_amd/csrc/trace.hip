@@ -781,13 +781,12 @@ __device__ __forceinline__ void sort2(float& ta, uint32_t& ia, float& tb, uint32
     ia = i;
 }
 
-// bf16 of an entry distance rounded toward -inf (so bf16_up(bf16_down(t)) <= t: positive t
-// truncated, negative t rounded away from zero; infinities and NaNs keep their class)
-__device__ __forceinline__ uint16_t bf16_down(float t) {
-    uint32_t b = __float_as_uint(t);
-    if ((b & 0x80000000u) && (b & 0xFFFFu) && (b & 0x7F800000u) != 0x7F800000u) b += 0x10000u;
-    return (uint16_t)(b >> 16);
-}
+// A 16-bit key for an entry distance t that never exceeds it: the upper half of max(t, 0)
+// (fmaxf drops NaN).  Positive t is truncated (rounded down); t <= 0 becomes 0, which is below
+// every best distance (a hit's t > EPSILON), as t is: an entry is dropped on pop only when the
+// exact test would drop it too.  One v_max_f32; the store takes the high half (the first
+// form rounded negative t away from zero: six VALU and two SALU per push).
+__device__ __forceinline__ uint16_t bf16_down(float t) { return (uint16_t)(__float_as_uint(fmaxf(t, 0.f)) >> 16); }
 __device__ __forceinline__ float bf16_up(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 // Walk modes of k_bounce_trav: 0 reference order, 1 nearest-first (binary records), 2 the
