@@ -32,6 +32,7 @@ struct rtbvh_ctx {
     Mat* d_mats = nullptr;
     float wvp[16], wv[16];
     bool have_scene = false, have_camera = false, built = false;
+    bool built_clz64 = false;   // the BVH was built with the clz64 delta: a valid tree (no cycles)
 
     // build buffers (capacity cap_T)
     uint32_t cap_T = 0;
@@ -289,6 +290,7 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.stack_limit = lim && lim < (uint32_t)STACK_SIZE ? (int)lim : STACK_SIZE;
     a.stack_limit4 = lim && lim < (uint32_t)STACK4 ? (int)lim : STACK4;
     a.limited = lim != 0 && lim < (uint32_t)STACK4;
+    a.acyclic = c->built_clz64;
     return a;
 }
 
@@ -727,6 +729,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         if (timing) c->n_builds++;
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
         c->built = true;
+        c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
         return check_launch(c, "build kernel");
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
@@ -744,6 +747,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (timing) c->n_builds++;
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
     c->built = true;
+    c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
     return check_launch(c, "build kernels");
 }
 
@@ -818,6 +822,7 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
     c->nranks = 1;
     c->last_slot = 0;
     c->traced = c->built = true;
+    c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
     c->frame_here = c->intensity_here = true;
     return rtbvh_synchronize(c);
 }

@@ -97,6 +97,8 @@ struct TraceArgs {
     unsigned long long* overflow;   // stack overflows / guard trips, accumulated over every trace (never reset)
     int stack_limit, stack_limit4;  // stack entries the binary / 4-wide walks may use (<= STACK_SIZE / STACK4)
     bool limited;                   // a limit below a capacity: the kernels read the limits (else constants)
+    bool acyclic;                   // built with the clz64 delta (a radix tree): the 4-wide primary walk
+                                    //   needs no walk-length guard
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)

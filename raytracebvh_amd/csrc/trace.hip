@@ -340,7 +340,7 @@ template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t
 // pushes with the parent-mask AND, 2.23 with the lanes-0..3 form, 2.20 with the sentinel and
 // the NaN min.z, 2.18 with the z test as its own lane mask (VALU -> SALU); a branchless tail
 // (descend or pop by selects, the stack top read at the step's start) ran 2.45.
-template <bool COUNT>
+template <bool COUNT, bool GUARD>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
                                                  uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
                                                  uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*(STACK4+1)] */) {
@@ -448,19 +448,21 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
         const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
         const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
         mask = ((uint64_t)hi << 32) | lo;
-    } while (node != INVALID && --guard != 0);
-    if (guard == 0) c.overflow++;
+    } while (node != INVALID && (!GUARD || --guard != 0));
+    if (GUARD && guard == 0) c.overflow++;
     const bool hit = key != NO_HIT;
     if (hit) { best = __uint_as_float((uint32_t)(key >> 32)); best_leaf = (uint32_t)key; }
     return hit;
 }
 
 // Primary walks: 0 per-lane reference order, 1 per-lane nearest-first,
-// 2 packet reference order, 3 packet nearest-first, 4 4-wide packet (axis-parallel test)
+// 2 packet reference order, 3 packet nearest-first, 4 4-wide packet (axis-parallel test),
+// 5 the same without the walk-length guard (a clz64 tree has no cycles; ~6 SALU per step)
 template <int K> struct PrimaryWalk {
     static constexpr bool NEAREST = (K == 1 || K == 3);
     static constexpr bool PACKET = (K >= 2);
-    static constexpr bool WIDE = (K == 4);
+    static constexpr bool WIDE = (K >= 4);
+    static constexpr bool GUARD = (K != 5);   // 5: the 4-wide walk on a clz64 tree (acyclic)
 };
 
 struct HitInfo {
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     uint32_t bl = 0;
     bool phit = false;
     if (PW::WIDE)     // whole wave, before any divergence
-        phit = traverse_packet4<COUNT>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c,
+        phit = traverse_packet4<COUNT, PW::GUARD>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c,
                                             s_pst + w * PST);
     else if (PW::PACKET)
         phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, lim, best, bl, c,
@@ -1216,7 +1218,10 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
         case PrimaryKind::LANE_NEAREST: launch_primary_c<1>(a, q, qcount, count, emit, grid, s); break;
         case PrimaryKind::PACKET_REFERENCE: launch_primary_c<2>(a, q, qcount, count, emit, grid, s); break;
         case PrimaryKind::PACKET_NEAREST: launch_primary_c<3>(a, q, qcount, count, emit, grid, s); break;
-        case PrimaryKind::PACKET_WIDE: launch_primary_c<4>(a, q, qcount, count, emit, grid, s); break;
+        case PrimaryKind::PACKET_WIDE:
+            if (a.acyclic) launch_primary_c<5>(a, q, qcount, count, emit, grid, s);
+            else launch_primary_c<4>(a, q, qcount, count, emit, grid, s);
+            break;
         default: launch_primary_c<0>(a, q, qcount, count, emit, grid, s); break;
     }
 }
