@@ -340,7 +340,11 @@ template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t
 // pushes with the parent-mask AND, 2.23 with the lanes-0..3 form, 2.20 with the sentinel and
 // the NaN min.z, 2.18 with the z test as its own lane mask (VALU -> SALU); a branchless tail
 // (descend or pop by selects, the stack top read at the step's start) ran 2.45.
-template <bool COUNT, bool GUARD>
+// GUARD false (a clz64 tree, k_primary walk 5): no walk-length guard, and without a run-time
+// stack limit (CHECK false) no stack check either: a clz64 tree has <= 64 internal levels (each
+// child's common-prefix length exceeds its parent's, 0..63), a step descends two levels and
+// pushes <= 3 entries, so the stack holds <= 3 * 32 + 1 < STACK4 + 1 entries.
+template <bool COUNT, bool GUARD, bool CHECK>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
                                                  uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
                                                  uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*(STACK4+1)] */) {
@@ -426,7 +430,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             if (hs != 0) {
                 const uint32_t rest = hs & (hs - 1);
                 const int npush = __builtin_popcount(rest);
-                if (sp + npush <= limit + 1) {
+                if (!CHECK || sp + npush <= limit + 1) {
                     const uint32_t first = (uint32_t)__builtin_ctz(hs);
                     node = __builtin_amdgcn_readlane(vid, first);
                     mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, first) << 32 |
@@ -644,7 +648,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     uint32_t bl = 0;
     bool phit = false;
     if (PW::WIDE)     // whole wave, before any divergence
-        phit = traverse_packet4<COUNT, PW::GUARD>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c,
+        phit = traverse_packet4<COUNT, PW::GUARD, PW::GUARD || LIM>(a.inner, a.leaf, a.T, o, d, inv, valid, lim4, best, bl, c,
                                             s_pst + w * PST);
     else if (PW::PACKET)
         phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, lim, best, bl, c,
