@@ -445,7 +445,7 @@ __device__ __forceinline__ bool crossing(uint4 topo_k, uint32_t k) {
 // the largest lo and smallest hi byte whose decoded corners (qdecode, the traversal's own
 // arithmetic) still contain it.  false: no finite frame (the node keeps the exact record
 // pair).  Division-free: s and 1/s are built from exponent bits (both normal: s is in
-// [2^-120, 2^116] for |corners| <= 1e37), so (x - o) * (1/s) is exactly (x - o) / s.
+// [2^-120, 2^94] for |corners| <= 2^100), so (x - o) * (1/s) is exactly (x - o) / s.
 // PMC: the first form (correctly rounded divisions, frexpf/ldexpf) ran ~3,500 VALU per
 // node and made the QNode pass VALU-bound (0.90 ms at 10M nodes).
 __device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
@@ -457,7 +457,9 @@ __device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float 
         m = fmaxf(m, hi[c]);
     }
     const float ext = m - o;
-    if (!(fabsf(o) <= 1e37f && fabsf(m) <= 1e37f && ext <= 1e37f)) return false;   // also NaN
+    // corners within 2^100 (also excludes NaN): the bounce walk's slack test (trace.hip
+    // qbox_fast) then stays finite for every ray it takes (|o| <= 2^90, |1/d| <= 2^20)
+    if (!(fabsf(o) <= 0x1p100f && fabsf(m) <= 0x1p100f && ext <= 0x1p100f)) return false;
     // ext in [2^E, 2^(E+1)): 255 * 2^(E-8) < ext, so the smallest valid step is >= 2^(E-8)
     int e = -120;
     if (ext > 0.f) {

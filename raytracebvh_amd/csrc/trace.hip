@@ -808,7 +808,54 @@ __device__ __forceinline__ float bf16_up(uint16_t h) { return __uint_as_float((u
 constexpr int SB = 16;   // 16 x 4 B x 256 lanes = 16 KB per block
 constexpr int SW = 12;   // 12 x 6 B x 256 lanes = 18 KB per block (8 blocks per CU)
 
-template <bool COUNT, int MODE, bool LIM>
+// ---- the slack test of a quantized node --------------------------------------------------
+// The exact form (RTBVH_QBOX below) decodes each corner, org + q * scl, and runs the reference
+// slab test on it: 6 decodes + 12 slab operations per box.  Here the slab is evaluated in the
+// node's grid, t(q) = q * b + a with b = scl * inv (exact: a power of two times inv) and
+// a = (org - o) * inv, shared by the node's four boxes; and the ray's sign picks each axis's
+// near and far corner word once per node, so a box costs 6 cvt + 6 fma + max3 + min3.
+// Conservative against the reference test on the EXACT box: for every corner x the box
+// contains and its decoded corner D (D <= x on the near side), the reference's
+// RN(RN(x - o) * inv) and t(q) both lie within 8u * M * |inv| of (org + q scl - o) * inv
+// (u = 2^-24, M = |org| + |o| + 256 scl: the roundings of the decode, the subtraction, the
+// products and the fma), so the near distances are taken E = 2^-20 * M * |inv| (16u) low and
+// the far ones E high.  Every box the exact test hits is hit, at an entry distance <= the
+// exact one: the walk reaches every leaf the exact walk reaches and prunes only what it would.
+// Finite for |o| <= 2^90, |inv| <= 2^20 (qnode_fast_ray) and corners within 2^100 (a QNode
+// with larger ones keeps the exact record pair, build.hip quantize_axis); other rays take the
+// exact decode.
+__device__ __forceinline__ bool qnode_fast_ray(f3 o, f3 inv) {
+    const float mi = fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
+    const float mo = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    return mi <= 0x1p20f && mo <= 0x1p90f;   // NaN: false
+}
+struct QAxis { uint32_t nw, fw; float b, an, af; };
+__device__ __forceinline__ QAxis qaxis(float org, float scl, uint32_t lw, uint32_t hw, float o, float inv) {
+    QAxis r;
+    const bool neg = inv < 0.f;
+    r.nw = neg ? hw : lw;
+    r.fw = neg ? lw : hw;
+    const float m = fmaf(scl, 256.f, fabsf(org) + fabsf(o));
+    const float e = m * fabsf(inv);
+    const float a = (org - o) * inv;
+    r.an = fmaf(e, -0x1p-20f, a);
+    r.af = fmaf(e, 0x1p-20f, a);
+    r.b = scl * inv;
+    return r;
+}
+__device__ __forceinline__ float qt(uint32_t w, int c, float b, float a) {
+    return fmaf((float)((w >> (8 * c)) & 255u), b, a);
+}
+__device__ __forceinline__ bool qbox_fast(const QAxis& x, const QAxis& y, const QAxis& z, int c, bool hit, float best,
+                                          float& tmin) {
+    const float mn = fmaxf(fmaxf(qt(x.nw, c, x.b, x.an), qt(y.nw, c, y.b, y.an)), qt(z.nw, c, z.b, z.an));
+    const float mx = fminf(fminf(qt(x.fw, c, x.b, x.af), qt(y.fw, c, y.b, y.af)), qt(z.fw, c, z.b, z.af));
+    tmin = mn;
+    return 0 <= mx && mn <= mx && (!hit || mn <= best);
+}
+
+// GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it)
+template <bool COUNT, int MODE, bool LIM, bool GUARD>
 __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
@@ -824,7 +871,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     if (n == 0) return;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0, 0, 0};
-    bool has = false, hit = false;
+    bool has = false, hit = false, qfast = false;
     uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
     int sp = 0;
     float best = 0.f;
@@ -876,6 +923,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                     o = mk(q0.z, q0.w, q1.x);
                     d = mk(q1.y, q1.z, q1.w);
                     inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+                    qfast = WIDE && qnode_fast_ray(o, inv);
                     has = true;
                     hit = false;
                     best = 0.f;
@@ -908,7 +956,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                                : reinterpret_cast<const v4f*>(inner + node);
         v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
         pin(q0); pin(q1); pin(q2); pin(q3);
-        if (--guard == 0) {
+        if (GUARD && --guard == 0) {
             c.overflow++;
             done = true;
         } else if (isleaf) {
@@ -941,14 +989,25 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
                 a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
                 b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
+                if (qfast) {
+                    const QAxis X = qaxis(ox, sx, lx, hx, o.x, inv.x), Y = qaxis(oy, sy, ly, hy, o.y, inv.y),
+                                Z = qaxis(oz, sz, lz, hz, o.z, inv.z);
+                    h0 = qbox_fast(X, Y, Z, 0, hit, best, t0);
+                    h1 = qbox_fast(X, Y, Z, 1, hit, best, t1);
+                    h2 = qbox_fast(X, Y, Z, 2, hit, best, t2);
+                    h3 = qbox_fast(X, Y, Z, 3, hit, best, t3);
+                } else {
 #define RTBVH_QBOX(c, t)                                                                                      \
     ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
             qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), hit, best, t)
-                h0 = RTBVH_QBOX(0, t0);
-                h1 = RTBVH_QBOX(1, t1) & (a3.y != INVALID);
-                h2 = RTBVH_QBOX(2, t2);
-                h3 = RTBVH_QBOX(3, t3) & (b3.y != INVALID);
+                    h0 = RTBVH_QBOX(0, t0);
+                    h1 = RTBVH_QBOX(1, t1);
+                    h2 = RTBVH_QBOX(2, t2);
+                    h3 = RTBVH_QBOX(3, t3);
 #undef RTBVH_QBOX
+                }
+                h1 = h1 & (a3.y != INVALID);
+                h3 = h3 & (b3.y != INVALID);
             } else {
                 // a node without a finite grid: its exact record pair (node = its slot; the
                 // pair of its children's records is at 2 * own, own = word 14 of its record)
@@ -1033,7 +1092,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
         if (done) {
             hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
             has = false;
-            if (COUNT) {   // walk length census (stats trav_max_steps / trav_steps_log2)
+            if (COUNT && GUARD) {   // walk length census (stats trav_max_steps / trav_steps_log2)
                 const uint32_t steps = 2 * T + 2 - guard;
                 atomicAdd(&counters[32 + (31 - __clz(steps | 1u))], 1ull);
                 atomicMax(&counters[13], (unsigned long long)steps);
@@ -1201,12 +1260,14 @@ template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           float2* hitrec, uint32_t* next, uint32_t blocks, hipStream_t s) {
     const int lim = MODE == 2 ? a.stack_limit4 : a.stack_limit;
-    if (a.limited)
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, true>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf,
-                           a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim);
-    else
-        hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, false>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode,
-                           a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim);
+#define RTBVH_BT(L, G)                                                                                              \
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)
+    // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
+    const bool guard = COUNT || !a.acyclic;
+    if (a.limited) { if (guard) RTBVH_BT(true, true); else RTBVH_BT(true, false); }
+    else { if (guard) RTBVH_BT(false, true); else RTBVH_BT(false, false); }
+#undef RTBVH_BT
 }
 
 }  // namespace

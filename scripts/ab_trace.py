@@ -65,6 +65,14 @@ def main():
                 ndiff = int((fb != ref).any(axis=-1).sum())
                 sha = hashlib.sha1(fb.tobytes()).hexdigest()[:16]   # compare across RTBVH_LIB builds
                 print(json.dumps({"variant": v, "pixels_differing_from_first": ndiff, "frame_sha1": sha}), flush=True)
+    if os.environ.get("AB_COUNTS"):   # visit counts of each variant (one counting trace)
+        for v, srt in variants:
+            ctx.set_flags(srt | rt.FLAG_COUNT_VISITS)
+            ctx.trace(W, H, 1)
+            st = ctx.stats()
+            print(json.dumps({"variant": v, "packet_steps": list(st["packet_steps"]),
+                              "internal_visits": list(st["internal_visits"]), "leaf_visits": list(st["leaf_visits"]),
+                              "trav_wave_steps": st["trav_wave_steps"]}))
     for (v, srt), xs in res.items():
         a = np.array(xs)
         print(json.dumps({"variant": v, "primary_ms_med": float(np.median(a[:, 0])),
