@@ -283,7 +283,7 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
 __device__ __forceinline__ float ray_triangle_flat(f3 o, f3 d, f3 p0, f3 e1, f3 e2, bool in) {
     const f3 tmp = cross(d, e2);
     const float dx = dot(e1, tmp);
-    const float idx = 1.f / dx;
+    const float idx = recip(dx);
     const f3 rt = sub(o, p0);
     const float u = dot(rt, tmp) * idx;
     const f3 q = cross(rt, e1);
