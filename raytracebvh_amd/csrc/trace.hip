@@ -304,6 +304,13 @@ __device__ __forceinline__ float ray_triangle_flat(f3 o, f3 d, f3 p0, f3 e1, f3 
     return in ? r : -1.f;
 }
 
+// (t, leaf) of the best hit as one u64 key, t's bits above: t > EPSILON > 0, so the u64 order is
+// the (t, leaf) order; before any hit (+inf, ~0), which every hit beats.  The entry distance of a
+// box is then compared with the key's t alone: with no hit it is +inf, and a box whose entry is
+// not <= +inf (NaN) fails the slab test's own mn <= mx too, as the reference's !hit || ... does.
+constexpr uint64_t NO_HIT = 0x7F800000FFFFFFFFull;
+__device__ __forceinline__ float key_t(uint64_t key) { return __uint_as_float((uint32_t)(key >> 32)); }
+
 // v_writelane_b32: lane K of v := the wave-uniform s (a VALU op, no scalar work)
 template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t s) {
     asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "i"(K));
@@ -355,9 +362,6 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
     if (mask == 0) return false;
     const float qnan = __builtin_nanf("");
     const f2v oxy = valid ? f2v{o.x, o.y} : f2v{qnan, qnan};
-    // (t, leaf) of the best hit as one u64 key, t's bits above: t > EPSILON > 0, so the u64
-    // order is the (t, leaf) order; before any hit (+inf, ~0), which every hit beats
-    constexpr uint64_t NO_HIT = 0x7F800000FFFFFFFFull;
     uint64_t key = NO_HIT;
     uint32_t vid = 0, vlo = 0, vhi = 0;
     // entry 0 is a sentinel (node INVALID): popping it ends the walk, so a pop needs no
@@ -873,6 +877,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
     Counts c = {0, 0, 0, 0, 0};
     bool has = false, hit = false, qfast = false;
     uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
+    uint64_t key = NO_HIT;   // WIDE: the lexicographic (t, leaf) minimum (hit / best / bl of the binary walks)
     int sp = 0;
     float best = 0.f;
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
@@ -928,6 +933,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                     hit = false;
                     best = 0.f;
                     bl = 0;
+                    key = NO_HIT;
                     sp = 0;
                     top = INVALID;
                     node = root_slot(T);
@@ -964,11 +970,18 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             const v4f la = q0, lb = q1;
             const float e2z = q2.x;
             if (COUNT) c.leaf++;
-            const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
-            if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
-                best = t;
-                bl = j;
-                hit = true;
+            if (WIDE) {   // branch-free test (the same accept predicate), u64 key minimum
+                const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
+                                                   mk(lb.z, lb.w, e2z), true);
+                const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
+                key = k < key ? k : key;
+            } else {
+                const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
+                if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
+                    best = t;
+                    bl = j;
+                    hit = true;
+                }
             }
             if (WIDE) {
                 node = INVALID;   // pop below
@@ -983,6 +996,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             uint4 a3, b3;
             float t0, t1, t2, t3;
             bool h0, h1, h2, h3;
+            const float kb = key_t(key);
             if (q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
                 const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w, sy = q1.x, sz = q1.y;
                 const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
@@ -992,14 +1006,14 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 if (qfast) {
                     const QAxis X = qaxis(ox, sx, lx, hx, o.x, inv.x), Y = qaxis(oy, sy, ly, hy, o.y, inv.y),
                                 Z = qaxis(oz, sz, lz, hz, o.z, inv.z);
-                    h0 = qbox_fast(X, Y, Z, 0, hit, best, t0);
-                    h1 = qbox_fast(X, Y, Z, 1, hit, best, t1);
-                    h2 = qbox_fast(X, Y, Z, 2, hit, best, t2);
-                    h3 = qbox_fast(X, Y, Z, 3, hit, best, t3);
+                    h0 = qbox_fast(X, Y, Z, 0, true, kb, t0);
+                    h1 = qbox_fast(X, Y, Z, 1, true, kb, t1);
+                    h2 = qbox_fast(X, Y, Z, 2, true, kb, t2);
+                    h3 = qbox_fast(X, Y, Z, 3, true, kb, t3);
                 } else {
 #define RTBVH_QBOX(c, t)                                                                                      \
     ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
-            qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), hit, best, t)
+            qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), true, kb, t)
                     h0 = RTBVH_QBOX(0, t0);
                     h1 = RTBVH_QBOX(1, t1);
                     h2 = RTBVH_QBOX(2, t2);
@@ -1023,10 +1037,10 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 if (a3.y != INVALID && !(a3.y & LEAF_BIT)) a3.y = 2 * ol + 1;
                 if (!(b3.x & LEAF_BIT)) b3.x = 2 * orr;
                 if (b3.y != INVALID && !(b3.y & LEAF_BIT)) b3.y = 2 * orr + 1;
-                h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, t0);
-                h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, t1) & (a3.y != INVALID);
-                h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, hit, best, t2);
-                h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, hit, best, t3) & (b3.y != INVALID);
+                h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, true, kb, t0);
+                h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, true, kb, t1) & (a3.y != INVALID);
+                h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, true, kb, t2);
+                h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, true, kb, t3) & (b3.y != INVALID);
             }
             const float INF = __builtin_inff();
             float k0 = h0 ? t0 : INF, k1 = h1 ? t1 : INF, k2 = h2 ? t2 : INF, k3 = h3 ? t3 : INF;
@@ -1082,7 +1096,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
                 uint2 e;
                 if (sp < SW) e = make_uint2(s_wid[sp][tid], __float_as_uint(bf16_up(s_wt[sp][tid])));
                 else e = wstack[sp - SW];
-                if (!hit || __uint_as_float(e.y) <= best) {
+                if (__uint_as_float(e.y) <= key_t(key)) {
                     node = e.x;
                     break;
                 }
@@ -1090,7 +1104,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restric
             done = node == INVALID;
         }
         if (done) {
-            hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
+            if (WIDE) hitrec[r] = make_float2(key_t(key), __uint_as_float(key != NO_HIT ? (uint32_t)key : INVALID));
+            else hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
             has = false;
             if (COUNT && GUARD) {   // walk length census (stats trav_max_steps / trav_steps_log2)
                 const uint32_t steps = 2 * T + 2 - guard;
