@@ -8,6 +8,13 @@
 
 namespace rtbvh {
 
+// waves per SIMD of the persistent bounce walk (its launch bounds; the full grid is 256 blocks
+// of 4 waves per wave/SIMD over the 1,024 SIMDs)
+#ifndef RTBVH_BOUNCE_WAVES
+#define RTBVH_BOUNCE_WAVES 8
+#endif
+constexpr uint32_t BOUNCE_WAVES = RTBVH_BOUNCE_WAVES;
+
 struct Mat4 { float m[16]; };
 
 // ---- radix sort (sort.hip) --------------------------------------------------

@@ -860,7 +860,7 @@ __device__ __forceinline__ bool qbox_fast(const QAxis& x, const QAxis& y, const 
 
 // GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it)
 template <bool COUNT, int MODE, bool LIM, bool GUARD>
-__global__ __launch_bounds__(BLOCK, 8) void k_bounce_trav(const Inner* __restrict__ inner,
+__global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
                                                           const RayQ* __restrict__ qin,
