@@ -538,9 +538,8 @@ __device__ __forceinline__ float4 sample_texture(const TraceArgs& a, uint32_t k,
 // getHitLoc (:15-19) + getNromalTexCoord (RayTraceHelper.hlsl:12-35) + renderPixel*specular
 // (RayTraceRender.hlsl:16-29, RayTraceLaunch.hlsl:57-59) for the hit triangle only
 // (the reference transforms all three vertices at every leaf it visits).
-__device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_leaf, f3 o, f3 d, float t) {
+__device__ __forceinline__ HitInfo shade_hit_tri(const TraceArgs& a, uint32_t tri, f3 o, f3 d, float t) {
     HitInfo h;
-    const uint32_t tri = __float_as_uint(a.leaf[4 * (size_t)best_leaf + 2].y);
     const float4* P = a.tclip + 3 * (size_t)tri;
     const float4 a0 = P[0], a1 = P[1], a2 = P[2];
     const f3 P0 = mk(a0.x, a0.y, a0.z), P1 = mk(a1.x, a1.y, a1.z), P2 = mk(a2.x, a2.y, a2.z);
@@ -577,6 +576,11 @@ __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_l
     h.alpha = m.alpha;
     h.optical_density = m.optical_density;
     return h;
+}
+
+// the same for sorted leaf best_leaf (its record holds the triangle index)
+__device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_leaf, f3 o, f3 d, float t) {
+    return shade_hit_tri(a, __float_as_uint(a.leaf[4 * (size_t)best_leaf + 2].y), o, d, t);
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -877,6 +881,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     Counts c = {0, 0, 0, 0, 0};
     bool has = false, hit = false, qfast = false;
     uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
+    uint32_t btri = 0;       // triangle of the best hit (leaf record word 9): the hit record's id
     uint64_t key = NO_HIT;   // WIDE: the lexicographic (t, leaf) minimum (hit / best / bl of the binary walks)
     int sp = 0;
     float best = 0.f;
@@ -974,12 +979,14 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                 const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
                                                    mk(lb.z, lb.w, e2z), true);
                 const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
+                btri = k < key ? __float_as_uint(q2.y) : btri;
                 key = k < key ? k : key;
             } else {
                 const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
                 if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
                     best = t;
                     bl = j;
+                    btri = __float_as_uint(q2.y);
                     hit = true;
                 }
             }
@@ -1104,8 +1111,9 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
             done = node == INVALID;
         }
         if (done) {
-            if (WIDE) hitrec[r] = make_float2(key_t(key), __uint_as_float(key != NO_HIT ? (uint32_t)key : INVALID));
-            else hitrec[r] = make_float2(best, __uint_as_float(hit ? bl : INVALID));
+            // (t, triangle) of the hit, INVALID for a miss: the shading reads no leaf record
+            if (WIDE) hitrec[r] = make_float2(key_t(key), __uint_as_float(key != NO_HIT ? btri : INVALID));
+            else hitrec[r] = make_float2(best, __uint_as_float(hit ? btri : INVALID));
             has = false;
             if (COUNT && GUARD) {   // walk length census (stats trav_max_steps / trav_steps_log2)
                 const uint32_t steps = 2 * T + 2 - guard;
@@ -1151,13 +1159,13 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
     if (i < n) {
         e = qin[i];
         const float2 h2 = hitrec[i];
-        const uint32_t bl = __float_as_uint(h2.y);
+        const uint32_t tri = __float_as_uint(h2.y);
         const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
         float4 col = a.color[e.idx];
         float intensity = e.intensity;
-        if (bl != INVALID) {
+        if (tri != INVALID) {
             hits = 1;
-            const HitInfo h = shade_hit(a, bl, o, d, h2.x);
+            const HitInfo h = shade_hit_tri(a, tri, o, d, h2.x);
             tex = h.textured;
             col = make_float4(lerpf(col.x, h.color.x, intensity), lerpf(col.y, h.color.y, intensity),
                               lerpf(col.z, h.color.z, intensity), lerpf(col.w, h.color.w, intensity));
