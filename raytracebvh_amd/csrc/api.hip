@@ -410,7 +410,10 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     // persistent grid of the bounce walk: 2048 blocks (8 waves/SIMD), 1024 for a shard of
     // < 4M pixels -- with frames in flight the next frame's primary blocks then share the CUs
     // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame)
-    const uint32_t tblocks = P < (1u << 22) ? 1024 : 256 * BOUNCE_WAVES;
+#ifndef RTBVH_BOUNCE_GRID
+#define RTBVH_BOUNCE_GRID (256 * BOUNCE_WAVES)
+#endif
+    const uint32_t tblocks = P < (1u << 22) ? 1024 : RTBVH_BOUNCE_GRID;
     if (records) {
         if (c->cap_rec < P) {
             HIPC(c, dalloc(c->d_refl_rec, 14 * (size_t)P));
