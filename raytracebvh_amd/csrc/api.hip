@@ -160,7 +160,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_kb, n));
     HIPC(c, dalloc(c->d_vb, n));
     HIPC(c, dalloc(c->d_sort_scratch, sort_scratch_words(T)));
-    HIPC(c, dalloc(c->d_tclip, 3 * n));
+    HIPC(c, dalloc(c->d_tclip, TCS * n));
     HIPC(c, dalloc(c->d_leaf, 4 * n));
     HIPC(c, dalloc(c->d_inner, ni));
     HIPC(c, dalloc(c->d_topo, ni));

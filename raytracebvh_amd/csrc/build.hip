@@ -150,29 +150,31 @@ __device__ __forceinline__ uint32_t morton_code(const BuildArgs& a, uint32_t t, 
 __device__ __forceinline__ uint32_t morton_tri(const BuildArgs& a, uint32_t t) {
     float4 clip[3];
     const uint32_t code = morton_code(a, t, clip);
-    float4* o = a.tclip + 3 * (size_t)t;
+    float4* o = a.tclip + TCS * (size_t)t;
     o[0] = clip[0]; o[1] = clip[1]; o[2] = clip[2];
+    if (TCS == 4) o[3] = make_float4(0.f, 0.f, 0.f, 0.f);
     return code;
 }
 // One thread per triangle; the 48-B clip-space triangles of a wave (3 KB contiguous) are staged
 // in LDS and stored 16 B per lane (scripts/write_roofline.hip: 4.1 TB/s against 2.5-2.9 for a
 // whole record per lane).
 __global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
-    __shared__ float4 s_clip[BLOCK / 64][3 * 64];
+    __shared__ float4 s_clip[BLOCK / 64][TCS * 64];
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     if (t < a.T) {
         float4 clip[3];
         morton_code(a, t, clip);
 #pragma unroll
-        for (int k = 0; k < 3; k++) s_clip[w][3 * lane + k] = clip[k];
+        for (int k = 0; k < 3; k++) s_clip[w][TCS * lane + k] = clip[k];
+        if (TCS == 4) s_clip[w][TCS * lane + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
     const uint32_t t0 = t - lane;   // the wave's first triangle
     const uint32_t n = a.T > t0 ? min(64u, a.T - t0) : 0u;
-    float4* dst = a.tclip + 3 * (size_t)t0;
+    float4* dst = a.tclip + TCS * (size_t)t0;
 #pragma unroll
-    for (uint32_t k = 0; k < 3; k++)
-        if (64 * k + lane < 3 * n) st_out<1>(dst + 64 * k + lane, s_clip[w][64 * k + lane]);
+    for (uint32_t k = 0; k < TCS; k++)
+        if (64 * k + lane < TCS * n) st_out<1>(dst + 64 * k + lane, s_clip[w][64 * k + lane]);
 }
 
 // ---- Karras 2012 (BVHConstructP1.hlsl:61-165) --------------------------------
@@ -244,7 +246,7 @@ __device__ void karras_node(const C& c, uint32_t n, uint32_t i, uint4* __restric
 // the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
 __device__ __forceinline__ void leaf_record_words(const BuildArgs& a, uint32_t i, f3& lo, f3& hi, float4 (&r)[4]) {
     const uint32_t t = a.sorted_vals[i];
-    const float4* src = a.tclip + 3 * (size_t)t;
+    const float4* src = a.tclip + TCS * (size_t)t;
     const float4 s0 = src[0], s1 = src[1], s2 = src[2];
     const f3 v0 = mk(s0.x, s0.y, s0.z), v1 = mk(s1.x, s1.y, s1.z), v2 = mk(s2.x, s2.y, s2.z);
     const f3 e1 = sub(v1, v0), e2 = sub(v2, v0);

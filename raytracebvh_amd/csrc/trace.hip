@@ -540,7 +540,7 @@ __device__ __forceinline__ float4 sample_texture(const TraceArgs& a, uint32_t k,
 // (the reference transforms all three vertices at every leaf it visits).
 __device__ __forceinline__ HitInfo shade_hit_tri(const TraceArgs& a, uint32_t tri, f3 o, f3 d, float t) {
     HitInfo h;
-    const float4* P = a.tclip + 3 * (size_t)tri;
+    const float4* P = a.tclip + TCS * (size_t)tri;
     const float4 a0 = P[0], a1 = P[1], a2 = P[2];
     const f3 P0 = mk(a0.x, a0.y, a0.z), P1 = mk(a1.x, a1.y, a1.z), P2 = mk(a2.x, a2.y, a2.z);
     f3 n[3];
