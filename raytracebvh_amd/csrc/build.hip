@@ -241,6 +241,13 @@ __device__ void karras_node(const C& c, uint32_t n, uint32_t i, uint4* __restric
     if (right_leaf) pleaf[r] = (i << 1) | 1u; else pint[r] = (i << 1) | 1u;
 }
 
+// the leaf record's word 9: the triangle index, bit 31 set when the leaf box needs the general slab
+// test for axis-parallel primary rays (the same rule as general_box below; the primary walk
+// re-tests a leaf's box before its triangle, trace.hip traverse_packet4)
+__device__ __forceinline__ uint32_t leaf_tri_word(uint32_t t, f3 lo, f3 hi) {
+    const bool fast = lo.x < hi.x && lo.y < hi.y && lo.z <= hi.z && 0.f <= hi.z && hi.z < INFINITY;
+    return t | (fast ? 0u : LEAF_BIT);
+}
 // leaf record of sorted position i: gather the clip-space triangle once, store
 // (v0, e1, e2) for the triangle test (the reference's edge1/edge2, :43-44) and
 // the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
@@ -256,7 +263,7 @@ __device__ __forceinline__ void leaf_record_words(const BuildArgs& a, uint32_t i
     hi = vmax(hi, v2);
     r[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
     r[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
-    r[2] = make_float4(e2.z, __uint_as_float(t), lo.x, lo.y);
+    r[2] = make_float4(e2.z, __uint_as_float(leaf_tri_word(t, lo, hi)), lo.x, lo.y);
     r[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
 }
 __device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i, f3& lo, f3& hi) {
@@ -959,7 +966,7 @@ __global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restri
         o.child_l = INVALID;
         o.child_r = INVALID;
         o.code = a.sorted_keys[r];
-        o.index = a.leaf ? 3u * __float_as_uint(a.leaf[4 * (size_t)r + 2].y) : 0u;
+        o.index = a.leaf ? 3u * (__float_as_uint(a.leaf[4 * (size_t)r + 2].y) & ~LEAF_BIT) : 0u;
     } else {
         const uint32_t k = r - T;
         e = a.pint[k];

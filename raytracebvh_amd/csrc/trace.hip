@@ -351,10 +351,20 @@ template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t
 // stack limit (CHECK false) no stack check either: a clz64 tree has <= 64 internal levels (each
 // child's common-prefix length exceeds its parent's, 0..63), a step descends two levels and
 // pushes <= 3 entries, so the stack holds <= 3 * 32 + 1 < STACK4 + 1 entries.
+// No lane masks on the stack: a wave needs the lanes that reach a node only at a leaf (which
+// lanes test its triangle), and those are the lanes whose ray passes the leaf's own box with the
+// current bound -- its record holds the box (words 10..15), so the leaf step tests it again, with
+// the fast or the general form as the parent step did.  Every lane the parent step let through
+// passes it unless its bound has since fallen below the box's entry, and such a lane cannot improve
+// its (t, leaf) minimum there.  Internal steps never needed the masks (a child's box lies inside its
+// parent's, and the slab test is monotone in the box), so a stack entry is a node id alone: one
+// v_writelane per child instead of three, one word per push and pop.  The visit counters (COUNT)
+// still keep each entry's lanes, beside the same walk.
 template <bool COUNT, bool GUARD, bool CHECK>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
                                                  uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
                                                  uint32_t& best_leaf, Counts& c, uint32_t* s_st /* [3*(STACK4+1)] */) {
+    constexpr int EW = COUNT ? 3 : 1;   // words per stack entry: the node, and its lanes for the counters
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t mask = __ballot(valid);
     best = 0.f;
@@ -376,8 +386,20 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             const uint32_t j = node & ~LEAF_BIT;
             const v16f q = sload16(leaf + 4 * (size_t)j);
             if (COUNT && lane == 0) c.wleaf++;
-            const bool in = (mask >> lane) & 1u;
-            if (COUNT) c.leaf += in;
+            // the lanes that need this leaf: its own box {min q[10..12], max q[13..15]}, tested as the
+            // parent step tested it (rtbvh_device.h word 15: the fast form for a box that allows it)
+            const float lx = q[10], ly = q[11], lz = q[12], hx = q[13], hy = q[14], hz = q[15];
+            const float bound = __uint_as_float((uint32_t)(key >> 32));
+            bool in;
+            if (!(__float_as_uint(q[9]) & LEAF_BIT)) {   // the box allows the fast form (build.hip leaf_tri_word)
+                const f2v d0 = oxy - f2v{lx, ly}, d1 = f2v{hx, hy} - oxy;
+                in = fminf(fminf(d0.x, d0.y), fminf(d1.x, d1.y)) > 0.f && lz <= bound;
+            } else {
+                const bool hit = key != NO_HIT;
+                float tt;
+                in = valid && ray_box_xy(o, inv, f2v{lx, ly}, f2v{hx, hy}, lz, hz, hit, hit ? bound : 0.f, tt);
+            }
+            if (COUNT) c.leaf += (mask >> lane) & 1u;
             const float t =
                 ray_triangle_flat(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]), in);
             const uint64_t k = t == -1.f ? ~0ull : (uint64_t)__float_as_uint(t) << 32 | j;
@@ -408,7 +430,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
                 const float bst = hit ? bound : 0.f;
                 bool h0 = false, h1 = false, h2 = false, h3 = false;
                 float t0, t1, t2, t3;
-                if ((mask >> lane) & 1u) {
+                if (valid) {   // a lane the parent let not through fails these too (monotone)
                     h0 = ray_box_xy(o, inv, A.s01, A.s23, A[8], A[9], hit, bst, t0);
                     h1 = ray_box_xy(o, inv, A.s45, A.s67, A[10], A[11], hit, bst, t1) & (id1 != INVALID);
                     h2 = ray_box_xy(o, inv, B.s01, B.s23, B[8], B[9], hit, bst, t2);
@@ -420,30 +442,36 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             writelane<1>(vid, id1);
             writelane<2>(vid, id2);
             writelane<3>(vid, id3);
-            writelane<0>(vlo, (uint32_t)m0);
-            writelane<1>(vlo, (uint32_t)m1);
-            writelane<2>(vlo, (uint32_t)m2);
-            writelane<3>(vlo, (uint32_t)m3);
-            writelane<0>(vhi, (uint32_t)(m0 >> 32));
-            writelane<1>(vhi, (uint32_t)(m1 >> 32));
-            writelane<2>(vhi, (uint32_t)(m2 >> 32));
-            writelane<3>(vhi, (uint32_t)(m3 >> 32));
+            if (COUNT) {
+                writelane<0>(vlo, (uint32_t)m0);
+                writelane<1>(vlo, (uint32_t)m1);
+                writelane<2>(vlo, (uint32_t)m2);
+                writelane<3>(vlo, (uint32_t)m3);
+                writelane<0>(vhi, (uint32_t)(m0 >> 32));
+                writelane<1>(vhi, (uint32_t)(m1 >> 32));
+                writelane<2>(vhi, (uint32_t)(m2 >> 32));
+                writelane<3>(vhi, (uint32_t)(m3 >> 32));
+            }
             // (an absent second child -- INVALID id, a leaf's pseudo-record -- has a NaN min.z and
             // hits no lane in the fast test; the general test checks its id)
-            const uint32_t hs = (uint32_t)__builtin_amdgcn_ballot_w64((vlo | vhi) != 0);   // lanes >= 4 stay 0
+            const uint32_t hs = (uint32_t)(m0 != 0) | (uint32_t)(m1 != 0) << 1 | (uint32_t)(m2 != 0) << 2 |
+                                (uint32_t)(m3 != 0) << 3;
             if (hs != 0) {
                 const uint32_t rest = hs & (hs - 1);
                 const int npush = __builtin_popcount(rest);
                 if (!CHECK || sp + npush <= limit + 1) {
                     const uint32_t first = (uint32_t)__builtin_ctz(hs);
                     node = __builtin_amdgcn_readlane(vid, first);
-                    mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, first) << 32 |
-                           (uint32_t)__builtin_amdgcn_readlane(vlo, first);
+                    if (COUNT)
+                        mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, first) << 32 |
+                               (uint32_t)__builtin_amdgcn_readlane(vlo, first);
                     if (((uint64_t)rest >> lane) & 1u) {   // the later a child, the deeper its entry
                         const int pos = sp + __builtin_popcount(rest >> (lane + 1));
-                        s_st[3 * pos] = vid;
-                        s_st[3 * pos + 1] = vlo;
-                        s_st[3 * pos + 2] = vhi;
+                        s_st[EW * pos] = vid;
+                        if (COUNT) {
+                            s_st[EW * pos + 1] = vlo;
+                            s_st[EW * pos + 2] = vhi;
+                        }
                     }
                     sp += npush;
                     continue;
@@ -452,10 +480,12 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             }
         }
         --sp;
-        node = __builtin_amdgcn_readfirstlane(s_st[3 * sp]);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 1]);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[3 * sp + 2]);
-        mask = ((uint64_t)hi << 32) | lo;
+        node = __builtin_amdgcn_readfirstlane(s_st[EW * sp]);
+        if (COUNT) {
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(s_st[EW * sp + 1]);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(s_st[EW * sp + 2]);
+            mask = ((uint64_t)hi << 32) | lo;
+        }
     } while (node != INVALID && (!GUARD || --guard != 0));
     if (GUARD && guard == 0) c.overflow++;
     const bool hit = key != NO_HIT;
@@ -580,7 +610,7 @@ __device__ __forceinline__ HitInfo shade_hit_tri(const TraceArgs& a, uint32_t tr
 
 // the same for sorted leaf best_leaf (its record holds the triangle index)
 __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_leaf, f3 o, f3 d, float t) {
-    return shade_hit_tri(a, __float_as_uint(a.leaf[4 * (size_t)best_leaf + 2].y), o, d, t);
+    return shade_hit_tri(a, __float_as_uint(a.leaf[4 * (size_t)best_leaf + 2].y) & ~LEAF_BIT, o, d, t);
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -979,14 +1009,14 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                 const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
                                                    mk(lb.z, lb.w, e2z), true);
                 const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
-                btri = k < key ? __float_as_uint(q2.y) : btri;
+                btri = k < key ? __float_as_uint(q2.y) & ~LEAF_BIT : btri;
                 key = k < key ? k : key;
             } else {
                 const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
                 if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
                     best = t;
                     bl = j;
-                    btri = __float_as_uint(q2.y);
+                    btri = __float_as_uint(q2.y) & ~LEAF_BIT;
                     hit = true;
                 }
             }
