@@ -358,7 +358,8 @@ template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t
 // passes it unless its bound has since fallen below the box's entry, and such a lane cannot improve
 // its (t, leaf) minimum there.  Internal steps never needed the masks (a child's box lies inside its
 // parent's, and the slab test is monotone in the box), so a stack entry is a node id alone: one
-// v_writelane per child instead of three, one word per push and pop.  The visit counters (COUNT)
+// v_writelane per child for its id and one for its any-lane bit instead of three, one word per push
+// and pop.  The visit counters (COUNT)
 // still keep each entry's lanes, beside the same walk.
 template <bool COUNT, bool GUARD, bool CHECK>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
@@ -454,8 +455,14 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             }
             // (an absent second child -- INVALID id, a leaf's pseudo-record -- has a NaN min.z and
             // hits no lane in the fast test; the general test checks its id)
-            const uint32_t hs = (uint32_t)(m0 != 0) | (uint32_t)(m1 != 0) << 1 | (uint32_t)(m2 != 0) << 2 |
-                                (uint32_t)(m3 != 0) << 3;
+            // which children any lane hits: the OR of each mask's halves in lanes 0..3, one ballot
+            // (the same from four 64-bit compares on the SALU: +45% SALU, primary +2%)
+            uint32_t vor = 0;
+            writelane<0>(vor, (uint32_t)m0 | (uint32_t)(m0 >> 32));
+            writelane<1>(vor, (uint32_t)m1 | (uint32_t)(m1 >> 32));
+            writelane<2>(vor, (uint32_t)m2 | (uint32_t)(m2 >> 32));
+            writelane<3>(vor, (uint32_t)m3 | (uint32_t)(m3 >> 32));
+            const uint32_t hs = (uint32_t)__builtin_amdgcn_ballot_w64(vor != 0);   // lanes >= 4 stay 0
             if (hs != 0) {
                 const uint32_t rest = hs & (hs - 1);
                 const int npush = __builtin_popcount(rest);
