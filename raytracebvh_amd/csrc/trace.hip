@@ -359,8 +359,7 @@ template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t
 // its (t, leaf) minimum there.  Internal steps never needed the masks (a child's box lies inside its
 // parent's, and the slab test is monotone in the box), so a stack entry is a node id alone: one
 // v_writelane per child for its id and one for its any-lane bit instead of three, one word per push
-// and pop.  The visit counters (COUNT)
-// still keep each entry's lanes, beside the same walk.
+// and pop.  The visit counters (COUNT) still keep each entry's lanes, beside the same walk.
 template <bool COUNT, bool GUARD, bool CHECK>
 __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner4, const float4* __restrict__ leaf,
                                                  uint32_t T, f3 o, f3 d, f3 inv, bool valid, int limit, float& best,
