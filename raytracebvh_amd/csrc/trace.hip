@@ -945,6 +945,70 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
         }
         ++sp;
     };
+    // WIDE: the QNode at `node` (words q0..q3): its four entries, hit ones first by entry distance
+    // (k: entry distance, i: id; a missing child has INVALID and +inf)
+    auto qchildren = [&](v4f q0, v4f q1, v4f q2, v4f q3, float& k0, float& k1, float& k2, float& k3, uint32_t& i0,
+                         uint32_t& i1, uint32_t& i2, uint32_t& i3) {
+        // the four grandchildren: ids (a3.x, a3.y, b3.x, b3.y), entry distances t0..t3
+        uint4 a3, b3;
+        float t0, t1, t2, t3;
+        bool h0, h1, h2, h3;
+        const float kb = key_t(key);
+        if (q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
+            const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w, sy = q1.x, sz = q1.y;
+            const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
+            const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
+            a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
+            b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
+            if (qfast) {
+                const QAxis X = qaxis(ox, sx, lx, hx, o.x, inv.x), Y = qaxis(oy, sy, ly, hy, o.y, inv.y),
+                            Z = qaxis(oz, sz, lz, hz, o.z, inv.z);
+                h0 = qbox_fast(X, Y, Z, 0, true, kb, t0);
+                h1 = qbox_fast(X, Y, Z, 1, true, kb, t1);
+                h2 = qbox_fast(X, Y, Z, 2, true, kb, t2);
+                h3 = qbox_fast(X, Y, Z, 3, true, kb, t3);
+            } else {
+    #define RTBVH_QBOX(c, t)                                                                                      \
+ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
+        qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), true, kb, t)
+                h0 = RTBVH_QBOX(0, t0);
+                h1 = RTBVH_QBOX(1, t1);
+                h2 = RTBVH_QBOX(2, t2);
+                h3 = RTBVH_QBOX(3, t3);
+    #undef RTBVH_QBOX
+            }
+            h1 = h1 & (a3.y != INVALID);
+            h3 = h3 & (b3.y != INVALID);
+        } else {
+            // a node without a finite grid: its exact record pair (node = its slot; the
+            // pair of its children's records is at 2 * own, own = word 14 of its record)
+            const uint32_t own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
+            const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
+            q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
+            const v4f q4 = pr[4], q5 = pr[5], q6 = pr[6], q7 = pr[7];
+            a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
+            b3 = make_uint4(__float_as_uint(q7.x), __float_as_uint(q7.y), 0u, 0u);
+            // grandchild ids -> slots (2 * parent + side; parent = word 14)
+            const uint32_t ol = __float_as_uint(q3.z), orr = __float_as_uint(q7.z);
+            if (!(a3.x & LEAF_BIT)) a3.x = 2 * ol;
+            if (a3.y != INVALID && !(a3.y & LEAF_BIT)) a3.y = 2 * ol + 1;
+            if (!(b3.x & LEAF_BIT)) b3.x = 2 * orr;
+            if (b3.y != INVALID && !(b3.y & LEAF_BIT)) b3.y = 2 * orr + 1;
+            h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, true, kb, t0);
+            h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, true, kb, t1) & (a3.y != INVALID);
+            h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, true, kb, t2);
+            h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, true, kb, t3) & (b3.y != INVALID);
+        }
+        const float INF = __builtin_inff();
+        k0 = h0 ? t0 : INF; k1 = h1 ? t1 : INF; k2 = h2 ? t2 : INF; k3 = h3 ? t3 : INF;
+        i0 = h0 ? a3.x : INVALID; i1 = h1 ? a3.y : INVALID; i2 = h2 ? b3.x : INVALID; i3 = h3 ? b3.y : INVALID;
+        // 4-element sorting network on the entry distance (missing children last)
+        sort2(k0, i0, k1, i1);
+        sort2(k2, i2, k3, i3);
+        sort2(k0, i0, k2, i2);
+        sort2(k1, i1, k3, i3);
+        sort2(k1, i1, k2, i2);
+    };
     bool drained = false;
     uint32_t kseg = 0;   // segments claimed from so far (wave-uniform)
     unsigned long long wsteps = 0, mixed = 0, active_lanes = 0;
@@ -994,157 +1058,118 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
         }
         if (!has) continue;
         bool done = false;
-        // one fetch for every active lane, leaf or internal, before the branch: a wave
-        // holding both kinds would otherwise wait for two dependent round trips
-        // (leaf records, child-pair records and quantized nodes are all 64-B aligned records)
-        const bool isleaf = (node & LEAF_BIT) != 0;
-        const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(node & ~LEAF_BIT))
-                        : WIDE ? reinterpret_cast<const v4f*>(qn + node)
-                               : reinterpret_cast<const v4f*>(inner + node);
-        v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
-        pin(q0); pin(q1); pin(q2); pin(q3);
-        if (GUARD && --guard == 0) {
-            c.overflow++;
-            done = true;
-        } else if (isleaf) {
-            const uint32_t j = node & ~LEAF_BIT;
-            const v4f la = q0, lb = q1;
-            const float e2z = q2.x;
-            if (COUNT) c.leaf++;
-            if (WIDE) {   // branch-free test (the same accept predicate), u64 key minimum
-                const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
-                                                   mk(lb.z, lb.w, e2z), true);
-                const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
-                btri = k < key ? __float_as_uint(q2.y) & ~LEAF_BIT : btri;
-                key = k < key ? k : key;
+        if (WIDE) {
+            // A step: the QNode of an internal `node`, then one leaf test -- the nearest child when it
+            // is a leaf (the next child is visited), or the leaf the step began at -- so a leaf found
+            // by the node test costs no step of its own, and the leaf test is one block of code.
+            uint32_t L = INVALID;
+            if (GUARD && --guard == 0) {
+                c.overflow++;
+                done = true;
             } else {
-                const float t = ray_triangle(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y), mk(lb.z, lb.w, e2z));
+                if (node & LEAF_BIT) {
+                    L = node;
+                    node = INVALID;
+                } else {
+                    const v4f* rr = reinterpret_cast<const v4f*>(qn + node);
+                    v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
+                    pin(q0); pin(q1); pin(q2); pin(q3);
+                    if (COUNT) c.internal++;
+                    float k0, k1, k2, k3;
+                    uint32_t i0, i1, i2, i3;
+                    qchildren(q0, q1, q2, q3, k0, k1, k2, k3, i0, i1, i2, i3);
+                    const bool lf0 = i0 != INVALID && (i0 & LEAF_BIT);
+                    L = lf0 ? i0 : INVALID;
+                    node = lf0 ? i1 : i0;   // INVALID when no child is left -> pop below
+                    if (sp + 3 > limit) {
+                        c.overflow++;
+                        done = true;
+                    } else {   // push the others farthest first
+                        if (i3 != INVALID) wpush(i3, k3);
+                        if (i2 != INVALID) wpush(i2, k2);
+                        if (!lf0 && i1 != INVALID) wpush(i1, k1);
+                    }
+                }
+                if (L != INVALID) {   // branch-free test (the same accept predicate), u64 key minimum
+                    const uint32_t j = L & ~LEAF_BIT;
+                    const v4f* lr = reinterpret_cast<const v4f*>(leaf + 4 * (size_t)j);
+                    v4f la = lr[0], lb = lr[1], lc = lr[2];
+                    pin(la); pin(lb); pin(lc);
+                    if (COUNT) c.leaf++;
+                    const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
+                                                       mk(lb.z, lb.w, lc.x), true);
+                    const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
+                    btri = k < key ? __float_as_uint(lc.y) & ~LEAF_BIT : btri;
+                    key = k < key ? k : key;
+                }
+                if (!done && node == INVALID) {   // pop, dropping entries that cannot improve
+                    while (sp > 0) {
+                        --sp;
+                        uint2 e;
+                        if (sp < SW) e = make_uint2(s_wid[sp][tid], __float_as_uint(bf16_up(s_wt[sp][tid])));
+                        else e = wstack[sp - SW];
+                        if (__uint_as_float(e.y) <= key_t(key)) {
+                            node = e.x;
+                            break;
+                        }
+                    }
+                    done = node == INVALID;
+                }
+            }
+        } else {
+            // binary walks: one fetch for every active lane, leaf or internal, before the branch: a
+            // wave holding both kinds would otherwise wait for two dependent round trips (leaf records
+            // and child-pair records are both 64-B aligned records)
+            const bool isleaf = (node & LEAF_BIT) != 0;
+            const v4f* rr = isleaf ? reinterpret_cast<const v4f*>(leaf + 4 * (size_t)(node & ~LEAF_BIT))
+                                   : reinterpret_cast<const v4f*>(inner + node);
+            v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
+            pin(q0); pin(q1); pin(q2); pin(q3);
+            if (GUARD && --guard == 0) {
+                c.overflow++;
+                done = true;
+            } else if (isleaf) {
+                const uint32_t j = node & ~LEAF_BIT;
+                if (COUNT) c.leaf++;
+                const float t = ray_triangle(o, d, mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), mk(q1.z, q1.w, q2.x));
                 if (t != -1.f && (!hit || t < best || (NEAREST && t == best && j < bl))) {
                     best = t;
                     bl = j;
                     btri = __float_as_uint(q2.y) & ~LEAF_BIT;
                     hit = true;
                 }
-            }
-            if (WIDE) {
-                node = INVALID;   // pop below
-            } else {
                 node = top;                             // pop
                 spop_top();
                 done = sp == -1;
-            }
-        } else if (WIDE) {
-            if (COUNT) c.internal++;
-            // the four grandchildren: ids (a3.x, a3.y, b3.x, b3.y), entry distances t0..t3
-            uint4 a3, b3;
-            float t0, t1, t2, t3;
-            bool h0, h1, h2, h3;
-            const float kb = key_t(key);
-            if (q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
-                const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w, sy = q1.x, sz = q1.y;
-                const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
-                const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
-                a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
-                b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
-                if (qfast) {
-                    const QAxis X = qaxis(ox, sx, lx, hx, o.x, inv.x), Y = qaxis(oy, sy, ly, hy, o.y, inv.y),
-                                Z = qaxis(oz, sz, lz, hz, o.z, inv.z);
-                    h0 = qbox_fast(X, Y, Z, 0, true, kb, t0);
-                    h1 = qbox_fast(X, Y, Z, 1, true, kb, t1);
-                    h2 = qbox_fast(X, Y, Z, 2, true, kb, t2);
-                    h3 = qbox_fast(X, Y, Z, 3, true, kb, t3);
+            } else {
+                if (COUNT) c.internal++;
+                const uint32_t own = __float_as_uint(q3.z);
+                const uint32_t cl = child_slot(__float_as_uint(q3.x), own, 0), cr = child_slot(__float_as_uint(q3.y), own, 1);
+                float tl, tr;
+                const bool lh = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, tl);
+                const bool rh = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, tr);
+                if (!lh && !rh) {
+                    node = top;                             // pop
+                    spop_top();
+                    done = sp == -1;
                 } else {
-#define RTBVH_QBOX(c, t)                                                                                      \
-    ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
-            qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), true, kb, t)
-                    h0 = RTBVH_QBOX(0, t0);
-                    h1 = RTBVH_QBOX(1, t1);
-                    h2 = RTBVH_QBOX(2, t2);
-                    h3 = RTBVH_QBOX(3, t3);
-#undef RTBVH_QBOX
-                }
-                h1 = h1 & (a3.y != INVALID);
-                h3 = h3 & (b3.y != INVALID);
-            } else {
-                // a node without a finite grid: its exact record pair (node = its slot; the
-                // pair of its children's records is at 2 * own, own = word 14 of its record)
-                const uint32_t own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
-                const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
-                q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
-                const v4f q4 = pr[4], q5 = pr[5], q6 = pr[6], q7 = pr[7];
-                a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
-                b3 = make_uint4(__float_as_uint(q7.x), __float_as_uint(q7.y), 0u, 0u);
-                // grandchild ids -> slots (2 * parent + side; parent = word 14)
-                const uint32_t ol = __float_as_uint(q3.z), orr = __float_as_uint(q7.z);
-                if (!(a3.x & LEAF_BIT)) a3.x = 2 * ol;
-                if (a3.y != INVALID && !(a3.y & LEAF_BIT)) a3.y = 2 * ol + 1;
-                if (!(b3.x & LEAF_BIT)) b3.x = 2 * orr;
-                if (b3.y != INVALID && !(b3.y & LEAF_BIT)) b3.y = 2 * orr + 1;
-                h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, true, kb, t0);
-                h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, true, kb, t1) & (a3.y != INVALID);
-                h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, true, kb, t2);
-                h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, true, kb, t3) & (b3.y != INVALID);
-            }
-            const float INF = __builtin_inff();
-            float k0 = h0 ? t0 : INF, k1 = h1 ? t1 : INF, k2 = h2 ? t2 : INF, k3 = h3 ? t3 : INF;
-            uint32_t i0 = h0 ? a3.x : INVALID, i1 = h1 ? a3.y : INVALID, i2 = h2 ? b3.x : INVALID,
-                     i3 = h3 ? b3.y : INVALID;
-            // 4-element sorting network on the entry distance (missing children last)
-            sort2(k0, i0, k1, i1);
-            sort2(k2, i2, k3, i3);
-            sort2(k0, i0, k2, i2);
-            sort2(k1, i1, k3, i3);
-            sort2(k1, i1, k2, i2);
-            node = i0;   // nearest (INVALID when no child is hit -> pop below)
-            if (sp + 3 > limit) {
-                c.overflow++;
-                done = true;
-            } else {   // push the others farthest first
-                if (i3 != INVALID) wpush(i3, k3);
-                if (i2 != INVALID) wpush(i2, k2);
-                if (i1 != INVALID) wpush(i1, k1);
-            }
-        } else {
-            if (COUNT) c.internal++;
-            const uint32_t own = __float_as_uint(q3.z);
-            const uint32_t cl = child_slot(__float_as_uint(q3.x), own, 0), cr = child_slot(__float_as_uint(q3.y), own, 1);
-            float tl, tr;
-            const bool lh = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, hit, best, tl);
-            const bool rh = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, tr);
-            if (!lh && !rh) {
-                node = top;                             // pop
-                spop_top();
-                done = sp == -1;
-            } else {
-                const bool swap = NEAREST && lh && rh && tr < tl;
-                if (lh && rh) {
-                    if (sp + 1 >= limit) {
-                        c.overflow++;
-                        node = top;
-                        spop_top();
-                        done = sp == -1;
+                    const bool swap = NEAREST && lh && rh && tr < tl;
+                    if (lh && rh) {
+                        if (sp + 1 >= limit) {
+                            c.overflow++;
+                            node = top;
+                            spop_top();
+                            done = sp == -1;
+                        } else {
+                            spush(top);                     // push the second child
+                            top = swap ? cl : cr;
+                            node = swap ? cr : cl;
+                        }
                     } else {
-                        spush(top);                     // push the second child
-                        top = swap ? cl : cr;
-                        node = swap ? cr : cl;
+                        node = lh ? cl : cr;
                     }
-                } else {
-                    node = lh ? cl : cr;
                 }
             }
-        }
-        if (WIDE && !done && node == INVALID) {   // pop, dropping entries that cannot improve
-            while (sp > 0) {
-                --sp;
-                uint2 e;
-                if (sp < SW) e = make_uint2(s_wid[sp][tid], __float_as_uint(bf16_up(s_wt[sp][tid])));
-                else e = wstack[sp - SW];
-                if (__uint_as_float(e.y) <= key_t(key)) {
-                    node = e.x;
-                    break;
-                }
-            }
-            done = node == INVALID;
         }
         if (done) {
             // (t, triangle) of the hit, INVALID for a miss: the shading reads no leaf record
