@@ -233,6 +233,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     BuildArgs a{};
     a.opos = c->d_opos;
     a.idx = c->d_idx;
+    a.matidx = c->d_matidx;
     a.V = c->V;
     a.T = c->T;
     a.morton_mode = (int)c->cfg.morton_mode;

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounds_final(float* __restrict__ boun
 
 // MortonCodes.hlsl:54-125 (HLSL mode) / ShaderSim/main.cpp:292-301 (CPUTests mode):
 // triangle t's code (also stored in keys/vals) and its clip-space triangle
-__device__ __forceinline__ uint32_t morton_code(const BuildArgs& a, uint32_t t, float4 (&clip)[3]) {
+__device__ __forceinline__ uint32_t morton_code(const BuildArgs& a, uint32_t t, float4 (&clip)[4]) {
     const uint32_t i0 = a.idx[3 * (size_t)t], i1 = a.idx[3 * (size_t)t + 1], i2 = a.idx[3 * (size_t)t + 2];
     const float4 q0 = a.opos[i0], q1 = a.opos[i1], q2 = a.opos[i2];
     const f3 p0 = mk(q0.x, q0.y, q0.z), p1 = mk(q1.x, q1.y, q1.z), p2 = mk(q2.x, q2.y, q2.z);
@@ -145,14 +145,16 @@ __device__ __forceinline__ uint32_t morton_code(const BuildArgs& a, uint32_t t, 
     clip[0] = make_float4(c0.x, c0.y, c0.z, __uint_as_float(t));
     clip[1] = make_float4(c1.x, c1.y, c1.z, 0.f);
     clip[2] = make_float4(c2.x, c2.y, c2.z, 0.f);
+    // the shading's gathers in one record: the vertex indices and the material index
+    clip[3] = make_float4(__uint_as_float(i0), __uint_as_float(i1), __uint_as_float(i2), __uint_as_float(a.matidx[t]));
     return code;
 }
 __device__ __forceinline__ uint32_t morton_tri(const BuildArgs& a, uint32_t t) {
-    float4 clip[3];
+    float4 clip[4];
     const uint32_t code = morton_code(a, t, clip);
     float4* o = a.tclip + TCS * (size_t)t;
     o[0] = clip[0]; o[1] = clip[1]; o[2] = clip[2];
-    if (TCS == 4) o[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (TCS == 4) o[3] = clip[3];
     return code;
 }
 // One thread per triangle; the 48-B clip-space triangles of a wave (3 KB contiguous) are staged
@@ -162,11 +164,11 @@ __global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
     __shared__ float4 s_clip[BLOCK / 64][TCS * 64];
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     if (t < a.T) {
-        float4 clip[3];
+        float4 clip[4];
         morton_code(a, t, clip);
 #pragma unroll
         for (int k = 0; k < 3; k++) s_clip[w][TCS * lane + k] = clip[k];
-        if (TCS == 4) s_clip[w][TCS * lane + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (TCS == 4) s_clip[w][TCS * lane + 3] = clip[3];
     }
     __syncthreads();
     const uint32_t t0 = t - lane;   // the wave's first triangle

@@ -3,7 +3,8 @@
 //
 // HBM layout (see DESIGN.md "Data layout"):
 //   opos   float4[V]     object-space vertex positions (w unused), set_scene
-//   tclip  float4[4*T]   per-triangle clip-space vertices (+ a zero float4), TRIANGLE order (Morton kernel)
+//   tclip  float4[4*T]   per-triangle clip-space vertices (w of the first: the triangle) and
+//                        {vertex indices, material index}: 64-B records, TRIANGLE order (Morton kernel)
 //   keys/vals u32[T] x2  radix ping-pong (Morton code, triangle id)
 //   leaf   float4[4*T]   64-B leaf records in SORTED order: {v0.xyz, e1.x}, {e1.yz, e2.xy},
 //                        {e2.z, tri, bmin.xy}, {bmin.z, bmax.xyz}; e1 = v1-v0, e2 = v2-v0

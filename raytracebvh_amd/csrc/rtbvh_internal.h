@@ -41,6 +41,7 @@ SortResult radix_sort_pairs(const uint32_t* kin, const uint32_t* vin, uint32_t* 
 struct BuildArgs {
     const float4* opos;       // [V]
     const uint32_t* idx;      // [3T]
+    const uint32_t* matidx;   // [T] (into the clip triangle's fourth float4 for the shading)
     uint32_t V, T;
     int morton_mode, delta_mode;
     Mat4 wvp;
@@ -48,7 +49,7 @@ struct BuildArgs {
     float* bounds;            // CPUTests mode: [0..5] scene box (min xyz, max xyz), [8..] 1024 x 6 partials
     uint32_t* keys;           // [T] Morton codes (triangle order) -> sort input
     uint32_t* vals;           // [T] triangle ids
-    float4* tclip;            // [3T]
+    float4* tclip;            // [TCS * T]
     const uint32_t* sorted_keys;  // [T]
     const uint32_t* sorted_vals;  // [T]
     float4* leaf;             // [4T] 64-B sorted leaf records

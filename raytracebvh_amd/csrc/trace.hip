@@ -578,12 +578,22 @@ __device__ __forceinline__ HitInfo shade_hit_tri(const TraceArgs& a, uint32_t tr
     HitInfo h;
     const float4* P = a.tclip + TCS * (size_t)tri;
     const float4 a0 = P[0], a1 = P[1], a2 = P[2];
+    // vertex and material indices: the record's fourth float4 (k_morton), else the index arrays
+    uint32_t vi[3], mi;
+    if (TCS == 4) {
+        const float4 a3 = P[3];
+        vi[0] = __float_as_uint(a3.x); vi[1] = __float_as_uint(a3.y); vi[2] = __float_as_uint(a3.z);
+        mi = __float_as_uint(a3.w);
+    } else {
+        vi[0] = a.idx[3 * (size_t)tri]; vi[1] = a.idx[3 * (size_t)tri + 1]; vi[2] = a.idx[3 * (size_t)tri + 2];
+        mi = a.matidx[tri];
+    }
     const f3 P0 = mk(a0.x, a0.y, a0.z), P1 = mk(a1.x, a1.y, a1.z), P2 = mk(a2.x, a2.y, a2.z);
     f3 n[3];
     float uv[3][2];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        const float* v = a.verts + 8 * (size_t)a.idx[3 * (size_t)tri + k];
+        const float* v = a.verts + 8 * (size_t)vi[k];
         n[k] = xform_normal(a.wv.m, mk(v[3], v[4], v[5]));
         uv[k][0] = v[6];
         uv[k][1] = v[7];
@@ -597,7 +607,7 @@ __device__ __forceinline__ HitInfo shade_hit_tri(const TraceArgs& a, uint32_t tr
     const float tu = (uv[0][0] * w1 + uv[1][0] * w2) + uv[2][0] * w3;
     const float tv = (uv[0][1] * w1 + uv[1][1] * w2) + uv[2][1] * w3;
     h.nrm = add(add(mul(n[0], w1), mul(n[1], w2)), mul(n[2], w3));
-    const Mat& m = a.mats[a.matidx[tri]];
+    const Mat& m = a.mats[mi];
     h.textured = m.tex_num != -1;
     float tx = 1.f, ty = 1.f, tz = 1.f, tw = 1.f;   // RayTraceRender.hlsl:19
     if (h.textured && (uint32_t)m.tex_num < a.ntex) {   // :22-26 (no texture bound: white)
