@@ -14,11 +14,12 @@ namespace rtbvh {
 namespace {
 
 #ifndef RTBVH_NT_STORES
-#define RTBVH_NT_STORES 3
+#define RTBVH_NT_STORES 7
 #endif
 // Streaming stores of the coalesced build outputs (RTBVH_NT_STORES bit 0: the Morton pass's clip
-// triangles, bit 1: the staged leaf records).  NT = 1 only; the scattered record/QNode stores stay
-// plain (non-temporal there: refit stage 1.0 -> 3.3 ms at C4).
+// triangles, bit 1: the staged leaf records, bit 2: k_refit's staged records / pseudo-records /
+// QNodes).  NT = 1 only; scattered 64-B record stores non-temporal ran 3x slower (refit stage
+// 1.0 -> 3.3 ms at C4), the same records staged through LDS and stored 16 B per lane 12% faster.
 template <int BIT>
 __device__ __forceinline__ void st_out(float4* p, float4 v) {
     typedef float v4 __attribute__((ext_vector_type(4)));
@@ -33,6 +34,12 @@ constexpr uint32_t BLOCK = 256;
 // leaves (and node indices) per k_refit workgroup: the nodes whose leaf range lies inside
 // one join in LDS; the others ("crossing") climb in k_refit_top
 constexpr uint32_t RBLOCK = RTBVH_REFIT_BLOCK;
+#ifndef RTBVH_REFIT_STAGE
+#define RTBVH_REFIT_STAGE 1   // k_refit phase 4: records, pseudo-records and QNodes out through LDS
+#endif
+#ifndef RTBVH_REFIT_STAGE_SLOTS
+#define RTBVH_REFIT_STAGE_SLOTS 512   // slots per phase-4 round (32 KB; C4 A/B: 256 and 512 alike, 1024 slower)
+#endif
 
 __device__ __forceinline__ uint32_t expand_bits(uint32_t var) {   // MortonCodes.hlsl:13-31
     var &= 0x000003ffu; var |= var << 16;
@@ -380,14 +387,23 @@ __device__ __forceinline__ void ld_box_sc1(const float* src, f3& lo, f3& hi) {
 __device__ __forceinline__ uint32_t general_box(f3 lo, f3 hi) {
     return lo.x < hi.x && lo.y < hi.y && lo.z <= hi.z && 0.f <= hi.z && hi.z < INFINITY ? 0u : 1u;
 }
-__device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
-                                             uint32_t cr, uint32_t own) {
-    float4* d = reinterpret_cast<float4*>(dst);
+__device__ __forceinline__ void record_words(f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl, uint32_t cr, uint32_t own,
+                                             float4 (&d)[4]) {
     const uint32_t gen = general_box(lmin, lmax) | general_box(rmin, rmax) << 1;
     d[0] = make_float4(lmin.x, lmin.y, lmax.x, lmax.y);
     d[1] = make_float4(rmin.x, rmin.y, rmax.x, rmax.y);
     d[2] = make_float4(lmin.z, lmax.z, rmin.z, rmax.z);
     d[3] = make_float4(__uint_as_float(cl), __uint_as_float(cr), __uint_as_float(own), __uint_as_float(gen));
+}
+__device__ __forceinline__ void store4(void* dst, const float4 (&w)[4]) {
+    float4* d = reinterpret_cast<float4*>(dst);
+    d[0] = w[0]; d[1] = w[1]; d[2] = w[2]; d[3] = w[3];
+}
+__device__ __forceinline__ void store_record(Inner* dst, f3 lmin, f3 lmax, f3 rmin, f3 rmax, uint32_t cl,
+                                             uint32_t cr, uint32_t own) {
+    float4 w[4];
+    record_words(lmin, lmax, rmin, rmax, cl, cr, own, w);
+    store4(dst, w);
 }
 // box of child `side` from a node record: min xyz, max xyz
 __device__ __forceinline__ void record_box(const Inner* r, uint32_t side, float out[6]) {
@@ -404,14 +420,18 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t parent_code, uint32_t T) {
 // record whose two children are the leaf itself and nothing).  The absent second child repeats
 // the box with a NaN min.z, which fails the primary walk's fast test (min.z <= bound) for every
 // lane, so that walk needs no id check; both bits of word 15 are the leaf box's own.
-__device__ __forceinline__ void store_pseudo_record(Inner* dst, uint32_t leaf_id, f3 lo, f3 hi) {
-    float4* d = reinterpret_cast<float4*>(dst);
+__device__ __forceinline__ void pseudo_words(uint32_t leaf_id, f3 lo, f3 hi, float4 (&d)[4]) {
     const uint32_t gen = general_box(lo, hi) * 3u;
     d[0] = make_float4(lo.x, lo.y, hi.x, hi.y);
     d[1] = make_float4(lo.x, lo.y, hi.x, hi.y);
     d[2] = make_float4(lo.z, hi.z, __uint_as_float(ABSENT_MINZ), hi.z);
     d[3] = make_float4(__uint_as_float(leaf_id), __uint_as_float(INVALID), __uint_as_float(leaf_id),
                        __uint_as_float(gen));
+}
+__device__ __forceinline__ void store_pseudo_record(Inner* dst, uint32_t leaf_id, f3 lo, f3 hi) {
+    float4 w[4];
+    pseudo_words(leaf_id, lo, hi, w);
+    store4(dst, w);
 }
 __device__ __forceinline__ void store_leaf_record(Inner* rec, uint32_t p, uint32_t side, uint32_t leaf_id, f3 lo,
                                                   f3 hi) {
@@ -509,9 +529,9 @@ __device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float 
 
 // the QNode of a node from its four grandchild boxes (x/y/z min and max per grandchild c) and
 // ids, written as four 16-B stores
-__device__ __forceinline__ void store_qnode(QNode* dst, const float (&lx)[4], const float (&ly)[4],
-                                            const float (&lz)[4], const float (&hx)[4], const float (&hy)[4],
-                                            const float (&hz)[4], uint4 ids) {
+__device__ __forceinline__ void qnode_words(const float (&lx)[4], const float (&ly)[4], const float (&lz)[4],
+                                            const float (&hx)[4], const float (&hy)[4], const float (&hz)[4], uint4 ids,
+                                            float4 (&d)[4]) {
     QNode q;
     bool ok = quantize_axis(lx, hx, q.org[0], q.scl[0], q.lo[0], q.hi[0]);
     ok = quantize_axis(ly, hy, q.org[1], q.scl[1], q.lo[1], q.hi[1]) && ok;
@@ -519,7 +539,6 @@ __device__ __forceinline__ void store_qnode(QNode* dst, const float (&lx)[4], co
     if (!ok) q.scl[0] = 0.f;   // the traversal reads the exact pair for this node
     q.id[0] = ids.x; q.id[1] = ids.y; q.id[2] = ids.z; q.id[3] = ids.w;
     const float4* qs = reinterpret_cast<const float4*>(&q);
-    float4* d = reinterpret_cast<float4*>(dst);
     d[0] = qs[0]; d[1] = qs[1]; d[2] = qs[2]; d[3] = qs[3];
 }
 
@@ -548,7 +567,7 @@ __device__ __forceinline__ void qent_sel(QEnt& d, const QEnt& s, bool take) {
 }
 // Kids(e, c0, c1): the two children of internal entry e
 template <class Kids>
-__device__ __forceinline__ void greedy_qnode(const QEnt& e0, const QEnt& e1, Kids&& kids, QNode* dst) {
+__device__ __forceinline__ void greedy_qnode_words(const QEnt& e0, const QEnt& e1, Kids&& kids, float4 (&out)[4]) {
     QEnt E[4] = {e0, e1, e0, e0};
     uint32_t n = 2;
 #pragma unroll
@@ -590,7 +609,13 @@ __device__ __forceinline__ void greedy_qnode(const QEnt& e0, const QEnt& e1, Kid
     }
     if (absent1) id[1] = INVALID;
     if (absent3) id[3] = INVALID;
-    store_qnode(dst, lx, ly, lz, hx, hy, hz, make_uint4(id[0], id[1], id[2], id[3]));
+    qnode_words(lx, ly, lz, hx, hy, hz, make_uint4(id[0], id[1], id[2], id[3]), out);
+}
+template <class Kids>
+__device__ __forceinline__ void greedy_qnode(const QEnt& e0, const QEnt& e1, Kids&& kids, QNode* dst) {
+    float4 w[4];
+    greedy_qnode_words(e0, e1, kids, w);
+    store4(dst, w);
 }
 // entries from the node records in global memory (record words: rtbvh_device.h)
 __device__ __forceinline__ void record_kids(const Inner* __restrict__ rec, uint32_t slot, QEnt& c0, QEnt& c1) {
@@ -659,11 +684,14 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     __shared__ uint32_t s_cnt[RBLOCK];
     // node base + k: the boxes of its children (side 0, 1); before the climb, the staging
     // buffer of the leaf-record stores (128 float4 per wave)
-    __shared__ __align__(16) float s_box[RBLOCK][2][6];
+    // (RBLOCK rows; more when phase 4's staging buffer, which reuses it, needs them)
+    __shared__ __align__(16) float s_box[RBLOCK * 12 >= RTBVH_REFIT_STAGE_SLOTS * 16 ? RBLOCK
+                                                                                  : RTBVH_REFIT_STAGE_SLOTS * 16 / 12 + 1][2][6];
     static_assert(sizeof(float) * 12 * RBLOCK >= 16 * 128 * (RBLOCK / 64), "leaf staging fits in s_box");
     __shared__ uint4 s_topo[RBLOCK];        // the block's nodes [base, base + BLOCK): ids, leaf range
     __shared__ uint32_t s_pint[RBLOCK];
     __shared__ uint32_t s_xn;
+    __shared__ uint32_t s_own[RTBVH_REFIT_STAGE_SLOTS / 32];   // phase 4: staged slots of this round
     const uint32_t T = a.T;
     const uint32_t base = blockIdx.x * RBLOCK, tid = threadIdx.x;
     const uint32_t i = base + tid;
@@ -740,15 +768,18 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     __syncthreads();
     if (tid == 0) a.xcnt[blockIdx.x] = s_xn;
     // 3. the block's in-block nodes: record, leaf pseudo-records, QNode
-    if (i + 1 >= T || xnode) return;
+    const bool mine = i + 1 < T && !xnode;
+    if (!RTBVH_REFIT_STAGE && !mine) return;
+    f3 l0 = mk(0.f, 0.f, 0.f), l1 = l0, r0 = l0, r1 = l0;
+    uint32_t slot = INVALID;
+    float4 rw[4], qw[4];
+    if (mine) {
     const float* L = s_box[tid][0];
     const float* R = s_box[tid][1];
-    const f3 l0 = mk(L[0], L[1], L[2]), l1 = mk(L[3], L[4], L[5]);
-    const f3 r0 = mk(R[0], R[1], R[2]), r1 = mk(R[3], R[4], R[5]);
-    const uint32_t slot = slot_of(s_pint[tid], T);
-    store_record(a.rec + slot, l0, l1, r0, r1, q.x, q.y, i);
-    if (q.x & LEAF_BIT) store_leaf_record(a.rec, i, 0, q.x, l0, l1);
-    if (q.y & LEAF_BIT) store_leaf_record(a.rec, i, 1, q.y, r0, r1);
+    l0 = mk(L[0], L[1], L[2]); l1 = mk(L[3], L[4], L[5]);
+    r0 = mk(R[0], R[1], R[2]); r1 = mk(R[3], R[4], R[5]);
+    slot = slot_of(s_pint[tid], T);
+    record_words(l0, l1, r0, r1, q.x, q.y, i, rw);
     // the QNode: its entries' boxes are in LDS (an in-block node's subtree is in the block)
     const auto lds_kids = [&](uint32_t x, QEnt& c0, QEnt& c1) {   // children of in-block node x
         const uint4 xq = s_topo[x - base];
@@ -764,7 +795,66 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     };
     QEnt e0, e1;
     lds_kids(i, e0, e1);
-    greedy_qnode(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, a.qnode + slot);
+    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, qw);
+    }
+    if (!RTBVH_REFIT_STAGE) {
+        store4(a.rec + slot, rw);
+        if (q.x & LEAF_BIT) store_leaf_record(a.rec, i, 0, q.x, l0, l1);
+        if (q.y & LEAF_BIT) store_leaf_record(a.rec, i, 1, q.y, r0, r1);
+        store4(a.qnode + slot, qw);
+        return;
+    }
+    // 4. the outputs through LDS.  Every slot this block writes in phase 3 lies in its window
+    // [2 base, 2 base + 2 RBLOCK) -- a node's record / QNode at 2 parent + side with the parent in
+    // the block, a leaf child's pseudo-record at 2 i + side -- except the record and QNode of a
+    // node whose parent crosses the block (a few per block; stored directly).  The window goes
+    // out STAGE slots at a time: the writers fill the staging buffer (over s_box, read no more)
+    // and mark their slots, then the block stores the marked slots 16 B per lane, consecutive
+    // lanes on consecutive bytes (a 64-B record per lane writes at ~0.6x that rate).
+    // Unmarked slots (records of crossing nodes, k_refit_top's; other blocks' records) are left
+    // alone.
+    constexpr uint32_t STAGE = RTBVH_REFIT_STAGE_SLOTS;
+    static_assert(sizeof(s_box) >= 64 * STAGE, "staging fits in s_box");
+    static_assert((2 * RBLOCK) % STAGE == 0, "whole rounds");
+    float4* s_stage = reinterpret_cast<float4*>(&s_box[0][0][0]);
+    const uint32_t w0 = 2 * base;
+    const bool rin = mine && slot - w0 < 2 * RBLOCK;
+    if (mine && !rin) {
+        store4(a.rec + slot, rw);
+        store4(a.qnode + slot, qw);
+    }
+    const uint32_t nslots = 2 * T - 1;
+#pragma unroll
+    for (uint32_t kind = 0; kind < 2; kind++) {   // 0: records and pseudo-records, 1: QNodes
+        float4* dst = kind ? reinterpret_cast<float4*>(a.qnode) : reinterpret_cast<float4*>(a.rec);
+#pragma unroll 1
+        for (uint32_t r = 0; r < 2 * RBLOCK; r += STAGE) {
+            __syncthreads();   // s_box reads (first round) / the previous round's stores are done
+            if (tid < STAGE / 32) s_own[tid] = 0;
+            __syncthreads();
+            const uint32_t lo_slot = w0 + r;
+            const auto put = [&](uint32_t sl, const float4 (&w)[4]) {
+                const uint32_t k = sl - lo_slot;
+                if (k < STAGE) {
+                    s_stage[4 * k] = w[0]; s_stage[4 * k + 1] = w[1];
+                    s_stage[4 * k + 2] = w[2]; s_stage[4 * k + 3] = w[3];
+                    atomicOr(&s_own[k >> 5], 1u << (k & 31));
+                }
+            };
+            if (rin) put(slot, kind ? qw : rw);
+            if (kind == 0 && mine) {
+                float4 pw[4];
+                if (q.x & LEAF_BIT) { pseudo_words(q.x, l0, l1, pw); put(2 * i, pw); }
+                if (q.y & LEAF_BIT) { pseudo_words(q.y, r0, r1, pw); put(2 * i + 1, pw); }
+            }
+            __syncthreads();
+            for (uint32_t c = tid; c < 4 * STAGE; c += RBLOCK) {
+                const uint32_t k = c >> 2;
+                if ((s_own[k >> 5] >> (k & 31)) & 1u && lo_slot + k < nslots)
+                    st_out<4>(dst + 4 * (size_t)(lo_slot + k) + (c & 3), s_stage[c]);
+            }
+        }
+    }
 }
 
 // The crossing nodes (a few per k_refit workgroup, the top of the tree among them): k_refit
