@@ -36,6 +36,9 @@ def main():
     if os.environ.get("AB_SET") == "base":   # the bench's mode only (A/B of two builds via RTBVH_LIB)
         variants = [("nearest-first-wide", rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST
                      | rt.FLAG_WIDE_BVH)]
+    if os.environ.get("AB_SET") == "split":   # one frame over 1 / 2 / 3 primary->bounce chains
+        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+        variants = [(f"split {k}", base | (k << rt.FLAG_SPLIT_SHIFT)) for k in (1, 2, 3, 4)]
     if os.environ.get("AB_SET") == "wide":
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE
         variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),
