@@ -372,6 +372,13 @@ def main():
         traversal["frames_identical"][m] = ident
         if ident and args.traversal != "reference" and r["ms_step"] < res[use_name]["ms_step"]:
             use_name = m
+    # the profiled mode (its PMC file prices the roofline's traffic) unless another identical mode
+    # is clearly faster: within 2% the step times are noise (a gloo rehearsal's step is its host-side
+    # gather), and the headline is then the profiled mode's own, never a faster one's
+    pref = "nearest-first-wide"
+    if use_name != pref and traversal["frames_identical"].get(pref) and args.traversal != "reference" \
+            and res[pref]["ms_step"] <= 1.02 * res[use_name]["ms_step"]:
+        use_name = pref
     use = res[use_name]
     traversal["mode"] = use_name
     mode_flags = modes[use_name]
