@@ -189,14 +189,22 @@ __global__ __launch_bounds__(BLOCK) void k_morton(BuildArgs a) {
 // ---- Karras 2012 (BVHConstructP1.hlsl:61-165) --------------------------------
 // `c` is the sorted code sequence: a pointer, or an accessor c(j) (the one-workgroup build
 // reads the codes from LDS)
+// Indices are 32-bit: set_scene takes T < 2^30, so every probe I + k * d of the searches below
+// (k <= 2^30: the doubling stops at the first probe outside [0, T)) lies in (-2^31, 2^31), and
+// one unsigned compare is the range test (a negative j wraps above n).
 template <class C>
-__device__ __forceinline__ uint32_t code_at(const C& c, int64_t j) { return c[j]; }
+__device__ __forceinline__ uint32_t code_at(const C& c, int32_t j) { return c[j]; }
 
+// Branch-free (selects, one code read at a clamped index): the searches' lanes probe different
+// j, and a divergent early return or tie branch cost the wave both paths on every probe.
 template <class C>
-__device__ __forceinline__ int delta_clz64(const C& c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
-    if (j < 0 || j >= n) return -1;   // leadingPrefixBounds :78-84
-    const uint32_t cj = code_at(c, j);
-    return ci != cj ? __clz((int)(ci ^ cj)) : 32 + __clz((int)(i ^ (uint32_t)j));
+__device__ __forceinline__ int delta_clz64(const C& c, uint32_t n, uint32_t i, uint32_t ci, int32_t j) {
+    const bool in = (uint32_t)j < n;   // leadingPrefixBounds :78-84: -1 outside
+    const uint32_t jj = in ? (uint32_t)j : i;
+    const uint32_t x = ci ^ code_at(c, (int32_t)jj), y = i ^ jj;
+    int rx = (int)__clz((int)x), ry = 32 + (int)__clz((int)y);
+    asm volatile("" : "+v"(rx), "+v"(ry));   // both computed, then selected (not a divergent branch)
+    return in ? (x != 0u ? rx : ry) : -1;
 }
 __device__ __forceinline__ int debruijn_lz(uint32_t data) {   // RadixBVHCombo/main.cpp:136-151
     const int tbl[32] = {0, 31, 9, 30, 3, 8, 13, 29, 2, 5, 7, 21, 12, 24, 28, 19,
@@ -206,40 +214,41 @@ __device__ __forceinline__ int debruijn_lz(uint32_t data) {   // RadixBVHCombo/m
     return data ? tbl[(uint32_t)(data * 0x076be629u) >> 27] : 32;
 }
 template <class C>
-__device__ __forceinline__ int delta_cputests(const C& c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
-    if (j < 0 || j >= n) return -1;
+__device__ __forceinline__ int delta_cputests(const C& c, uint32_t n, uint32_t i, uint32_t ci, int32_t j) {
+    if ((uint32_t)j >= n) return -1;
     const uint32_t cj = code_at(c, j);
     return debruijn_lz(ci == cj ? (i ^ (uint32_t)j) : (ci ^ cj));
 }
 
 template <int MODE, class C>
-__device__ __forceinline__ int delta(const C& c, int64_t n, uint32_t i, uint32_t ci, int64_t j) {
+__device__ __forceinline__ int delta(const C& c, uint32_t n, uint32_t i, uint32_t ci, int32_t j) {
     return MODE == 0 ? delta_clz64(c, n, i, ci, j) : delta_cputests(c, n, i, ci, j);
 }
 
 template <int MODE, class C>
 __device__ void karras_node(const C& c, uint32_t n, uint32_t i, uint4* __restrict__ topo,
                             uint32_t* __restrict__ pleaf, uint32_t* __restrict__ pint) {
-    const int64_t N = n, I = i;
+    const uint32_t N = n;
+    const int32_t I = (int32_t)i;
     const uint32_t ci = code_at(c, I);
-    const int64_t d = delta<MODE>(c, N, i, ci, I + 1) < delta<MODE>(c, N, i, ci, I - 1) ? -1 : 1;
+    const int32_t d = delta<MODE>(c, N, i, ci, I + 1) < delta<MODE>(c, N, i, ci, I - 1) ? -1 : 1;
     const int min_lz = delta<MODE>(c, N, i, ci, I - d);
-    int64_t bound_len = 2;
+    int32_t bound_len = 2;
     while (min_lz < delta<MODE>(c, N, i, ci, I + bound_len * d)) bound_len <<= 1;
-    int64_t dl = bound_len, dsum = 0;
+    int32_t dl = bound_len, dsum = 0;
     do {
         dl = (dl + 1) >> 1;
         if (min_lz < delta<MODE>(c, N, i, ci, I + (dsum + dl) * d)) dsum += dl;
     } while (1 < dl);
-    const int64_t bound_start = I + dsum * d;
+    const int32_t bound_start = I + dsum * d;
     const int lz = delta<MODE>(c, N, i, ci, bound_start);
     dl = dsum;
-    int64_t tmp = 0;
+    int32_t tmp = 0;
     do {
         dl = (dl + 1) >> 1;
         if (lz < delta<MODE>(c, N, i, ci, I + (tmp + dl) * d)) tmp += dl;
     } while (1 < dl);
-    const int64_t loc = I + tmp * d + (d < 0 ? d : 0);
+    const int32_t loc = I + tmp * d + (d < 0 ? d : 0);
     const bool left_leaf = (I < bound_start ? I : bound_start) == loc;
     const bool right_leaf = (I > bound_start ? I : bound_start) == loc + 1;
     const uint32_t l = (uint32_t)loc, r = (uint32_t)(loc + 1);
@@ -319,15 +328,12 @@ constexpr int64_t KWIN = RTBVH_KARRAS_WIN;
 __shared__ uint32_t s_kwin[BLOCK + 2 * (KWIN > 0 ? KWIN : 0)];
 struct WindowCodes {
     const uint32_t* g;
-    int64_t lo, hi;   // the window [lo, hi) of the code sequence held in s_kwin
-    __device__ uint32_t operator[](int64_t j) const {
-        uint32_t v;
-        if (j >= lo && j < hi) {
-            v = s_kwin[j - lo];
-            asm volatile("" : "+v"(v));   // keeps the two loads apart (merged: one flat load of a selected pointer)
-        } else {
-            v = g[j];
-        }
+    int32_t lo, hi;   // the window [lo, hi) of the code sequence held in s_kwin
+    __device__ uint32_t operator[](int32_t j) const {
+        const bool in = (uint32_t)(j - lo) < (uint32_t)(hi - lo);
+        uint32_t v = s_kwin[in ? j - lo : 0];   // every lane reads LDS; the few outside also global
+        asm volatile("" : "+v"(v));   // keeps the two loads apart (merged: one flat load of a selected pointer)
+        if (!in) v = g[j];
         return v;
     }
 };
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(BLOCK) void k_karras(BuildArgs a) {
         const int64_t hi = base + BLOCK + KWIN < (int64_t)a.T ? base + BLOCK + KWIN : (int64_t)a.T;
         for (int64_t j = lo + threadIdx.x; j < hi; j += BLOCK) s_kwin[j - lo] = a.sorted_keys[j];
         __syncthreads();
-        const WindowCodes codes{a.sorted_keys, lo, hi};
+        const WindowCodes codes{a.sorted_keys, (int32_t)lo, (int32_t)hi};
         if (i + 1 < a.T) karras_node<MODE>(codes, a.T, i, a.topo, a.pleaf, a.pint);
     } else {
         if (i + 1 < a.T) karras_node<MODE>(a.sorted_keys, a.T, i, a.topo, a.pleaf, a.pint);
@@ -921,7 +927,7 @@ constexpr uint32_t SMALL_T = 2048;
 
 struct LdsCodes {   // sorted code j = the high word of the sorted 64-bit key
     const uint64_t* kv;
-    __device__ uint32_t operator[](int64_t j) const { return (uint32_t)(kv[j] >> 32); }
+    __device__ uint32_t operator[](int32_t j) const { return (uint32_t)(kv[j] >> 32); }
 };
 
 template <int MODE>
