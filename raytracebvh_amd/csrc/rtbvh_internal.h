@@ -21,7 +21,10 @@ struct Mat4 { float m[16]; };
 constexpr uint32_t SORT_BLOCK = 256;
 constexpr uint32_t SORT_ITEMS = 16;
 constexpr uint32_t SORT_TILE = SORT_BLOCK * SORT_ITEMS;   // 4096 keys per tile
-constexpr uint32_t RADIX_BITS = 8;
+#ifndef RTBVH_RADIX_BITS
+#define RTBVH_RADIX_BITS 8
+#endif
+constexpr uint32_t RADIX_BITS = RTBVH_RADIX_BITS;   // digit width: 8 (4 passes of 30-bit codes) or 10 (3)
 constexpr uint32_t RADIX = 1u << RADIX_BITS;
 constexpr size_t BOUNDS_WORDS = 8 + 6 * 1024;
 

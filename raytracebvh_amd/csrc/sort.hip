@@ -3,7 +3,7 @@
 // Replaces RadixSortP1.hlsl (1-bit flags + a 256-wide Blelloch scan per
 // group) and RadixSortP2.hlsl (a serial O(G) sum of group counts by thread 0,
 // then a scatter of whole 44-B nodes), run 32 times by Graphics.cpp:735-754.
-// Here: 8-bit digits (4 passes for 32-bit keys, one per byte), 8-B (key, value)
+// Here: RADIX_BITS-bit digits (8: 4 passes for 30-bit codes; 10: 3), 8-B (key, value)
 // payloads, and per pass a reduce-then-scan over 4096-key tiles:
 //   upsweep   tile digit histogram in LDS         -> counts[digit][tile]
 //   scan      one workgroup per digit row          -> exclusive tile offsets + digit totals
@@ -66,8 +66,8 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_upsweep(const uint32_t* __restri
         }
     }
     __syncthreads();
-    uint32_t c = hist[0][tid] + hist[1][tid] + hist[2][tid] + hist[3][tid];
-    counts[(size_t)tid * ntiles + tile] = c;
+    for (uint32_t d = tid; d < RADIX; d += SORT_BLOCK)
+        counts[(size_t)d * ntiles + tile] = hist[0][d] + hist[1][d] + hist[2][d] + hist[3][d];
 }
 
 // one workgroup per digit: exclusive scan of counts[digit][0..ntiles) in place
@@ -115,10 +115,19 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_downsweep(const uint32_t* __rest
     const uint32_t valid = (uint32_t)min((size_t)SORT_TILE, (size_t)n - base);
 
     // global start of each digit for this tile = sum of lower digits + this digit's earlier tiles
+    // (thread tid owns digits [RPT tid, RPT tid + RPT))
+    constexpr uint32_t RPT = RADIX / SORT_BLOCK;
+    static_assert(RADIX % SORT_BLOCK == 0, "whole digits per thread");
     {
-        uint32_t gtot = digit_totals[tid];
-        uint32_t gbase = block_exclusive_scan256(gtot, s_wave, nullptr);
-        s_gstart[tid] = gbase + counts[(size_t)tid * ntiles + tile];
+        uint32_t g[RPT], sum = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < RPT; r++) { g[r] = digit_totals[RPT * tid + r]; sum += g[r]; }
+        uint32_t gbase = block_exclusive_scan256(sum, s_wave, nullptr);
+#pragma unroll
+        for (uint32_t r = 0; r < RPT; r++) {
+            s_gstart[RPT * tid + r] = gbase + counts[(size_t)(RPT * tid + r) * ntiles + tile];
+            gbase += g[r];
+        }
     }
     for (uint32_t k = tid; k < 4 * RADIX; k += SORT_BLOCK) (&s_whist[0][0])[k] = 0;
     __syncthreads();
@@ -155,13 +164,23 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_downsweep(const uint32_t* __rest
     __syncthreads();
     // tile-local digit starts and per-wave offsets
     {
-        const uint32_t c0 = s_whist[0][tid], c1 = s_whist[1][tid], c2 = s_whist[2][tid], c3 = s_whist[3][tid];
-        const uint32_t lstart = block_exclusive_scan256(c0 + c1 + c2 + c3, s_wave, nullptr);
-        s_lstart[tid] = lstart;
-        s_whist[0][tid] = lstart;
-        s_whist[1][tid] = lstart + c0;
-        s_whist[2][tid] = lstart + c0 + c1;
-        s_whist[3][tid] = lstart + c0 + c1 + c2;
+        uint32_t c[RPT][4], sum = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < RPT; r++) {
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) { c[r][k] = s_whist[k][RPT * tid + r]; sum += c[r][k]; }
+        }
+        uint32_t lstart = block_exclusive_scan256(sum, s_wave, nullptr);   // (its barriers: all reads done)
+#pragma unroll
+        for (uint32_t r = 0; r < RPT; r++) {
+            const uint32_t d = RPT * tid + r;
+            s_lstart[d] = lstart;
+            s_whist[0][d] = lstart;
+            s_whist[1][d] = lstart + c[r][0];
+            s_whist[2][d] = lstart + c[r][0] + c[r][1];
+            s_whist[3][d] = lstart + c[r][0] + c[r][1] + c[r][2];
+            lstart += c[r][0] + c[r][1] + c[r][2] + c[r][3];
+        }
     }
     __syncthreads();
 #pragma unroll
