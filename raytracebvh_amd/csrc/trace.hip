@@ -811,7 +811,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __
 // Per-lane traversal state and visit order are exactly those of traverse().
 // A wave refills when at least REFILL_MIN lanes are idle.  A/B on C5 (bounce pass):
 // 4 -> 15.6 ms, 8 -> 9.2, 16 -> 5.5, 24 -> 4.13, 32 -> 3.87, 40 -> 3.84, 48 -> 3.90,
-// 64 -> 5.36 (the single work counter's atomic contention below 32).
+// 64 -> 5.36 (the single work counter's atomic contention below 32).  Round 2's walk, bounce stage
+// with shading: 8 -> 2.67 ms, 16 -> 2.57, 24 -> 2.59, 32 -> 2.62.
 // Work counters: the queue is cut into NEXT_SEGS contiguous segments, each with its own
 // counter on its own 128-B line.  Workgroup b runs on XCD b % 8 (round-robin dispatch); its
 // waves claim from the segments of their XCD first (starting at one picked by b / 8), then from
