@@ -36,8 +36,10 @@ typedef enum {
     RTBVH_ERR_OOM = 3,
     RTBVH_ERR_NOT_READY = 4,      /* e.g. trace before build, build before set_scene */
     RTBVH_ERR_STACK_OVERFLOW = 5, /* rays of a trace hit rtbvh_config.stack_limit (or a cyclic CPUTests-delta
-                                     tree tripped the walk-length guard): the frame is complete, those rays
-                                     ended with the best hit found so far; returned by the synchronising call
+                                     tree tripped the walk-length guard): the frame is complete; a per-lane
+                                     walk's ray ended early, a packet walk skipped the subtree for the rays
+                                     that hit it, each with the best hit found so far (stats.stack_overflows
+                                     counts those rays per event); returned by the synchronising call
                                      after the trace (rtbvh_trace, rtbvh_compute_bvh, rtbvh_trace_tiles,
                                      rtbvh_synchronize), once per new overflow.  The reference's 32-entry
                                      stack is unchecked (RayTraceTraversal.hlsl:9,115,187). */
@@ -151,7 +153,8 @@ typedef struct {
     float scene_bb_max[3];   /* MORTON_HLSL only: cbuffer sceneBBMax (Graphics.cpp:528 uses +700) */
     void* stream;            /* hipStream_t to use, or NULL: the context creates its own */
     uint32_t stack_limit;    /* traversal stack entries a ray may use, 0 = the compiled capacity (66 binary,
-                                100 4-wide; a clz64 tree never needs more); 32 = the reference's stack
+                                100 for the 4-wide primary packets, 192 for the 4-wide bounce walk; a clz64
+                                tree never needs more); 32 = the reference's stack
                                 (RayTraceTraversal.hlsl:9): rays that would overflow it end early and the
                                 trace reports RTBVH_ERR_STACK_OVERFLOW */
     uint32_t reserved;       /* must be 0 */

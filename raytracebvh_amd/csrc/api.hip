@@ -150,8 +150,18 @@ hipError_t dalloc(T*& p, size_t count) {
     return hipMalloc((void**)&p, count * sizeof(T));
 }
 
+// A captured frame (RTBVH_FLAG_GRAPH) holds the device pointers of capture time: every
+// reallocation below drops it, so a replay never writes to a freed buffer.
+void drop_graph(rtbvh_ctx* c) {
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->graph_exec = nullptr;
+    c->graph = nullptr;
+}
+
 rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     if (T <= c->cap_T && c->d_codes) return RTBVH_OK;
+    drop_graph(c);
     const size_t n = T, ni = T > 1 ? T - 1 : 1;
     HIPC(c, dalloc(c->d_codes, n));
     HIPC(c, dalloc(c->d_ids, n));
@@ -179,6 +189,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
 
 rtbvh_status ensure_trace_capacity(rtbvh_ctx* c, size_t P) {
     if (P <= c->cap_P && c->d_color) return RTBVH_OK;
+    drop_graph(c);
     HIPC(c, dalloc(c->d_color, P));
     HIPC(c, dalloc(c->d_intensity, P));
     HIPC(c, dalloc(c->d_q[0], P));
@@ -209,7 +220,8 @@ uint32_t trace_split(const rtbvh_ctx* c, size_t pixels) {
 rtbvh_status ensure_split_capacity(rtbvh_ctx* c, uint32_t nsplit, size_t rays) {
     if (nsplit < 2) return RTBVH_OK;
     const bool grow = rays > c->cap_split;
-    if (grow) {   // every chain's queues hold cap_split rays: drop the smaller ones
+    if (grow) {
+        drop_graph(c);   // every chain's queues hold cap_split rays: drop the smaller ones
         for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // (after any frame in flight on them)
             if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
         c->cap_split = rays;
@@ -290,7 +302,8 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     const uint32_t lim = c->cfg.stack_limit;
     a.stack_limit = lim && lim < (uint32_t)STACK_SIZE ? (int)lim : STACK_SIZE;
     a.stack_limit4 = lim && lim < (uint32_t)STACK4 ? (int)lim : STACK4;
-    a.limited = lim != 0 && lim < (uint32_t)STACK4;
+    a.stack_limit4b = lim && lim < (uint32_t)STACK4B ? (int)lim : STACK4B;
+    a.limited = lim != 0 && lim < (uint32_t)STACK4B;
     a.acyclic = c->built_clz64;
     return a;
 }
@@ -375,13 +388,6 @@ const Rccl& rccl() {
     return lib;
 }
 
-void drop_graph(rtbvh_ctx* c) {
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-    if (c->graph) (void)hipGraphDestroy(c->graph);
-    c->graph_exec = nullptr;
-    c->graph = nullptr;
-}
-
 rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(c, RTBVH_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -417,6 +423,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t tblocks = P < (1u << 22) ? 1024 : RTBVH_BOUNCE_GRID;
     if (records) {
         if (c->cap_rec < P) {
+            drop_graph(c);
             HIPC(c, dalloc(c->d_refl_rec, 14 * (size_t)P));
             HIPC(c, dalloc(c->d_refr_rec, 14 * (size_t)P));
             c->cap_rec = P;
@@ -1016,7 +1023,8 @@ rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
         c->ovf_seen = ovf;
         return fail(c, RTBVH_ERR_STACK_OVERFLOW,
                     "traversal stack overflow: " + std::to_string(n) +
-                        " ray(s) ended early with the best hit found so far (stack limit " +
+                        " event(s) -- a per-lane walk's ray ended early, or a packet walk skipped a subtree "
+                        "for the rays that hit it; each keeps the best hit found so far (stack limit " +
                         std::to_string(c->cfg.stack_limit ? c->cfg.stack_limit : (uint32_t)STACK_SIZE) +
                         " entries; the reference's 32-entry stack is unchecked, RayTraceTraversal.hlsl:9,115)");
     }

@@ -136,6 +136,26 @@ struct RangeLimit {   // jdmaster.c prepare_range_limit_table, the post-IDCT par
     }
     uint8_t clamp(int x) const { return simple[x < -256 ? 0 : x > 511 ? 767 : x + 256]; }
 };
+// jdcolor.c build_ycc_rgb_table: built once, thread-safe (a function-local static)
+struct YccTables {
+    int cr_r[256], cb_b[256];
+    int32_t cr_g[256], cb_g[256];
+    YccTables() {
+        const int32_t F1402 = (int32_t)(1.40200 * 65536 + 0.5), F1772 = (int32_t)(1.77200 * 65536 + 0.5);
+        const int32_t F0714 = (int32_t)(0.71414 * 65536 + 0.5), F0344 = (int32_t)(0.34414 * 65536 + 0.5);
+        for (int i = 0, x = -128; i < 256; i++, x++) {
+            cr_r[i] = (int)((F1402 * x + 32768) >> 16);
+            cb_b[i] = (int)((F1772 * x + 32768) >> 16);
+            cr_g[i] = -F0714 * x;
+            cb_g[i] = -F0344 * x + 32768;
+        }
+    }
+};
+const YccTables& ycc_tables() {
+    static const YccTables t;
+    return t;
+}
+
 const RangeLimit& range_limit() {
     static const RangeLimit r;
     return r;
@@ -390,7 +410,8 @@ bool decode(const uint8_t* data, size_t size, uint32_t& W_out, uint32_t& H_out, 
                 memset(blk, 0, sizeof(blk));
                 int t;
                 if (!decode_huff(bits, hdc[c.td], t) || t > 11) return false;
-                c.pred += extend(bits.get(t), t);
+                c.pred += extend(bits.get(t), t);   // |diff| < 2^11 per block
+                if (c.pred < -32768 || c.pred > 32767) return false;   // no 16-bit DC: malformed
                 blk[0] = (int16_t)c.pred;
                 for (int k = 1; k < 64;) {
                     int rs;
@@ -463,20 +484,7 @@ bool decode(const uint8_t* data, size_t size, uint32_t& W_out, uint32_t& H_out, 
         upsample(c, dw, dh, hs, vs, W, H, full[k]);
     }
     // jdcolor.c ycc_rgb_convert (SCALEBITS 16); grayscale: R = G = B = Y
-    static int cr_r[256], cb_b[256];
-    static int32_t cr_g[256], cb_g[256];
-    static bool tables = false;
-    if (!tables) {
-        const int32_t F1402 = (int32_t)(1.40200 * 65536 + 0.5), F1772 = (int32_t)(1.77200 * 65536 + 0.5);
-        const int32_t F0714 = (int32_t)(0.71414 * 65536 + 0.5), F0344 = (int32_t)(0.34414 * 65536 + 0.5);
-        for (int i = 0, x = -128; i < 256; i++, x++) {
-            cr_r[i] = (int)((F1402 * x + 32768) >> 16);
-            cb_b[i] = (int)((F1772 * x + 32768) >> 16);
-            cr_g[i] = -F0714 * x;
-            cb_g[i] = -F0344 * x + 32768;
-        }
-        tables = true;
-    }
+    const YccTables& yt = ycc_tables();
     const RangeLimit& rl = range_limit();
     rgba.assign((size_t)W * H * 4, 255);
     for (size_t i = 0; i < (size_t)W * H; i++) {
@@ -487,9 +495,9 @@ bool decode(const uint8_t* data, size_t size, uint32_t& W_out, uint32_t& H_out, 
             continue;
         }
         const int cb = full[1][i], cr = full[2][i];
-        o[0] = rl.clamp(y + cr_r[cr]);
-        o[1] = rl.clamp(y + (int)((cb_g[cb] + cr_g[cr]) >> 16));
-        o[2] = rl.clamp(y + cb_b[cb]);
+        o[0] = rl.clamp(y + yt.cr_r[cr]);
+        o[1] = rl.clamp(y + (int)((yt.cb_g[cb] + yt.cr_g[cr]) >> 16));
+        o[2] = rl.clamp(y + yt.cb_b[cb]);
     }
     W_out = (uint32_t)W;
     H_out = (uint32_t)H;

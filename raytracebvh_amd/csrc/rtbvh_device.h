@@ -37,7 +37,11 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t INVALID = 0xFFFFFFFFu;
 constexpr uint32_t ABSENT_MINZ = 0x7FC00000u;   // min.z (a quiet NaN) of a pseudo-record's absent child
 constexpr int STACK_SIZE = 66;   // binary walks: >= 64 levels of a clz64 Karras tree + sentinel
-constexpr int STACK4 = 100;      // 4-wide walks: <= 3 pushes per level of a <= 32-level 4-wide tree
+constexpr int STACK4 = 100;      // 4-wide primary packets (record pairs: a step descends two levels, pushes
+                                 //   <= 3) on a <= 64-level clz64 tree: <= 3 * 32 + sentinel
+constexpr int STACK4B = 3 * 64;  // 4-wide bounce walk on QNodes: the greedy collapse (build.hip) may leave
+                                 //   entries one and three levels below the node, so a step can descend one
+                                 //   level and push 3: <= 3 per level of <= 64 internal levels
 // float4 per clip-space triangle in tclip: 64-B aligned records, so the refit's gather in sorted
 // order reads one line per triangle (48-B records straddled lines: 1.47 read requests per
 // triangle); C4 A/B: Morton +0.03 ms, refit -0.035 ms, build traffic -0.4 GB

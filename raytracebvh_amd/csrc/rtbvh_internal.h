@@ -106,7 +106,8 @@ struct TraceArgs {
     float* intensity;         // optional, same indexing as color
     unsigned long long* counters;   // [64] per trace: see flush_counts (trace.hip) and rtbvh_get_stats
     unsigned long long* overflow;   // stack overflows / guard trips, accumulated over every trace (never reset)
-    int stack_limit, stack_limit4;  // stack entries the binary / 4-wide walks may use (<= STACK_SIZE / STACK4)
+    int stack_limit, stack_limit4;  // stack entries the binary / 4-wide primary walks may use (<= STACK_SIZE / STACK4)
+    int stack_limit4b;              // ... and the 4-wide bounce walk (<= STACK4B)
     bool limited;                   // a limit below a capacity: the kernels read the limits (else constants)
     bool acyclic;                   // built with the clz64 delta (a radix tree): the 4-wide primary walk
                                     //   needs no walk-length guard

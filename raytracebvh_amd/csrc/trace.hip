@@ -201,7 +201,7 @@ __device__ __forceinline__ bool traverse_packet(const Inner* __restrict__ inner,
     if (mask == 0) return false;
     uint32_t guard = 2 * T + 2;
     while (true) {
-        if (--guard == 0) { c.overflow++; break; }
+        if (--guard == 0) { c.overflow += valid; break; }   // the wave's rays in the frame end early
         bool pop = false;
         if (node & LEAF_BIT) {
             const uint32_t j = node & ~LEAF_BIT;
@@ -482,7 +482,9 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
                     sp += npush;
                     continue;
                 }
-                c.overflow++;
+                // the step's children are skipped: count the rays that hit one of them (once per lane,
+                // not 64 per wave event)
+                c.overflow += (uint32_t)(((m0 | m1 | m2 | m3) >> lane) & 1u);
             }
         }
         --sp;
@@ -493,7 +495,7 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
             mask = ((uint64_t)hi << 32) | lo;
         }
     } while (node != INVALID && (!GUARD || --guard != 0));
-    if (GUARD && guard == 0) c.overflow++;
+    if (GUARD && guard == 0) c.overflow += valid;
     const bool hit = key != NO_HIT;
     if (hit) { best = __uint_as_float((uint32_t)(key >> 32)); best_leaf = (uint32_t)key; }
     return hit;
@@ -921,7 +923,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           unsigned long long* __restrict__ counters,
                                                           unsigned long long* __restrict__ overflow, int stack_limit) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
-    const int limit = LIM ? stack_limit : WIDE ? STACK4 : STACK_SIZE;
+    const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
     const uint32_t n = *qin_count;
     if (n == 0) return;
     const uint32_t lane = lane_id();
@@ -937,7 +939,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     uint32_t stack[WIDE ? 1 : STACK_SIZE - SB];   // entries [SB, STACK_SIZE)
     __shared__ uint32_t s_wid[WIDE ? SW : 1][BLOCK];
     __shared__ uint16_t s_wt[WIDE ? SW : 1][BLOCK];
-    uint2 wstack[WIDE ? STACK4 - SW : 1];        // entries [SW, STACK4)
+    uint2 wstack[WIDE ? STACK4B - SW : 1];       // entries [SW, STACK4B)
     const uint32_t tid = threadIdx.x;
     auto spush = [&](uint32_t v) {
         if (sp < SB) s_stk[sp][tid] = v;
@@ -1354,7 +1356,7 @@ void launch_primary_c(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count,
 template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           float2* hitrec, uint32_t* next, uint32_t blocks, hipStream_t s) {
-    const int lim = MODE == 2 ? a.stack_limit4 : a.stack_limit;
+    const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
 #define RTBVH_BT(L, G)                                                                                              \
     hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
                        a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)

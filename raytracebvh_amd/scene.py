@@ -77,15 +77,43 @@ def _from_native(handle) -> Scene:
 def load_texture(path: str) -> np.ndarray:
     """Image::loadImage (Image.cpp:35-61): RGBA8 rows in the order DevIL hands them over
     without IL_ORIGIN_SET -- the file's own order (BMP: bottom row first; JPEG: top row
-    first), decoded natively by librtbvh (rtbvh_texture_load: BMP or baseline JPEG)."""
+    first), decoded natively by librtbvh (rtbvh_texture_load: BMP or baseline JPEG).
+    Formats the native decoders do not read (PNG, TGA, progressive JPEG, ...), which DevIL
+    decodes, fall back to PIL as host-side image I/O, in the same file-order convention."""
     L = _L.lib()
     t = _L.Texture()
-    _L.check(L.rtbvh_texture_load(os.fsencode(path), ctypes.byref(t)))
+    st = L.rtbvh_texture_load(os.fsencode(path), ctypes.byref(t))
+    if st == _L.ERR_IO and os.path.isfile(path):
+        return _load_texture_pil(path)
+    _L.check(st)
     try:
         return np.ctypeslib.as_array(ctypes.cast(t.rgba8, ctypes.POINTER(ctypes.c_uint8)),
                                      shape=(t.height, t.width, 4)).copy()
     finally:
         L.rtbvh_texture_free(ctypes.byref(t))
+
+
+def _load_texture_pil(path: str) -> np.ndarray:
+    """PIL decode of a texture the native decoders reject; rows in file order as DevIL
+    hands them over: a TGA stored bottom-up (image descriptor bit 5 clear) bottom row
+    first, every other format top row first.  Raises RtbvhError(ERR_IO) if PIL cannot
+    read the file either."""
+    try:
+        from PIL import Image
+    except ImportError as e:   # no host image library: the native decoders' error stands
+        raise _L.RtbvhError(_L.ERR_IO, f"{path}: not BMP/baseline JPEG and PIL is unavailable") from e
+    try:
+        with Image.open(path) as im:
+            fmt = im.format
+            rgba = np.asarray(im.convert("RGBA"), dtype=np.uint8).copy()
+    except (OSError, ValueError) as e:
+        raise _L.RtbvhError(_L.ERR_IO, f"{path}: {e}") from e
+    if fmt == "TGA":
+        with open(path, "rb") as f:
+            hdr = f.read(18)
+        if len(hdr) == 18 and not (hdr[17] & 0x20):   # bottom-left origin: DevIL keeps file order
+            rgba = rgba[::-1].copy()
+    return rgba
 
 
 def decode_jpeg(data: bytes) -> np.ndarray:

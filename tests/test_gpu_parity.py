@@ -813,6 +813,33 @@ def test_graph_replay_after_band_traces_and_other_sizes():
         np.testing.assert_array_equal(g.read_framebuffer(), want)
 
 
+def test_graph_replay_after_a_larger_trace_reallocates():
+    """compute_bvh(320x240) -> trace(640x480) -> compute_bvh(320x240): the larger trace
+    reallocates the trace buffers the captured graph points at, so the context drops the graph
+    and captures again; the replayed frame is the plain context's and read_framebuffer returns
+    it (a stale graph wrote to freed buffers)."""
+    d = load_scene_fixture("Test")
+    s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    W, H = 320, 240
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0) as plain, rt.Context(device=0, flags=rt.FLAG_GRAPH) as g:
+        for c in (plain, g):
+            c.set_scene(s)
+            c.set_camera(wvp, wv)
+        plain.compute_bvh(W, H, 1)
+        want = plain.read_framebuffer()
+        g.compute_bvh(W, H, 1)
+        g.compute_bvh(W, H, 1)
+        assert g.stats()["graph_captures"] == 1
+        g.trace(640, 480, 1)        # grows every trace buffer
+        plain.trace(640, 480, 1)
+        np.testing.assert_array_equal(g.read_framebuffer(), plain.read_framebuffer())
+        for _ in range(2):
+            g.compute_bvh(W, H, 1)
+            np.testing.assert_array_equal(g.read_framebuffer(), want)
+        assert g.stats()["graph_captures"] == 2
+
+
 @pytest.mark.parametrize("mode", ["reference", "nearest", "packet", "nearest+packet", "nearest+packet+refill",
                                   "nearest+packet+wide", "refill+sort"])
 def test_stack_limit_reports_overflow(mode):

@@ -271,7 +271,7 @@ def test_jpeg_decoder_grayscale_and_rejections():
 
 def test_texture_load_by_magic(golden_dir, tmp_path):
     """rtbvh_texture_load: BMP (Map__1_Composite.bmp, bottom row first as DevIL keeps it) or JPEG
-    by content; anything else is an I/O error."""
+    by content; anything else is an I/O error (a truncated PNG also fails the PIL fallback)."""
     from raytracebvh_amd.scene import load_texture
     bmp = os.path.join(golden_dir, "textures", "Map__1_Composite.bmp")
     got = load_texture(bmp)
@@ -279,4 +279,28 @@ def test_texture_load_by_magic(golden_dir, tmp_path):
     (tmp_path / "x.png").write_bytes(b"\x89PNG\r\n\x1a\n" + b"\0" * 64)
     with pytest.raises(rt.RtbvhError) as e:
         load_texture(str(tmp_path / "x.png"))
+    assert e.value.status == _lib.ERR_IO
+
+
+def test_texture_load_falls_back_to_pil(tmp_path):
+    """Textures the native decoders do not read (PNG, TGA, progressive JPEG) -- which DevIL
+    decodes for Image::loadImage (Image.cpp:35-61) -- load through PIL in DevIL's file-order
+    convention: PNG and JPEG top row first, a bottom-up TGA bottom row first."""
+    from PIL import Image
+
+    from raytracebvh_amd.scene import load_texture
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 256, (13, 17, 4), dtype=np.uint8)
+    Image.fromarray(a, "RGBA").save(tmp_path / "t.png")
+    np.testing.assert_array_equal(load_texture(str(tmp_path / "t.png")), a)
+    Image.fromarray(a, "RGBA").save(tmp_path / "t.tga")
+    assert not (open(tmp_path / "t.tga", "rb").read(18)[17] & 0x20)   # stored bottom-up
+    np.testing.assert_array_equal(load_texture(str(tmp_path / "t.tga")), a[::-1])
+    Image.fromarray(a[:, :, :3], "RGB").save(tmp_path / "p.jpg", progressive=True, quality=90)
+    with Image.open(tmp_path / "p.jpg") as im:
+        want = np.asarray(im.convert("RGBA"))
+    np.testing.assert_array_equal(load_texture(str(tmp_path / "p.jpg")), want)
+    (tmp_path / "junk.bin").write_bytes(b"not an image")
+    with pytest.raises(rt.RtbvhError) as e:
+        load_texture(str(tmp_path / "junk.bin"))
     assert e.value.status == _lib.ERR_IO
