@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RTBVH_ABI_VERSION 3
+#define RTBVH_ABI_VERSION 4
 
 typedef enum {
     RTBVH_OK = 0,
@@ -127,12 +127,16 @@ enum {
     RTBVH_FLAG_WIDE_BVH = 1u << 7,        /* trace: walk the node records 4-wide (a node's four grandchild
                                              boxes share one 128-B line), keeping the lexicographic
                                              (t, leaf) minimum as NEAREST_FIRST does */
-    RTBVH_FLAG_AUTO_WALK = 1u << 8,       /* choose the walks by scene size, ignoring the four walk flags above:
-                                             up to 65536 triangles the reference-order kernels (exact by
-                                             construction; the fastest on the reference's own meshes), above
-                                             that NEAREST_FIRST | PACKET_PRIMARY | REFILL_BOUNCE | WIDE_BVH
-                                             (identical frames whenever containment holds: check a scene
-                                             once with rtbvh_verify_walk) */
+    RTBVH_FLAG_AUTO_WALK = 1u << 8,       /* choose the walks, ignoring the four walk flags above, and return
+                                             the reference-order frame always: up to 65536 triangles the
+                                             reference-order kernels (exact by construction; the fastest on the
+                                             reference's own meshes); above that, per frame key (scene + camera
+                                             of the build, camera, size, bounces, band), the first frame is
+                                             traced in the reference order into the outputs AND with
+                                             NEAREST_FIRST | PACKET_PRIMARY | REFILL_BOUNCE | WIDE_BVH into
+                                             scratch, compared on the device; the key's later frames take the
+                                             fast walks only if nothing differed (stats walk_state /
+                                             walk_checks / walk_fallbacks) */
     RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
                                               build instead of the one-workgroup build (same output) */
     /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n
@@ -181,11 +185,18 @@ typedef struct {
      * and a histogram, [k] = rays of floor(log2(iterations)) == k */
     uint64_t trav_max_steps, trav_steps_log2[32];
     uint64_t graph_captures;   /* RTBVH_FLAG_GRAPH: frames captured so far (a replay captures nothing) */
-    uint32_t walk_flags;       /* the walk flags the next trace uses (after RTBVH_FLAG_AUTO_WALK) */
-    uint32_t reserved;
+    uint32_t walk_flags;       /* the walk flags the last trace's frame was traced with (RTBVH_FLAG_AUTO_WALK:
+                                  the reference order, or the four walk flags once verified) */
+    uint32_t walk_state;       /* RTBVH_FLAG_AUTO_WALK, last trace: 0 the reference order by size (<= 65536
+                                  triangles) or no AUTO; 1 the frame key was being checked (the frame is the
+                                  reference order's); 2 fast walks, verified for this key; 3 reference order
+                                  because the check found the fast walks' frame differing (a fallback) */
     /* RTBVH_FLAG_COUNT_VISITS, wave-packet primary walks: wave steps (one record fetch for the
      * wave each) at internal nodes [0] and at leaves [1] */
     uint64_t packet_steps[2];
+    /* RTBVH_FLAG_AUTO_WALK: device checks run (one per new frame key) and those that found the
+     * fast walks' frame differing from the reference order's (the key stays on the reference order) */
+    uint64_t walk_checks, walk_fallbacks;
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 

@@ -75,8 +75,9 @@ class Stats(ctypes.Structure):
                 ("ms_stage", ctypes.c_float * 8), ("trav_wave_steps", ctypes.c_uint64),
                 ("trav_mixed_steps", ctypes.c_uint64), ("trav_active_lanes", ctypes.c_uint64),
                 ("trav_max_steps", ctypes.c_uint64), ("trav_steps_log2", ctypes.c_uint64 * 32),
-                ("graph_captures", ctypes.c_uint64), ("walk_flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
-                ("packet_steps", ctypes.c_uint64 * 2)]
+                ("graph_captures", ctypes.c_uint64), ("walk_flags", ctypes.c_uint32),
+                ("walk_state", ctypes.c_uint32), ("packet_steps", ctypes.c_uint64 * 2),
+                ("walk_checks", ctypes.c_uint64), ("walk_fallbacks", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         d = {}

@@ -117,6 +117,28 @@ struct rtbvh_ctx {
         uint32_t W, H, bounces, nsplit;
         size_t rec_P;
     } graph_state{};
+    // RTBVH_FLAG_AUTO_WALK above AUTO_WALK_MAX_TRIS: a frame key (scene and camera of the build,
+    // camera, size, bounces, band) takes the fast walks only after one of its frames was traced
+    // both ways and compared on the device (enqueue_trace); until then, and for good after a
+    // mismatch, it takes the reference-order walks (findCollision's DFS)
+    uint64_t scene_gen = 0, cam_gen = 0;              // bumped by set_scene / a changed camera
+    uint64_t built_scene_gen = 0, built_cam_gen = 0;  // ... as of the last build
+    static constexpr int VKEYS = 8;
+    struct WalkKey { uint64_t w[4]; };
+    WalkKey vkeys[VKEYS] = {};                        // decided keys, ring
+    bool vfast[VKEYS] = {};                           //   true: fast walks verified; false: reference order
+    uint32_t nvkeys = 0;
+    bool vpending = false;                            // a check in flight (one at a time)
+    WalkKey vpend_key{};
+    hipEvent_t ev_verify = nullptr;
+    unsigned long long* d_vdiff = nullptr;            // differing pixels + intensities of the check
+    unsigned long long* h_vdiff = nullptr;            //   (pinned copy)
+    float4* d_vcolor = nullptr;                       // the fast walks' frame of a check
+    float* d_vinten = nullptr;
+    size_t cap_v = 0;
+    uint64_t walk_checks = 0, walk_fallbacks = 0;
+    uint32_t last_walk = 0;                           // walk flags of the last trace
+    uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
 };
 
 namespace {
@@ -310,18 +332,14 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
 
 // The walks of a trace (include/rtbvh.h RTBVH_FLAG_*).  RTBVH_FLAG_AUTO_WALK: the
 // reference-order kernels (the exact findCollision DFS) up to AUTO_WALK_MAX_TRIS triangles,
-// where they are the fastest (C2/C3: Image_Test.obj, Test.obj), and the 4-wide nearest-first
-// walks above (C5: 2.4x the reference order).
+// where they are the fastest (C2/C3: Image_Test.obj, Test.obj); above, the 4-wide
+// nearest-first walks (C5: 3.4x the reference order) for a frame key once a frame of that key
+// traced both ways compared equal on the device (enqueue_trace), the reference order otherwise.
 constexpr uint32_t AUTO_WALK_MAX_TRIS = 1u << 16;
 constexpr uint32_t WALK_FLAGS =
     RTBVH_FLAG_NEAREST_FIRST | RTBVH_FLAG_PACKET_PRIMARY | RTBVH_FLAG_REFILL_BOUNCE | RTBVH_FLAG_WIDE_BVH;
-uint32_t effective_flags(const rtbvh_ctx* c) {
-    uint32_t f = c->cfg.flags;
-    if (f & RTBVH_FLAG_AUTO_WALK) {
-        f &= ~WALK_FLAGS;
-        if (c->T > AUTO_WALK_MAX_TRIS) f |= WALK_FLAGS;
-    }
-    return f;
+bool auto_checked(const rtbvh_ctx* c) {
+    return (c->cfg.flags & RTBVH_FLAG_AUTO_WALK) && c->T > AUTO_WALK_MAX_TRIS;
 }
 struct Walks {
     PrimaryKind primary;
@@ -394,8 +412,10 @@ rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
     return RTBVH_OK;
 }
 
-rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
-                           float4* color, float* inten, hipStream_t s, uint32_t slot = 0) {
+// The kernels of one trace with the walks of `flags` (timed: record the stage events when
+// RTBVH_FLAG_TIMING asks for them).
+rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
+                           float4* color, float* inten, hipStream_t s, uint32_t slot, uint32_t flags, bool timed) {
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
     if (W == 0 || H == 0 || nranks == 0 || rank >= nranks || bounces > 14)
         return fail(c, RTBVH_ERR_INVALID_ARG, "bad trace dimensions");
@@ -403,12 +423,11 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (st) return st;
     if (!color) color = c->d_color;
     const bool count = (c->cfg.flags & RTBVH_FLAG_COUNT_VISITS) != 0;
-    const bool timing = (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream && !c->capturing;
+    const bool timing = timed && (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream && !c->capturing;
     TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
     a.counters = c->d_counters + 64 * slot;
     HIPC(c, hipMemsetAsync(a.counters, 0, 64 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
-    const uint32_t flags = effective_flags(c);
     const Walks wk = choose_walks(flags);
     const bool sort = wk.sort, refill = wk.refill;
     const bool records = (flags & RTBVH_FLAG_REFRACT_RECORDS) != 0;
@@ -503,7 +522,102 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     c->traced = true;
     c->frame_here = color == c->d_color && nranks == 1;
     c->intensity_here = c->frame_here && inten != nullptr;
+    c->last_walk = flags & WALK_FLAGS;
     return check_launch(c, "trace kernels");
+}
+
+// ---- RTBVH_FLAG_AUTO_WALK: the fast walks only where a device check found them exact --------
+// The 4-wide nearest-first walks return the lexicographic (t, leaf) minimum over the leaves they
+// reach, findCollision (RayTraceTraversal.hlsl:106-193) the first strict minimum over the leaves
+// IT reaches; the two agree whenever the hit lies inside every box on its root path under the
+// same rounding ("containment").  When containment fails the walks can differ
+// (tests/containment.py builds such a scene: two coplanar triangles whose Moller-Trumbore t
+// rounds below their slab entry).  No cheap per-ray certificate exists -- the hit a walk misses
+// lies in a subtree it pruned, unvisited -- so the check is per frame: the first frame of a key
+// is traced with the fast walks into scratch AND with the reference order into the outputs, and
+// the two are compared on the device.  The outputs are always the reference frame; the key takes
+// the fast walks from its next frame on only if nothing differed.  The build is deterministic, so
+// frames of one key are identical.
+rtbvh_ctx::WalkKey walk_key(const rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank,
+                            uint32_t nranks) {
+    rtbvh_ctx::WalkKey k;
+    k.w[0] = c->built_scene_gen << 32 | (c->built_cam_gen & 0xFFFFFFFFu);
+    k.w[1] = c->cam_gen;
+    k.w[2] = (uint64_t)W | (uint64_t)H << 32;
+    k.w[3] = (uint64_t)bounces | (uint64_t)rank << 8 | (uint64_t)nranks << 32;
+    return k;
+}
+int find_walk_key(const rtbvh_ctx* c, const rtbvh_ctx::WalkKey& k) {
+    const uint32_t n = c->nvkeys < (uint32_t)rtbvh_ctx::VKEYS ? c->nvkeys : rtbvh_ctx::VKEYS;
+    for (uint32_t i = 0; i < n; i++)
+        if (memcmp(&c->vkeys[i], &k, sizeof(k)) == 0) return (int)i;
+    return -1;
+}
+// Take the result of the check in flight once its event has completed (wait: block on it).
+void resolve_walk_check(rtbvh_ctx* c, bool wait) {
+    if (!c->vpending) return;
+    const hipError_t e = wait ? hipEventSynchronize(c->ev_verify) : hipEventQuery(c->ev_verify);
+    if (e == hipErrorNotReady) return;
+    c->vpending = false;
+    if (e != hipSuccess) return;   // undecided: the key is checked again
+    const bool fast = *c->h_vdiff == 0;
+    if (!fast) c->walk_fallbacks++;
+    const uint32_t i = c->nvkeys++ % rtbvh_ctx::VKEYS;
+    c->vkeys[i] = c->vpend_key;
+    c->vfast[i] = fast;
+}
+
+rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
+                           float4* color, float* inten, hipStream_t s, uint32_t slot = 0) {
+    const uint32_t f = c->cfg.flags;
+    if (!(f & RTBVH_FLAG_AUTO_WALK)) {
+        c->last_walk_state = 0;
+        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, f, true);
+    }
+    const uint32_t ref = f & ~WALK_FLAGS, fast = ref | WALK_FLAGS;
+    if (!auto_checked(c)) {   // small scenes: the reference order, the fastest there
+        c->last_walk_state = 0;
+        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, ref, true);
+    }
+    if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
+    resolve_walk_check(c, false);
+    const rtbvh_ctx::WalkKey key = walk_key(c, W, H, bounces, rank, nranks);
+    const int known = find_walk_key(c, key);
+    if (known >= 0) {
+        const bool fw = c->vfast[known];
+        c->last_walk_state = fw ? 2 : 3;
+        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, fw ? fast : ref, true);
+    }
+    // undecided: the reference order while another check is in flight, inside a graph capture
+    // (compute_graph decides the key with its plain frame first) and for the RayPresent records
+    if (c->vpending || c->capturing || (f & RTBVH_FLAG_REFRACT_RECORDS)) {
+        c->last_walk_state = 1;
+        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, ref, true);
+    }
+    if (!color) color = c->d_color;
+    const size_t n = (size_t)W * rtbvh_band_rows(H, rank, nranks);
+    if (c->cap_v < n) {
+        HIPC(c, dalloc(c->d_vcolor, n));
+        HIPC(c, dalloc(c->d_vinten, n));
+        c->cap_v = n;
+    }
+    if (!c->d_vdiff) HIPC(c, dalloc(c->d_vdiff, 1));
+    if (!c->h_vdiff) HIPC(c, hipHostMalloc((void**)&c->h_vdiff, sizeof(unsigned long long), hipHostMallocDefault));
+    if (!c->ev_verify) HIPC(c, hipEventCreateWithFlags(&c->ev_verify, hipEventDisableTiming));
+    rtbvh_status st =
+        enqueue_walks(c, W, H, bounces, rank, nranks, c->d_vcolor, inten ? c->d_vinten : nullptr, s, slot, fast, false);
+    if (!st) st = enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, ref, true);
+    if (st) return st;
+    HIPC(c, hipMemsetAsync(c->d_vdiff, 0, sizeof(unsigned long long), s));
+    launch_count_diff(c->d_vcolor, color, n, c->d_vdiff, s);
+    if (inten) launch_count_diff32(c->d_vinten, inten, n, c->d_vdiff, s);
+    HIPC(c, hipMemcpyAsync(c->h_vdiff, c->d_vdiff, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPC(c, hipEventRecord(c->ev_verify, s));
+    c->vpending = true;
+    c->vpend_key = key;
+    c->walk_checks++;
+    c->last_walk_state = 1;
+    return check_launch(c, "walk check");
 }
 
 }  // namespace
@@ -609,6 +723,9 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_texels); dfree(c->d_texinfo); dfree(c->d_srgb);
     dfree(c->d_counters);
     dfree(c->d_ovf);
+    dfree(c->d_vcolor); dfree(c->d_vinten); dfree(c->d_vdiff);
+    if (c->h_vdiff) (void)hipHostFree(c->h_vdiff);
+    if (c->ev_verify) (void)hipEventDestroy(c->ev_verify);
     if (c->h_ovf) (void)hipHostFree(c->h_ovf);
     for (auto& row : c->evb)
         for (auto& e : row)
@@ -698,6 +815,7 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
     }
     c->have_scene = true;
     c->built = false;
+    c->scene_gen++;
     return RTBVH_OK;
 }
 
@@ -711,6 +829,7 @@ rtbvh_status rtbvh_set_camera(rtbvh_ctx* c, const float wvp[16], const float wv[
     memcpy(c->wvp, wvp, sizeof(c->wvp));
     memcpy(c->wv, wv, sizeof(c->wv));
     c->have_camera = true;
+    c->cam_gen++;
     drop_graph(c);
     return RTBVH_OK;
 }
@@ -741,6 +860,8 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
         c->built = true;
         c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
+        c->built_scene_gen = c->scene_gen;
+        c->built_cam_gen = c->cam_gen;
         return check_launch(c, "build kernel");
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
@@ -759,6 +880,8 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
     c->built = true;
     c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
+    c->built_scene_gen = c->scene_gen;
+    c->built_cam_gen = c->cam_gen;
     return check_launch(c, "build kernels");
 }
 
@@ -864,12 +987,13 @@ rtbvh_status rtbvh_verify_walk(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
     unsigned long long* d_diff = nullptr;
     HIPC(c, hipMallocAsync((void**)&ref, n * sizeof(float4) + 256, c->stream));
     d_diff = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ref) + n * sizeof(float4));
-    const uint32_t saved = c->cfg.flags;
-    c->cfg.flags = saved & ~(WALK_FLAGS | RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_REFRACT_RECORDS);
-    st = enqueue_trace(c, W, H, bounces, 0, 1, ref, nullptr, c->stream);
-    c->cfg.flags = saved & ~RTBVH_FLAG_REFRACT_RECORDS;
-    if (!st) st = enqueue_trace(c, W, H, bounces, 0, 1, c->d_color, c->d_intensity, c->stream);
-    c->cfg.flags = saved;
+    // the reference order, then the walks the context would take for a key it has verified (AUTO:
+    // the fast walks above AUTO_WALK_MAX_TRIS), without the ray records
+    const uint32_t f = c->cfg.flags & ~RTBVH_FLAG_REFRACT_RECORDS;
+    const uint32_t refw = f & ~WALK_FLAGS;
+    const uint32_t mine = (f & RTBVH_FLAG_AUTO_WALK) ? (auto_checked(c) ? refw | WALK_FLAGS : refw) : f;
+    st = enqueue_walks(c, W, H, bounces, 0, 1, ref, nullptr, c->stream, 0, refw, true);
+    if (!st) st = enqueue_walks(c, W, H, bounces, 0, 1, c->d_color, c->d_intensity, c->stream, 0, mine, true);
     unsigned long long diff = 0;
     if (!st) {
         hipError_t e = hipMemsetAsync(d_diff, 0, sizeof(unsigned long long), c->stream);
@@ -1014,6 +1138,7 @@ rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
     HIPC(c, hipStreamSynchronize(c->stream));
     for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // and the frames in flight on caller streams
         if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
+    resolve_walk_check(c, true);
     // each trace ends by copying the never-reset overflow word into its slot's pinned word
     unsigned long long ovf = c->ovf_seen;
     for (uint32_t k = 0; k < rtbvh_ctx::MAXSPLIT; k++)
@@ -1207,7 +1332,11 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         out->packet_steps[0] = w[0];
         out->packet_steps[1] = w[1];
     }
-    out->walk_flags = effective_flags(c) & WALK_FLAGS;
+    resolve_walk_check(c, true);
+    out->walk_flags = c->last_walk;
+    out->walk_state = c->last_walk_state;
+    out->walk_checks = c->walk_checks;
+    out->walk_fallbacks = c->walk_fallbacks;
     return RTBVH_OK;
 }
 

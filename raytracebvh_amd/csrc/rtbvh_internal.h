@@ -141,6 +141,7 @@ void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qi
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
 // *diff += the number of the n float4 pixels of a and b whose bits differ
 void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long long* diff, hipStream_t s);
+void launch_count_diff32(const float* a, const float* b, size_t n, unsigned long long* diff, hipStream_t s);
 // frame from per-rank compact band buffers (stride_rows rows apart), see rtbvh_assemble_bands
 void launch_assemble(const float4* bands, uint32_t stride_rows, uint32_t W, uint32_t H, uint32_t nranks,
                      float4* frame, hipStream_t s);

@@ -1342,6 +1342,16 @@ __global__ __launch_bounds__(BLOCK) void k_count_diff(const uint4* __restrict__ 
     if (lane_id() == 0 && cnt) atomicAdd(diff, cnt);
 }
 
+// the same for 32-bit words (intensities)
+__global__ __launch_bounds__(BLOCK) void k_count_diff32(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                        size_t n, unsigned long long* __restrict__ diff) {
+    unsigned long long cnt = 0;
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) cnt += a[i] != b[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane_id() == 0 && cnt) atomicAdd(diff, cnt);
+}
+
 template <bool COUNT, int K>
 void launch_primary_t(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool emit, dim3 grid, hipStream_t s) {
     if (a.limited) hipLaunchKernelGGL((k_primary<COUNT, K, true>), grid, dim3(BLOCK), 0, s, a, q, qcount, (int)emit);
@@ -1452,6 +1462,14 @@ void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(k_count_diff, dim3((uint32_t)blocks), dim3(BLOCK), 0, s, reinterpret_cast<const uint4*>(a),
                        reinterpret_cast<const uint4*>(b), n, diff);
+}
+
+void launch_count_diff32(const float* a, const float* b, size_t n, unsigned long long* diff, hipStream_t s) {
+    if (n == 0) return;
+    size_t blocks = (n + BLOCK - 1) / BLOCK;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_count_diff32, dim3((uint32_t)blocks), dim3(BLOCK), 0, s, reinterpret_cast<const uint32_t*>(a),
+                       reinterpret_cast<const uint32_t*>(b), n, diff);
 }
 
 }  // namespace rtbvh
