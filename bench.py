@@ -162,11 +162,30 @@ def cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame):
     gnodes = ctx.read_bvh()
     osc = orc.Scene(scene.vertices, scene.indices, scene.mat_indices, scene.material_blob)
     parity = {"tolerance_rgb": 1e-4}
-    t0 = time.perf_counter()
-    onodes = orc.build(osc, wvp)
+    # the all-cores build (SURVEY 8(d) CPU baseline (2)): the reference-faithful path -- Morton,
+    # the 32 x 1-bit split sort with 256-wide Blelloch blocks, Karras, refit -- with OpenMP over
+    # triangles / groups / nodes / leaves on this process's CPU share (OMP_NUM_THREADS, 16 on the
+    # GPU boxes), over the WHOLE bench scene; its tree is the parity tree
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    n_s = 1_000_000
+    sub = rt.Scene(scene.vertices[: 3 * n_s], scene.indices[: 3 * n_s], scene.mat_indices[:n_s], scene.materials)
+    if "obj" in wl:
+        sub = scene
+    osub = orc.Scene(sub.vertices, sub.indices, sub.mat_indices, sub.material_blob)
+    orc.set_threads(threads)
+    try:
+        orc.build(osub, wvp, sort_mode=0)   # warm-up (thread pool, page faults), untimed
+        t0 = time.perf_counter()
+        onodes = orc.build(osc, wvp, sort_mode=0)
+        dtb = time.perf_counter() - t0
+    finally:
+        orc.set_threads(1)
+    build_all = {"value": scene.num_tris / dtb / 1e6, "unit": "Mtris/s", "cores": threads,
+                 "sample": f"orc_build (Morton + 32 split passes + Karras + refit, OpenMP) on all {scene.num_tris} "
+                           f"triangles of the bench scene, {dtb:.2f} s"}
     parity["tree_nodes"] = int(len(onodes))
     parity["tree_bit_identical"] = bool(all(np.array_equal(gnodes[f], onodes[f]) for f in NODE_FIELDS))
-    parity["tree_oracle_s"] = round(time.perf_counter() - t0, 2)
+    parity["tree_oracle_s"] = round(dtb, 2)
     del gnodes
     step = 8 if W * H > 4_000_000 else 4
     t0 = time.perf_counter()
@@ -178,8 +197,7 @@ def cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame):
                      f"of the same scene ({st['primary']} primary + {st['bounce']} bounce rays, {dt:.1f} s, 1 thread)",
            "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
     # BASELINE.md's all-cores variant: the same code, OpenMP over rows, on this process's CPU
-    # share (OMP_NUM_THREADS, 16 on the GPU boxes), over the WHOLE frame (the parity check)
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    # share, over the WHOLE frame (the parity check)
     orc.set_threads(threads)
     try:
         t0 = time.perf_counter()
@@ -201,16 +219,12 @@ def cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame):
                        "within_tolerance": bool(np.allclose(fb, gpu_frame, atol=1e-4, rtol=0)),
                        "oracle_rays": int(st2["primary"] + st2["bounce"])})
     # build baseline: reference-faithful 32 x 1-bit split sort + Karras + refit on a 1M-triangle sample
-    n_s = 1_000_000
-    sub = rt.Scene(scene.vertices[: 3 * n_s], scene.indices[: 3 * n_s], scene.mat_indices[:n_s], scene.materials)
-    if "obj" in wl:
-        sub = scene
-    osub = orc.Scene(sub.vertices, sub.indices, sub.mat_indices, sub.material_blob)
     t0 = time.perf_counter()
     orc.build(osub, wvp, sort_mode=0)
     dt = time.perf_counter() - t0
     res["build_mtris_s"] = sub.num_tris / dt / 1e6
     res["build_sample"] = f"orc_build (32 split passes + Karras + refit) on {sub.num_tris} triangles, {dt:.2f} s, 1 thread"
+    res["build_all_cores"] = build_all
     return res, parity
 
 
@@ -229,6 +243,9 @@ def main():
                     help="frames in flight per rank (one context + stream each)")
     ap.add_argument("--traversal", default="auto", choices=["auto", "reference"],
                     help="auto: report nearest-first when its frame is identical to the reference order's")
+    ap.add_argument("--root-share", type=int, default=None,
+                    help="rank 0's band share in 1/16 of another rank's (rtbvh_set_band_deal); default: "
+                         "16 at N <= 2, 15 at N <= 4, 13 above (rank 0 also receives and assembles the bands)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -267,6 +284,11 @@ def main():
     stream = torch.cuda.Stream(dev)
     assert stream.cuda_stream != 0
     ctx = rt.Context(device=local, flags=rt.FLAG_TIMING, stream=stream.cuda_stream)
+    # the band deal: rank 0 also receives (RCCL) and assembles every other rank's
+    # bands, about 0.1 ms per C5 frame whatever N (116 MB in at N = 8), against a rank's ~5.3/N ms
+    # of tracing: so it takes 1 - ~2% x N of a share (an estimate until an 8-GPU run measures it)
+    share = args.root_share if args.root_share is not None else (16 if world <= 2 else 15 if world <= 4 else 13)
+    ctx.set_band_deal(share)
     ctx.set_scene(scene)
     wvp, wv = rt.camera_reference(W, H)
     ctx.set_camera(wvp, wv)
@@ -295,7 +317,7 @@ def main():
     from raytracebvh_amd.tiles import BandGather
     # one band buffer per frame in flight (>= 2): frame i's RCCL gather overlaps frame i+1's
     # trace (tiles.py), and frames traced concurrently never share a buffer
-    g = BandGather(W, H, rank, world, device=dev, nbuf=max(2, args.inflight))
+    g = BandGather(W, H, rank, world, device=dev, nbuf=max(2, args.inflight), root_share=share)
     band = g.band
     # torch fills the new buffers on its current stream; the other contexts' streams are
     # not ordered after it (a late fill overwrote traced pixels in a 3-process rehearsal)
@@ -430,27 +452,38 @@ def main():
     recs = {"k_primary": sum(cst["packet_steps"]) or (cst["internal_visits"][0] + cst["leaf_visits"][0]),
             "k_bounce_trav": cst["internal_visits"][1] + cst["leaf_visits"][1],
             "k_bounce_shade": cst["bounce_rays"]}
+    # per kernel: "requested" = this layout's algorithmic bytes (what the walk asks the memory system
+    # for, L2 hits included) per HIP-event second; "frac" = the PMC HBM bytes of the same launch per
+    # second over the HBM peak (the fraction north_star asks for)
     for k, v in kern.items():
-        v["achieved_gbs"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
-        v["frac"] = v["achieved_gbs"] / PEAK_HBM_GBS
+        v["requested_gbs"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
+        v["requested_frac"] = v["requested_gbs"] / PEAK_HBM_GBS
         pm = load_pmc(args.workload, use_name, k)
         v["traffic"] = None
+        v["frac"] = None
         if pm and pm.get("records_per_launch") and recs.get(k):
             v["traffic"] = pm["hbm_bytes_per_launch"] / pm["records_per_launch"] * recs[k]
             v["traffic_gbs"] = v["traffic"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
-            v["traffic_frac"] = v["traffic_gbs"] / PEAK_HBM_GBS
+            v["frac"] = v["traffic_gbs"] / PEAK_HBM_GBS
     kd = kern[dom]
-    roofline = {"bound": "hbm", "achieved": round(kd["achieved_gbs"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(kd["frac"], 4),
+    measured = kd["traffic"] is not None
+    roofline = {"bound": "hbm",
+                "achieved": round(kd["traffic_gbs"] if measured else kd["requested_gbs"], 1),
+                "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(kd["frac"] if measured else kd["requested_frac"], 4),
+                "frac_definition": ("rocprofv3 PMC HBM bytes of the kernel per launch (TCC_EA0 read/write requests "
+                                    "x request size, MI355X_MICROARCH.md) / its HIP-event duration / 8 TB/s"
+                                    if measured else "no PMC profile for this mode: requested bytes / duration / 8 TB/s"),
                 "traffic": kd["traffic"], "kernel": dom, "kernel_ms": round(kd["ms"], 4),
                 "algorithmic_bytes": int(kd["bytes"]),
-                "bytes_model": "layout bytes: 64 B per record fetch (QNode, child-pair record, leaf record; "
-                               "a 4-wide primary step = 2) + per-ray queue/hit/colour bytes (DESIGN.md 7.1)",
+                "requested_gbs": round(kd["requested_gbs"], 1), "requested_frac": round(kd["requested_frac"], 4),
+                "bytes_model": "algorithmic_bytes / requested_*: this layout's bytes, 64 B per record fetch (QNode, "
+                               "child-pair record, leaf record; a 4-wide primary step = 2) + per-ray queue/hit/colour "
+                               "bytes (DESIGN.md 7.1); L2 and the Infinity Cache serve part of them",
                 "traffic_source": f"PMC profiles/pmc_{args.workload}_{use_name}.json (N=1), per record fetch x "
-                                  f"this launch's {recs[dom]} record fetches" if kd["traffic"] else None}
-    if kd["traffic"]:
-        roofline.update({"traffic_gbs": round(kd["traffic_gbs"], 1), "traffic_frac": round(kd["traffic_frac"], 4),
-                         "cache_served_frac": round(max(0.0, 1.0 - kd["traffic"] / kd["bytes"]), 4)})
+                                  f"this launch's {recs[dom]} record fetches" if measured else None}
+    if measured:
+        roofline["cache_served_frac"] = round(max(0.0, 1.0 - kd["traffic"] / kd["bytes"]), 4)
     pm = load_pmc(args.workload, use_name, dom)
     if dom == "k_bounce_trav" and pm and pm.get("counters", {}).get("TCC_HIT_sum") is not None \
             and pm.get("records_per_launch"):
@@ -472,9 +505,13 @@ def main():
                       "algorithmic_bytes": int(S_BUILD_PER_TRI * scene.num_tris), "ms": round(bst["ms_build"], 4),
                       "achieved": round(S_BUILD_PER_TRI * scene.num_tris / (bst["ms_build"] * 1e-3) / 1e9, 1),
                       "peak": PEAK_HBM_GBS, "unit": "GB/s"}
-    build_roofline["frac"] = round(build_roofline["achieved"] / PEAK_HBM_GBS, 4)
+    build_roofline["algorithmic_frac"] = round(build_roofline["achieved"] / PEAK_HBM_GBS, 4)
+    build_roofline["frac"] = None
     if bp:
+        tgbs = bp["hbm_bytes"] / (bst["ms_build"] * 1e-3) / 1e9
         build_roofline.update({"traffic": bp["hbm_bytes"], "traffic_per_kernel_gb": bp["per_kernel_gb"],
+                               "traffic_gbs": round(tgbs, 1), "frac": round(tgbs / PEAK_HBM_GBS, 4),
+                               "frac_definition": "PMC HBM bytes of the build kernels per build / build ms / 8 TB/s",
                                "traffic_vs_algorithmic": round(bp["hbm_bytes"] / build_roofline["algorithmic_bytes"], 3)})
     fb = frame_bytes(rst)
     # SURVEY 8(d)'s whole-frame figure prices the REFERENCE-ORDER walk's visits; a traversal
@@ -546,20 +583,50 @@ def main():
                         c.compute_bvh(wk["W"], wk["H"], wk["bounces"])
                     dt = (time.perf_counter() - t0) / 50
                     q2 = c.stats()
-                with rt.Context(device=local, flags=rt.FLAG_GRAPH) as c:   # the frame as one hipGraph
+                # the drop-in's own configuration: AUTO walk + the frame as one hipGraph
+                with rt.Context(device=local, flags=rt.FLAG_GRAPH | rt.FLAG_AUTO_WALK) as c:
                     c.set_scene(sk)
-                    c.set_camera(*rt.camera_reference(wk["W"], wk["H"]))
+                    wvp_k, wv_k = rt.camera_reference(wk["W"], wk["H"])
+                    c.set_camera(wvp_k, wv_k)
                     c.compute_bvh(wk["W"], wk["H"], wk["bounces"])   # capture
                     t0 = time.perf_counter()
                     for _ in range(50):
                         c.compute_bvh(wk["W"], wk["H"], wk["bounces"])
                     dtg = (time.perf_counter() - t0) / 50
+                    gframe, gtree = c.read_framebuffer(), c.read_bvh()
                 rk = q["primary_rays"] + q["bounce_rays"]
                 extras[f"{key}_frame"] = {"workload": wk["name"], "rays": int(rk),
                                           "mrays_s_trace": round(rk / (q2["ms_trace"] * 1e-3) / 1e6, 1),
                                           "mrays_s_build_plus_trace_wall": round(rk / dt / 1e6, 1),
                                           "mrays_s_build_plus_trace_wall_graph": round(rk / dtg / 1e6, 1),
                                           "ms_build": round(q2["ms_build"], 4), "ms_trace": round(q2["ms_trace"], 4)}
+                if key == "c3":
+                    # BASELINE.json's metric is quoted "@1080p" on C3 (Test.obj, primary + 1 reflection
+                    # bounce): its own first-class line, in the reference's frame semantics -- rebuild +
+                    # trace every frame, synchronously (Graphics.cpp:56, 667-831) -- with its frame and
+                    # tree checked against the oracle (OpenMP; cache-resident scene: the roofline is C5's)
+                    from oracle import lib as orc
+                    osk = orc.Scene(sk.vertices, sk.indices, sk.mat_indices, sk.material_blob)
+                    otree = orc.build(osk, wvp_k, sort_mode=0)
+                    orc.set_threads(int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1))
+                    try:
+                        oframe, _, _ = orc.trace(osk, otree, wvp_k, wv_k, wk["W"], wk["H"], wk["bounces"])
+                    finally:
+                        orc.set_threads(1)
+                    extras["c3_1080p"] = {
+                        "metric": "Mrays/s primary+1-bounce @1080p (BASELINE.json metric on its own config, C3)",
+                        "value": round(rk / dtg / 1e6, 1), "unit": "Mrays/s", "ms_per_frame": round(dtg * 1e3, 4),
+                        "higher_is_better": True, "dtype": "f32", "data": "Obj/Test.obj fixture (parsed reference mesh)",
+                        "config": {"workload": wk["name"], "width": wk["W"], "height": wk["H"], "bounces": 1,
+                                   "triangles": sk.num_tris, "rays_per_frame": int(rk)},
+                        "semantics": "rtbvh_compute_bvh per frame (BVH rebuilt + primary + 1 bounce, synchronous, "
+                                     "as Graphics::onUpdate -> computeBVH), RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_GRAPH",
+                        "build_ms": round(q2["ms_build"], 4), "trace_ms": round(q2["ms_trace"], 4),
+                        "mrays_s_trace_only": round(rk / (q2["ms_trace"] * 1e-3) / 1e6, 1),
+                        "parity": {"tree_bit_identical": bool(all(np.array_equal(gtree[f], otree[f])
+                                                                  for f in NODE_FIELDS)),
+                                   "frame_bit_identical": bool(np.array_equal(gframe, oframe)),
+                                   "pixels_checked": int(wk["W"] * wk["H"])}}
         cpu = parity = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline (oracle, bounded sample) ...")
@@ -574,7 +641,8 @@ def main():
             "data": "synthetic (splitmix64 generator, SURVEY §8(d))" if "obj" not in wl else "Obj/Test.obj fixture",
             "config": {"workload": wl["name"], "width": W, "height": H, "bounces": bounces,
                        "triangles": scene.num_tris, "rays_per_step": int(rays_per_step),
-                       "parallelism": f"image bands x{world} + RCCL gather" if world > 1 else "single GPU"},
+                       "parallelism": f"image bands x{world} + RCCL gather" if world > 1 else "single GPU",
+                       "band_deal_root_share": share},
             "roofline": roofline,
             "build_roofline": build_roofline,
             "parity": parity,

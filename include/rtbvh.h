@@ -234,9 +234,10 @@ rtbvh_status rtbvh_trace_async(rtbvh_ctx* ctx, uint32_t width, uint32_t height, 
 /* The whole computeBVH: build + trace (Graphics.cpp:667-831). */
 rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces);
 /* Image-tile shard for multi-GPU (no reference equivalent): trace
- * only the 8-row bands b with b % nranks == rank of a W x H frame and write them
- * compacted (band order) as RGBA f32 into dev_out (device memory, at least
- * rtbvh_band_rows(H, rank, nranks) * W * 4 floats), enqueued on `stream`
+ * only this rank's 8-row bands of a W x H frame under the context's deal (rtbvh_set_band_deal;
+ * by default b % nranks == rank) and write them compacted (band order) as RGBA f32 into
+ * dev_out (device memory, at least rtbvh_deal_rows(H, rank, nranks, share) * W * 4 floats,
+ * = rtbvh_band_rows(H, rank, nranks) for the default deal), enqueued on `stream`
  * (hipStream_t, NULL = the context stream).  The caller gathers the shards.
  * Frames in flight: each caller stream other than the context's (up to 3) gets trace
  * buffers of its own over the one BVH, so traces on different streams run concurrently
@@ -246,6 +247,19 @@ rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* ctx, uint32_t width, uint32_t height, 
 rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t bounces,
                                     uint32_t rank, uint32_t nranks, float* dev_out, void* stream);
 uint32_t rtbvh_band_rows(uint32_t height, uint32_t rank, uint32_t nranks);
+/* The band deal.  Bands b = 0 .. ceil(H/8)-1 go to the ranks by smooth weighted round-robin:
+ * rank 0 weighs root_share (0..16), every other rank 16; per band each rank's credit grows by its
+ * weight and the rank with the most credit (lowest rank on a tie) takes the band and pays the total
+ * weight.  root_share 16 (the default) is b % nranks; below 16, rank 0 -- which also receives and
+ * assembles every other rank's bands -- traces root_share/16 of another rank's share, spread evenly
+ * over the frame.  rtbvh_deal_bands writes rank's band indices in order (up to capacity) and
+ * returns their count; rtbvh_deal_rows returns its rows.  rtbvh_set_band_deal sets the context's
+ * deal for rtbvh_trace_band_async, rtbvh_assemble_bands and rtbvh_trace_tiles (every rank must use
+ * the same root_share). */
+uint32_t rtbvh_deal_bands(uint32_t height, uint32_t rank, uint32_t nranks, uint32_t root_share, uint32_t* bands,
+                          uint32_t capacity);
+uint32_t rtbvh_deal_rows(uint32_t height, uint32_t rank, uint32_t nranks, uint32_t root_share);
+rtbvh_status rtbvh_set_band_deal(rtbvh_ctx* ctx, uint32_t root_share);
 /* The per-scene identity check of a fast walk: traces the W x H frame in the reference order
  * (the exact findCollision DFS) and with the context's walk flags, compares the two on the device
  * and stores the number of pixels whose RGBA bits differ (0: the fast walk renders this frame
@@ -255,7 +269,8 @@ rtbvh_status rtbvh_verify_walk(rtbvh_ctx* ctx, uint32_t width, uint32_t height, 
                                uint64_t* differing_pixels);
 /* The frame from the ranks' compact band buffers, all on this device: buffer r (rank r's
  * rtbvh_trace_band_async output) starts stride_rows * W * 4 floats after buffer r-1
- * (stride_rows >= rtbvh_band_rows(H, 0, nranks)); writes W*H*4 floats to dev_frame.
+ * (stride_rows >= the most rows any rank has under the context's deal: rtbvh_deal_rows);
+ * writes W*H*4 floats to dev_frame.
  * Enqueued on `stream` (NULL = the context stream).  rtbvh_trace_tiles uses it on rank 0. */
 rtbvh_status rtbvh_assemble_bands(rtbvh_ctx* ctx, uint32_t width, uint32_t height, uint32_t nranks,
                                   const float* dev_bands, uint32_t stride_rows, float* dev_frame, void* stream);

@@ -117,12 +117,24 @@ uint32_t orc_morton_point_hlsl(float x, float y, float z) {
 /* ShaderSim/main.cpp:269-301: mesh vertex AABB, true centroid (x0+x1+x2)/3 */
 void orc_morton_tris_cputests(const orc_scene* s, uint32_t* codes) {
     f3 mn = mk(9999999e10f, 9999999e10f, 9999999e10f), mx = mk(-9999999e10f, -9999999e10f, -9999999e10f);
-    for (uint32_t i = 0; i < s->num_verts; i++) {
-        f3 p = vpos(s, i);
-        mn = vmin(p, mn);
-        mx = vmax(p, mx);
+    // (all-cores variant: per-thread partial boxes; min/max are exact, so the box is the same)
+#pragma omp parallel num_threads(g_threads) if (g_threads > 1)
+    {
+        f3 lo = mn, hi = mx;
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < (int64_t)s->num_verts; i++) {
+            f3 p = vpos(s, (uint32_t)i);
+            lo = vmin(p, lo);
+            hi = vmax(p, hi);
+        }
+#pragma omp critical
+        {
+            mn = vmin(lo, mn);
+            mx = vmax(hi, mx);
+        }
     }
     const uint32_t ntri = s->num_indices / 3;
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(static)
     for (uint32_t t = 0; t < ntri; t++) {
         f3 a = vpos(s, s->indices[3 * t]), b = vpos(s, s->indices[3 * t + 1]), c = vpos(s, s->indices[3 * t + 2]);
         float xv = a.x + b.x + c.x, yv = a.y + b.y + c.y, zv = a.z + b.z + c.z;
@@ -181,17 +193,24 @@ void orc_split_sort(const uint32_t* keys, uint32_t n, uint32_t* perm) {
     std::vector<uint32_t> k(np, 0xFFFFFFFFu), idx(np), k2(np), idx2(np), flags(np), zeros(G), prec(G);
     for (uint32_t i = 0; i < n; i++) k[i] = keys[i];
     for (uint32_t i = 0; i < np; i++) idx[i] = i;
+    // (all-cores variant, orc_set_threads > 1: the flags, the groups' scans and the scatter
+    // run in parallel -- one thread per element / group, as the GPU dispatch does)
     for (uint32_t r = 0; r < 32; r++) {
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(static)
         for (uint32_t i = 0; i < np; i++) flags[i] = !(k[i] & (1u << r));        // RadixSortP1.hlsl:78
-        uint32_t net = 0;
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(static)
         for (uint32_t g = 0; g < G; g++) {
             uint32_t* f = &flags[g * DS];
             uint32_t last = f[DS - 1];                                            // :84-85
             orc_blelloch_scan256(f);
             zeros[g] = last + f[DS - 1];                                          // :94-95
+        }
+        uint32_t net = 0;
+        for (uint32_t g = 0; g < G; g++) {
             prec[g] = net;                                                        // RadixSortP2.hlsl:16-22
             net += zeros[g];
         }
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(static)
         for (uint32_t i = 0; i < np; i++) {
             uint32_t g = i / DS, pos0 = flags[i];
             uint32_t present = i - pos0 - prec[g] + net;                         // RadixSortP2.hlsl:45-48
@@ -266,7 +285,10 @@ int32_t orc_delta(int mode, const uint32_t* codes, uint32_t n, uint32_t i, int64
 void orc_karras(int mode, const uint32_t* c, uint32_t n, uint32_t* parent, uint32_t* cl, uint32_t* cr) {
     const uint32_t total = 2 * n - 1;
     for (uint32_t k = 0; k < total; k++) { parent[k] = 0xFFFFFFFFu; cl[k] = 0xFFFFFFFFu; cr[k] = 0xFFFFFFFFu; }
-    for (int64_t i = 0; i + 1 < (int64_t)n; i++) {
+    // (all-cores variant: one iteration per internal node, as BVHConstructP1's threads; every
+    // node has one parent, so the writes of two iterations never meet)
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(static)
+    for (int64_t i = 0; i < (int64_t)n - 1; i++) {
         int64_t d = orc_delta(mode, c, n, (uint32_t)i, i + 1) < orc_delta(mode, c, n, (uint32_t)i, i - 1) ? -1 : 1;
         int32_t min_lz = orc_delta(mode, c, n, (uint32_t)i, i - d);
         int64_t bound_len = 2;
@@ -299,6 +321,30 @@ void orc_karras(int mode, const uint32_t* c, uint32_t n, uint32_t* parent, uint3
 uint32_t orc_refit(uint32_t n, const uint32_t* parent, const uint32_t* cl, const uint32_t* cr,
                    float* bmin, float* bmax) {
     if (n < 2) return 0;
+    if (g_threads > 1) {   // all-cores variant: the GPU's one thread per leaf with an atomic ticket per node
+        std::vector<uint32_t> ticket(n, 0);
+        uint32_t longest = 0;
+#pragma omp parallel for num_threads(g_threads) schedule(static) reduction(max : longest)
+        for (uint32_t t = 0; t < n; t++) {
+            uint32_t node = parent[t], loops = 0;
+            // acq_rel: the first arriver's child box is visible to the second (InterlockedAdd + the
+            // fence BVHConstructP2.hlsl lacks); min/max are exact, so the order does not matter
+            uint32_t value = __atomic_fetch_add(&ticket[node - n], 1u, __ATOMIC_ACQ_REL);
+            while (value) {
+                uint32_t a = cl[node], b = cr[node];
+                for (int k = 0; k < 3; k++) {
+                    bmin[3 * node + k] = fmin_h(bmin[3 * a + k], bmin[3 * b + k]);
+                    bmax[3 * node + k] = fmax_h(bmax[3 * a + k], bmax[3 * b + k]);
+                }
+                node = parent[node];
+                if (node == 0xFFFFFFFFu) break;
+                value = __atomic_fetch_add(&ticket[node - n], 1u, __ATOMIC_ACQ_REL);
+                loops++;
+            }
+            longest = std::max(longest, loops);
+        }
+        return longest;
+    }
     std::vector<uint32_t> transfer(n, 0);
     uint32_t longest = 0;
     for (uint32_t t = 0; t < n; t++) {
@@ -336,6 +382,7 @@ int orc_build(const orc_scene* s, const float wvp[16], int morton_mode, int delt
     std::vector<float> bmin(3 * (size_t)total, 0.f), bmax(3 * (size_t)total, 0.f);
     orc_karras(delta_mode, sorted.data(), n, parent.data(), cl.data(), cr.data());
     // leaf AABB in clip space: MortonCodes.hlsl:84-99, 115-116
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(static)
     for (uint32_t i = 0; i < n; i++) {
         uint32_t t = perm[i];
         f3 v = xform_point(wvp, vpos(s, s->indices[3 * t]));

@@ -31,6 +31,7 @@ EXPORTS = [
     "rtbvh_config_default", "rtbvh_create", "rtbvh_destroy", "rtbvh_last_error", "rtbvh_abi_version",
     "rtbvh_set_scene", "rtbvh_set_camera", "rtbvh_build", "rtbvh_build_async", "rtbvh_trace",
     "rtbvh_trace_async", "rtbvh_compute_bvh", "rtbvh_trace_band_async", "rtbvh_band_rows", "rtbvh_verify_walk",
+    "rtbvh_deal_bands", "rtbvh_deal_rows", "rtbvh_set_band_deal",
     "rtbvh_synchronize", "rtbvh_read_framebuffer", "rtbvh_read_intensity", "rtbvh_framebuffer_device",
     "rtbvh_read_bvh", "rtbvh_read_wide", "rtbvh_read_qnodes", "rtbvh_read_morton", "rtbvh_read_sorted", "rtbvh_read_rays", "rtbvh_get_stats",
     "rtbvh_reset_stats", "rtbvh_set_flags",
@@ -128,6 +129,9 @@ def lib() -> ctypes.CDLL:
         "rtbvh_compute_bvh": (i32, [vp, u32, u32, u32]),
         "rtbvh_trace_band_async": (i32, [vp, u32, u32, u32, u32, u32, vp, vp]),
         "rtbvh_band_rows": (u32, [u32, u32, u32]),
+        "rtbvh_deal_bands": (u32, [u32, u32, u32, u32, vp, u32]),
+        "rtbvh_deal_rows": (u32, [u32, u32, u32, u32]),
+        "rtbvh_set_band_deal": (i32, [vp, u32]),
         "rtbvh_verify_walk": (i32, [vp, u32, u32, u32, ctypes.POINTER(u64)]),
         "rtbvh_assemble_bands": (i32, [vp, u32, u32, u32, vp, u32, vp, vp]),
         "rtbvh_comm_unique_id": (i32, [vp]),

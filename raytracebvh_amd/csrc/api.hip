@@ -5,8 +5,10 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <new>
 #include <string>
 #include <type_traits>
@@ -139,6 +141,14 @@ struct rtbvh_ctx {
     uint64_t walk_checks = 0, walk_fallbacks = 0;
     uint32_t last_walk = 0;                           // walk flags of the last trace
     uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
+    // the band deal of band traces (rtbvh_set_band_deal): rank 0's weight in 1/16 of another rank's
+    uint32_t root_share = 16;
+    struct DealTab {   // a weighted deal's device table: every rank's bands, then slots[b] = r << 24 | pos
+        uint32_t H, nranks, share;
+        uint32_t* d;
+        std::vector<uint32_t> off;   // rank r's bands at d[off[r] .. off[r + 1])
+    };
+    std::deque<DealTab> deals;       // one per (H, nranks, share) used; kept until destroy (traces in flight read them)
 };
 
 namespace {
@@ -295,6 +305,79 @@ BuildArgs build_args(rtbvh_ctx* c) {
     return a;
 }
 
+// ---- the band deal ----------------------------------------------
+// The frame's 8-row bands b = 0 .. ceil(H / 8) - 1 go to the ranks by smooth weighted round-robin:
+// rank 0 has weight `share`, every other rank 16; for each band every rank's credit grows by its
+// weight, and the rank with the most credit (the lowest on a tie) takes the band and pays the
+// total weight.  share 16 deals b -> b % nranks exactly; below 16, rank 0 -- which also receives
+// and assembles the other ranks' bands -- traces share / 16 of another rank's bands, spread evenly
+// over the frame (the centre-heavy hit distribution stays balanced).
+void deal_owners(uint32_t H, uint32_t nranks, uint32_t share, std::vector<uint32_t>& owner) {
+    const uint32_t nb = (H + 7) / 8;
+    owner.assign(nb, 0);
+    if (nranks <= 1) return;
+    std::vector<int64_t> credit(nranks, 0);
+    const int64_t total = (int64_t)share + 16 * (int64_t)(nranks - 1);
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t best = 0;
+        for (uint32_t r = 0; r < nranks; r++) {
+            credit[r] += r == 0 ? share : 16;
+            if (credit[r] > credit[best]) best = r;
+        }
+        credit[best] -= total;
+        owner[b] = best;
+    }
+}
+uint32_t band_height(uint32_t H, uint32_t b) { return (H - b * 8) < 8 ? (H - b * 8) : 8; }
+uint32_t deal_rows(uint32_t H, uint32_t rank, uint32_t nranks, uint32_t share) {
+    if (nranks == 0 || rank >= nranks) return 0;
+    if (share == 16 || nranks == 1) {
+        uint32_t rows = 0;
+        for (uint32_t b = rank; b * 8 < H; b += nranks) rows += band_height(H, b);
+        return rows;
+    }
+    std::vector<uint32_t> owner;
+    deal_owners(H, nranks, share, owner);
+    uint32_t rows = 0;
+    for (uint32_t b = 0; b < owner.size(); b++)
+        if (owner[b] == rank) rows += band_height(H, b);
+    return rows;
+}
+uint32_t deal_max_rows(uint32_t H, uint32_t nranks, uint32_t share) {
+    uint32_t m = 0;
+    for (uint32_t r = 0; r < nranks; r++) m = std::max(m, deal_rows(H, r, nranks, share));
+    return m;
+}
+// The device table of a weighted deal (null for round-robin: the kernels compute it).  Uploaded
+// synchronously on first use, so not from inside a graph capture (whose frames have one rank).
+rtbvh_status get_deal(rtbvh_ctx* c, uint32_t H, uint32_t nranks, const rtbvh_ctx::DealTab** out) {
+    *out = nullptr;
+    if (c->root_share == 16 || nranks <= 1) return RTBVH_OK;
+    for (const auto& t : c->deals)
+        if (t.H == H && t.nranks == nranks && t.share == c->root_share) {
+            *out = &t;
+            return RTBVH_OK;
+        }
+    if (c->capturing) return fail(c, RTBVH_ERR_INVALID_ARG, "a new band deal inside a graph capture");
+    std::vector<uint32_t> owner;
+    deal_owners(H, nranks, c->root_share, owner);
+    const uint32_t nb = (uint32_t)owner.size();
+    rtbvh_ctx::DealTab t{H, nranks, c->root_share, nullptr, std::vector<uint32_t>(nranks + 1, 0)};
+    std::vector<uint32_t> host(2 * (size_t)nb + 1), cnt(nranks, 0);
+    for (uint32_t b = 0; b < nb; b++) t.off[owner[b] + 1]++;
+    for (uint32_t r = 0; r < nranks; r++) t.off[r + 1] += t.off[r];
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t r = owner[b], pos = cnt[r]++;
+        host[t.off[r] + pos] = b;           // rank r's pos-th band
+        host[nb + b] = r << 24 | pos;       // where band b sits (k_assemble)
+    }
+    HIPC(c, hipMalloc((void**)&t.d, host.size() * sizeof(uint32_t)));
+    HIPC(c, hipMemcpy(t.d, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->deals.push_back(std::move(t));
+    *out = &c->deals.back();
+    return RTBVH_OK;
+}
+
 TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks, float4* color, float* inten) {
     TraceArgs a{};
     a.inner = c->d_rec;
@@ -316,6 +399,9 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.nranks = nranks;
     a.band0 = 0;
     a.bstep = 1;
+    const uint32_t nb = (H + 7) / 8;
+    a.my_bands = rank < nb ? (nb - rank + nranks - 1) / nranks : 0;   // round-robin; enqueue_walks sets a deal's
+    a.band_list = nullptr;
     memcpy(a.wv.m, c->wv, sizeof(c->wv));
     a.color = color;
     a.intensity = inten;
@@ -425,6 +511,13 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool count = (c->cfg.flags & RTBVH_FLAG_COUNT_VISITS) != 0;
     const bool timing = timed && (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream && !c->capturing;
     TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
+    const rtbvh_ctx::DealTab* deal = nullptr;
+    rtbvh_status dst = get_deal(c, H, nranks, &deal);
+    if (dst) return dst;
+    if (deal) {
+        a.my_bands = deal->off[rank + 1] - deal->off[rank];
+        a.band_list = deal->d + deal->off[rank];
+    }
     a.counters = c->d_counters + 64 * slot;
     HIPC(c, hipMemsetAsync(a.counters, 0, 64 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
@@ -432,7 +525,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool sort = wk.sort, refill = wk.refill;
     const bool records = (flags & RTBVH_FLAG_REFRACT_RECORDS) != 0;
     if (records && slot) return fail(c, RTBVH_ERR_INVALID_ARG, "ray records are traced on the context stream only");
-    const uint32_t P = W * rtbvh_band_rows(H, rank, nranks);   // max live rays of this shard
+    const uint32_t P = W * deal_rows(H, rank, nranks, c->root_share);   // max live rays of this shard
     // persistent grid of the bounce walk: 2048 blocks (8 waves/SIMD), 1024 for a shard of
     // < 4M pixels -- with frames in flight the next frame's primary blocks then share the CUs
     // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame)
@@ -454,8 +547,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     // pipelines: the rank's bands dealt round-robin over nsplit primary -> bounce chains
     // (band k of this rank goes to chain k % nsplit), each with its own queues and work
     // counters, chain 0 on the context stream, chain g on sub[g]; joined before the end event
-    const uint32_t nbands = (H + 7) / 8;
-    const uint32_t my_bands = rank < nbands ? (nbands - rank + nranks - 1) / nranks : 0;
+    const uint32_t my_bands = a.my_bands;
     uint32_t nsplit = trace_split(c, (size_t)W * 8 * my_bands);
     // the coherence sort has one set of buffers; frames-in-flight slots use the chains' buffers
     if (sort || my_bands < nsplit || slot || c->slots_used) nsplit = 1;
@@ -544,7 +636,7 @@ rtbvh_ctx::WalkKey walk_key(const rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
     k.w[0] = c->built_scene_gen << 32 | (c->built_cam_gen & 0xFFFFFFFFu);
     k.w[1] = c->cam_gen;
     k.w[2] = (uint64_t)W | (uint64_t)H << 32;
-    k.w[3] = (uint64_t)bounces | (uint64_t)rank << 8 | (uint64_t)nranks << 32;
+    k.w[3] = (uint64_t)bounces | (uint64_t)rank << 8 | (uint64_t)c->root_share << 24 | (uint64_t)nranks << 32;
     return k;
 }
 int find_walk_key(const rtbvh_ctx* c, const rtbvh_ctx::WalkKey& k) {
@@ -595,7 +687,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, ref, true);
     }
     if (!color) color = c->d_color;
-    const size_t n = (size_t)W * rtbvh_band_rows(H, rank, nranks);
+    const size_t n = (size_t)W * deal_rows(H, rank, nranks, c->root_share);
     if (c->cap_v < n) {
         HIPC(c, dalloc(c->d_vcolor, n));
         HIPC(c, dalloc(c->d_vinten, n));
@@ -724,6 +816,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_counters);
     dfree(c->d_ovf);
     dfree(c->d_vcolor); dfree(c->d_vinten); dfree(c->d_vdiff);
+    for (auto& t : c->deals) dfree(t.d);
     if (c->h_vdiff) (void)hipHostFree(c->h_vdiff);
     if (c->ev_verify) (void)hipEventDestroy(c->ev_verify);
     if (c->h_ovf) (void)hipHostFree(c->h_ovf);
@@ -1011,11 +1104,36 @@ rtbvh_status rtbvh_verify_walk(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
     return rtbvh_synchronize(c);
 }
 
-uint32_t rtbvh_band_rows(uint32_t H, uint32_t rank, uint32_t nranks) {
-    if (nranks == 0 || rank >= nranks) return 0;
-    uint32_t rows = 0;
-    for (uint32_t b = rank; b * 8 < H; b += nranks) rows += (H - b * 8) < 8 ? (H - b * 8) : 8;
-    return rows;
+uint32_t rtbvh_band_rows(uint32_t H, uint32_t rank, uint32_t nranks) { return deal_rows(H, rank, nranks, 16); }
+
+uint32_t rtbvh_deal_rows(uint32_t H, uint32_t rank, uint32_t nranks, uint32_t root_share) {
+    return root_share > 16 ? 0 : deal_rows(H, rank, nranks, root_share);
+}
+
+uint32_t rtbvh_deal_bands(uint32_t H, uint32_t rank, uint32_t nranks, uint32_t root_share, uint32_t* bands,
+                          uint32_t capacity) {
+    if (nranks == 0 || rank >= nranks || root_share > 16) return 0;
+    std::vector<uint32_t> owner;
+    if (root_share == 16 || nranks == 1) {
+        owner.resize((H + 7) / 8);
+        for (uint32_t b = 0; b < owner.size(); b++) owner[b] = b % nranks;
+    } else {
+        deal_owners(H, nranks, root_share, owner);
+    }
+    uint32_t n = 0;
+    for (uint32_t b = 0; b < owner.size(); b++)
+        if (owner[b] == rank) {
+            if (bands && n < capacity) bands[n] = b;
+            n++;
+        }
+    return n;
+}
+
+rtbvh_status rtbvh_set_band_deal(rtbvh_ctx* c, uint32_t root_share) {
+    if (!c) return RTBVH_ERR_INVALID_ARG;
+    if (root_share > 16) return fail(c, RTBVH_ERR_INVALID_ARG, "set_band_deal: root_share > 16");
+    c->root_share = root_share;
+    return RTBVH_OK;
 }
 
 rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank,
@@ -1049,11 +1167,14 @@ rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32
 rtbvh_status rtbvh_assemble_bands(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t nranks, const float* dev_bands,
                                   uint32_t stride_rows, float* dev_frame, void* stream) {
     if (!c || !dev_bands || !dev_frame || W == 0 || H == 0 || nranks == 0 ||
-        stride_rows < rtbvh_band_rows(H, 0, nranks))
+        stride_rows < deal_max_rows(H, nranks, c->root_share))
         return RTBVH_ERR_INVALID_ARG;
     HIPC(c, hipSetDevice(c->cfg.device));
-    launch_assemble((const float4*)dev_bands, stride_rows, W, H, nranks, (float4*)dev_frame,
-                    stream ? (hipStream_t)stream : c->stream);
+    const rtbvh_ctx::DealTab* deal = nullptr;
+    rtbvh_status st = get_deal(c, H, nranks, &deal);
+    if (st) return st;
+    launch_assemble((const float4*)dev_bands, deal ? deal->d + (H + 7) / 8 : nullptr, stride_rows, W, H, nranks,
+                    (float4*)dev_frame, stream ? (hipStream_t)stream : c->stream);
     return check_launch(c, "assemble bands");
 }
 
@@ -1093,17 +1214,17 @@ rtbvh_status rtbvh_comm_destroy(void* comm) {
     return RTBVH_OK;
 }
 
-// bands of 8 rows dealt round-robin; one RCCL group of point-to-point
-// transfers into rank 0 (xGMI is point to point: each rank's shard travels its own link),
-// then the row scatter on rank 0.  Rank 0's buffer holds every rank's bands, rank r at
-// r * rows0 rows (rows0 = rank 0's band rows, the most any rank has).
+// bands of 8 rows dealt by the context's deal (rtbvh_set_band_deal); one RCCL
+// group of point-to-point transfers into rank 0 (xGMI is point to point: each rank's shard
+// travels its own link), then the row scatter on rank 0.  Rank 0's buffer holds every rank's
+// bands, rank r at r * rows0 rows (rows0 = the most band rows any rank has).
 rtbvh_status rtbvh_trace_tiles(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank,
                                uint32_t nranks, void* comm) {
     if (!c || !comm || W == 0 || H == 0 || nranks == 0 || rank >= nranks) return RTBVH_ERR_INVALID_ARG;
     const Rccl& r = rccl();
     if (!r.ok) return fail(c, RTBVH_ERR_COMM, r.err);
     HIPC(c, hipSetDevice(c->cfg.device));
-    const uint32_t rows0 = rtbvh_band_rows(H, 0, nranks);
+    const uint32_t rows0 = deal_max_rows(H, nranks, c->root_share);
     const size_t need = (size_t)(rank == 0 ? nranks : 1) * rows0 * W;
     if (c->cap_band < need) {
         HIPC(c, dalloc(c->d_band, need));
@@ -1115,17 +1236,23 @@ rtbvh_status rtbvh_trace_tiles(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
     ncclResult_t e = r.GroupStart();
     if (rank != 0) {
         if (e == ncclSuccess)
-            e = r.Send(c->d_band, (size_t)rtbvh_band_rows(H, rank, nranks) * W * 4, ncclFloat32, 0, cm, c->stream);
+            e = r.Send(c->d_band, (size_t)deal_rows(H, rank, nranks, c->root_share) * W * 4, ncclFloat32, 0, cm,
+                       c->stream);
     } else {
         for (uint32_t q = 1; q < nranks && e == ncclSuccess; q++)
-            e = r.Recv(c->d_band + (size_t)q * rows0 * W, (size_t)rtbvh_band_rows(H, q, nranks) * W * 4, ncclFloat32,
+            e = r.Recv(c->d_band + (size_t)q * rows0 * W, (size_t)deal_rows(H, q, nranks, c->root_share) * W * 4,
+                       ncclFloat32,
                        (int)q, cm, c->stream);
     }
     const ncclResult_t e2 = r.GroupEnd();
     if (e == ncclSuccess) e = e2;
     if (e != ncclSuccess) return fail(c, RTBVH_ERR_COMM, std::string("band gather: ") + r.GetErrorString(e));
     if (rank == 0) {
-        launch_assemble(c->d_band, rows0, W, H, nranks, c->d_color, c->stream);
+        const rtbvh_ctx::DealTab* deal = nullptr;
+        st = get_deal(c, H, nranks, &deal);
+        if (st) return st;
+        launch_assemble(c->d_band, deal ? deal->d + (H + 7) / 8 : nullptr, rows0, W, H, nranks, c->d_color,
+                        c->stream);
         st = check_launch(c, "assemble bands");
         if (st) return st;
     }
@@ -1307,7 +1434,7 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         HIPC(c, hipMemcpy(cnt, c->d_counters + 64 * c->last_slot, sizeof(cnt), hipMemcpyDeviceToHost));
         HIPC(c, hipMemcpy(q, c->d_qcount + 32 * c->last_slot, sizeof(uint32_t) * 32 * c->nsplit,
                           hipMemcpyDeviceToHost));
-        out->primary_rays = (uint64_t)c->W * rtbvh_band_rows(c->H, c->rank, c->nranks);
+        out->primary_rays = (uint64_t)c->W * deal_rows(c->H, c->rank, c->nranks, c->root_share);
         uint64_t b = 0;
         for (uint32_t g = 0; g < c->nsplit; g++)
             for (uint32_t k = 0; k < c->bounces; k++) b += q[32 * g + k];

@@ -101,6 +101,8 @@ struct TraceArgs {
     uint32_t ntex;
     uint32_t T, W, H, rank, nranks;
     uint32_t band0, bstep;    // this launch traces the rank's bands band0, band0 + bstep, ... (trace chains)
+    uint32_t my_bands;        // the rank's bands under the deal (rtbvh_deal_bands)
+    const uint32_t* band_list;   // the rank's bands in order (a weighted deal), or null: k * nranks + rank
     Mat4 wv;
     float4* color;            // output pixels (compacted band rows when nranks > 1)
     float* intensity;         // optional, same indexing as color
@@ -143,7 +145,8 @@ void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qi
 void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long long* diff, hipStream_t s);
 void launch_count_diff32(const float* a, const float* b, size_t n, unsigned long long* diff, hipStream_t s);
 // frame from per-rank compact band buffers (stride_rows rows apart), see rtbvh_assemble_bands
-void launch_assemble(const float4* bands, uint32_t stride_rows, uint32_t W, uint32_t H, uint32_t nranks,
+void launch_assemble(const float4* bands, const uint32_t* slots, uint32_t stride_rows, uint32_t W, uint32_t H,
+                     uint32_t nranks,
                      float4* frame, hipStream_t s);
 // presentation pass (RayTraceBVHPS.hlsl): flipped rows, UNORM8 RGBA
 void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, hipStream_t s);

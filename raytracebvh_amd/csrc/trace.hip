@@ -688,7 +688,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t k = a.band0 + blockIdx.y * a.bstep;   // the rank's k-th band
-    const uint32_t band = k * a.nranks + a.rank;
+    const uint32_t band = a.band_list ? a.band_list[k] : k * a.nranks + a.rank;
     const uint32_t y = band * 8 + (lane >> 3);
     const bool valid = x < a.W && y < a.H;
     const size_t out = ((size_t)k * 8 + (lane >> 3)) * a.W + x;
@@ -1316,16 +1316,19 @@ __global__ __launch_bounds__(BLOCK) void k_present(const float4* __restrict__ co
     out[i] = unorm8(c.x) | unorm8(c.y) << 8 | unorm8(c.z) << 16 | unorm8(c.w) << 24;
 }
 
-// frame row y of a W x H frame traced as 8-row bands dealt round-robin over nranks: band
-// b = y / 8 is rank b % nranks's (b / nranks)-th band, so it sits at row (b / nranks) * 8 +
-// y % 8 of that rank's compact buffer, buffers stacked stride_rows apart (tiles.py layout)
-__global__ __launch_bounds__(BLOCK) void k_assemble(const float4* __restrict__ bands, uint32_t stride_rows,
+// frame row y of a W x H frame traced as 8-row bands dealt over nranks: band b = y / 8 is
+// rank r's p-th band, so it sits at row p * 8 + y % 8 of that rank's compact buffer, buffers
+// stacked stride_rows apart (tiles.py layout).  Round-robin (slots null): r = b % nranks,
+// p = b / nranks; a weighted deal (rtbvh_deal_bands): slots[b] = r << 24 | p.
+__global__ __launch_bounds__(BLOCK) void k_assemble(const float4* __restrict__ bands,
+                                                    const uint32_t* __restrict__ slots, uint32_t stride_rows,
                                                     uint32_t W, uint32_t H, uint32_t nranks,
                                                     float4* __restrict__ frame) {
     const size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= (size_t)W * H) return;
     const uint32_t y = (uint32_t)(i / W), x = (uint32_t)(i % W);
-    const uint32_t b = y >> 3, r = b % nranks, k = (b / nranks) * 8 + (y & 7u);
+    const uint32_t b = y >> 3, sl = slots ? slots[b] : (b % nranks) << 24 | (b / nranks);
+    const uint32_t r = sl >> 24, k = (sl & 0xFFFFFFu) * 8 + (y & 7u);
     frame[i] = bands[((size_t)r * stride_rows + k) * W + x];
 }
 
@@ -1381,8 +1384,7 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
 
 void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, PrimaryKind kind,
                     hipStream_t s) {
-    const uint32_t nbands = (a.H + 7) / 8;
-    const uint32_t my_bands = a.rank < nbands ? (nbands - a.rank + a.nranks - 1) / a.nranks : 0;
+    const uint32_t my_bands = a.my_bands;
     const uint32_t launch_bands = my_bands > a.band0 ? (my_bands - a.band0 + a.bstep - 1) / a.bstep : 0;
     if (launch_bands == 0 || a.W == 0) return;
     dim3 grid((a.W + 31) / 32, launch_bands);
@@ -1444,11 +1446,11 @@ void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qi
                            qin_count, hitrec, qout, qout_count, (int)emit);
 }
 
-void launch_assemble(const float4* bands, uint32_t stride_rows, uint32_t W, uint32_t H, uint32_t nranks,
-                     float4* frame, hipStream_t s) {
+void launch_assemble(const float4* bands, const uint32_t* slots, uint32_t stride_rows, uint32_t W, uint32_t H,
+                     uint32_t nranks, float4* frame, hipStream_t s) {
     const size_t n = (size_t)W * H;
-    hipLaunchKernelGGL(k_assemble, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, bands, stride_rows,
-                       W, H, nranks, frame);
+    hipLaunchKernelGGL(k_assemble, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, bands, slots,
+                       stride_rows, W, H, nranks, frame);
 }
 
 void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, hipStream_t s) {

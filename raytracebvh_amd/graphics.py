@@ -107,6 +107,10 @@ class Context:
                                                     ctypes.c_void_p(dev_out_ptr),
                                                     ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def set_band_deal(self, root_share: int):
+        """rtbvh_set_band_deal: rank 0's share of the bands in 1/16 of another rank's (16 = b % nranks)."""
+        self._check(_L.lib().rtbvh_set_band_deal(self._h, root_share))
+
     def assemble_bands(self, width: int, height: int, nranks: int, dev_bands_ptr: int, stride_rows: int,
                        dev_frame_ptr: int, stream_ptr: int | None = None):
         """rtbvh_assemble_bands: the frame from the ranks' compact band buffers (one device)."""

@@ -2,11 +2,13 @@
 
 The reference is single-GPU.  Multi-GPU here: every rank holds the same scene
 and builds the same BVH (deterministic replicas); the frame's 8-row bands are
-dealt round-robin (band b -> rank b % nranks, which balances the centre-heavy hit
-distribution), each rank traces its bands into a compact buffer
-(rtbvh_trace_band_async), and rank 0 gathers the buffers over torch.distributed
-("nccl" = RCCL over xGMI on MI355X; "gloo" in the CPU tests) and scatters the rows
-into the frame.  The only collective of the path is that gather.
+dealt by smooth weighted round-robin (rtbvh_deal_bands: rank 0 weighs root_share/16
+of another rank, since it also receives and assembles every rank's bands; 16 gives
+band b -> rank b % nranks; either way the bands of a rank are spread over the frame,
+which balances the centre-heavy hit distribution), each rank traces its bands into a
+compact buffer (rtbvh_trace_band_async), and rank 0 gathers the buffers over
+torch.distributed ("nccl" = RCCL over xGMI on MI355X; "gloo" in the CPU tests) and
+scatters the rows into the frame.  The only collective of the path is that gather.
 
 Frames in flight: with `nbuf=2` the band buffer of frame i+1 is a different buffer
 than frame i's, so frame i's gather (on the collective's own stream) runs while
@@ -18,21 +20,36 @@ from __future__ import annotations
 BAND = 8
 
 
-def band_row_ids(H: int, rank: int, nranks: int) -> list:
+def band_ids(H: int, rank: int, nranks: int, root_share: int = 16) -> list:
+    """The bands of `rank` under the deal, in order (rtbvh_deal_bands)."""
+    import ctypes
+
+    import numpy as np
+
+    from . import _lib as _L
+    n = _L.lib().rtbvh_deal_bands(H, rank, nranks, root_share, None, 0)
+    out = np.zeros(max(n, 1), np.uint32)
+    _L.lib().rtbvh_deal_bands(H, rank, nranks, root_share, ctypes.c_void_p(out.ctypes.data), n)
+    return [int(b) for b in out[:n]]
+
+
+def band_row_ids(H: int, rank: int, nranks: int, root_share: int = 16) -> list:
     """Frame rows owned by `rank`, in the order they appear in its compact buffer."""
-    return [y for b in range(rank, (H + BAND - 1) // BAND, nranks) for y in range(BAND * b, min(BAND * b + BAND, H))]
+    return [y for b in band_ids(H, rank, nranks, root_share) for y in range(BAND * b, min(BAND * b + BAND, H))]
 
 
 class BandGather:
     """Band buffer(s) of this rank and, on rank 0, the assembled frame."""
 
-    def __init__(self, W: int, H: int, rank: int, world: int, device, dtype=None, nbuf: int = 1):
+    def __init__(self, W: int, H: int, rank: int, world: int, device, dtype=None, nbuf: int = 1,
+                 root_share: int = 16):
         import torch
 
         dtype = dtype or torch.float32
         self.W, self.H, self.rank, self.world = W, H, rank, world
         self.nbuf = nbuf
-        self.rows = [len(band_row_ids(H, r, world)) for r in range(world)]
+        self.root_share = root_share
+        self.rows = [len(band_row_ids(H, r, world, root_share)) for r in range(world)]
         self.max_rows = max(self.rows)
         # every rank sends a buffer of the same (max) size: dist.gather needs equal shapes
         self.bands = [torch.zeros((self.max_rows, W, 4), dtype=dtype, device=device) for _ in range(self.nbuf)]
@@ -50,7 +67,7 @@ class BandGather:
             self.frames = [torch.empty((H, W, 4), dtype=dtype, device=device) for _ in range(self.nbuf)]
             self.frame = self.frames[0]
             self.gather_lists = [[torch.empty_like(self.band) for _ in range(world)] for _ in range(self.nbuf)]
-            self.row_idx = [torch.tensor(band_row_ids(H, r, world), dtype=torch.long, device=device)
+            self.row_idx = [torch.tensor(band_row_ids(H, r, world, root_share), dtype=torch.long, device=device)
                             for r in range(world)]
 
     def band_buffer(self, i: int):

@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, W, H, out_path, nbuf):
+def _worker(rank, world, port, W, H, out_path, nbuf, share=16):
     import sys
     sys.path.insert(0, REPO)
     from oracle import lib as orc
@@ -33,8 +33,8 @@ def _worker(rank, world, port, W, H, out_path, nbuf):
     s = orc.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
     wvp, wv = orc.camera_reference(W, H)
     nodes = orc.build(s, wvp)
-    g = BandGather(W, H, rank, world, device="cpu", nbuf=nbuf)
-    rows = band_row_ids(H, rank, world)
+    g = BandGather(W, H, rank, world, device="cpu", nbuf=nbuf, root_share=share)
+    rows = band_row_ids(H, rank, world, share)
     mine = torch.zeros((len(rows), W, 4))
     for k, y in enumerate(rows):   # this rank's bands, compact
         rgba, _, _ = orc.trace(s, nodes, wvp, wv, W, H, 1, y, y + 1, 1)
@@ -65,11 +65,18 @@ def _worker(rank, world, port, W, H, out_path, nbuf):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("nbuf", [1, 2])
-def test_band_gather_gloo_matches_full_frame(tmp_path, nbuf):
-    W, H, world = 160, 77, 2   # ragged: 77 rows = 9 full bands + 5 rows
+@pytest.mark.parametrize("world,nbuf,share", [(2, 1, 16), (2, 2, 16), (3, 2, 11)])
+def test_band_gather_gloo_matches_full_frame(tmp_path, world, nbuf, share):
+    """World 2 with the even deal (b % nranks), and world 3 with the uneven deal the bench uses
+    for N > 1 (rank 0 traces share/16 of another rank's bands, since it also receives and
+    assembles them): rank 0's gathered frame equals a full-frame oracle render."""
+    W, H = 160, 77   # ragged: 77 rows = 9 full bands + 5 rows
+    from raytracebvh_amd.tiles import band_row_ids
+    if share < 16:   # the deal is uneven here: rank 0 holds fewer rows than the others
+        rows = [len(band_row_ids(H, r, world, share)) for r in range(world)]
+        assert rows[0] < min(rows[1:]) and sum(rows) == H
     out = str(tmp_path / "frames.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), W, H, out, nbuf), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), W, H, out, nbuf, share), nprocs=world, join=True,
                        start_method="spawn")
     from oracle import lib as orc
     d = load_scene_fixture("Test")
@@ -83,11 +90,42 @@ def test_band_gather_gloo_matches_full_frame(tmp_path, nbuf):
     assert (got[0] != 0.5).any()   # the scene is visible in this frame
 
 
+def _deal_restated(H, n, share):
+    """Smooth weighted round-robin (include/rtbvh.h rtbvh_deal_bands), restated."""
+    nb = (H + 7) // 8
+    credit = [0] * n
+    total = share + 16 * (n - 1)
+    owner = []
+    for _ in range(nb):
+        best = 0
+        for r in range(n):
+            credit[r] += share if r == 0 else 16
+            if credit[r] > credit[best]:
+                best = r
+        credit[best] -= total
+        owner.append(best)
+    return owner
+
+
 def test_band_rows_python_matches_native():
     import raytracebvh_amd as rt
-    from raytracebvh_amd.tiles import band_row_ids
+    from raytracebvh_amd.tiles import band_ids, band_row_ids
+    L = rt.lib()
     for H in (1, 7, 8, 77, 1080, 2160):
         for n in (1, 2, 3, 8):
             ids = [band_row_ids(H, r, n) for r in range(n)]
             assert sorted(sum(ids, [])) == list(range(H))
-            assert [len(x) for x in ids] == [rt.lib().rtbvh_band_rows(H, r, n) for r in range(n)]
+            assert [len(x) for x in ids] == [L.rtbvh_band_rows(H, r, n) for r in range(n)]
+            assert [band_ids(H, r, n) for r in range(n)] == [list(range(r, (H + 7) // 8, n)) for r in range(n)]
+            for share in (0, 5, 11, 13, 16):
+                owner = _deal_restated(H, n, share)
+                bands = [band_ids(H, r, n, share) for r in range(n)]
+                assert bands == [[b for b, o in enumerate(owner) if o == r] for r in range(n)]
+                rows = [band_row_ids(H, r, n, share) for r in range(n)]
+                assert sorted(sum(rows, [])) == list(range(H))
+                assert [len(x) for x in rows] == [L.rtbvh_deal_rows(H, r, n, share) for r in range(n)]
+                if n > 1 and H >= 1080:   # rank 0's share of the bands, within one band
+                    nb = (H + 7) // 8
+                    want = nb * share / (share + 16 * (n - 1))
+                    assert abs(len(bands[0]) - want) <= 1
+    assert L.rtbvh_deal_bands(64, 0, 2, 17, None, 0) == 0   # root_share > 16: rejected

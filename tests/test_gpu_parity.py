@@ -941,9 +941,13 @@ def test_containment_failure_auto_walk_returns_the_reference_frame():
                 assert st["walk_state"] == 3 and st["walk_flags"] == 0 and st["walk_checks"] == 1
 
 
-@pytest.mark.parametrize("nranks", [2, 3, 8])
-def test_band_split_reassembles_full_frame(nranks):
+@pytest.mark.parametrize("nranks,share", [(2, 16), (3, 16), (8, 16), (3, 11), (8, 13)])
+def test_band_split_reassembles_full_frame(nranks, share):
+    """Every rank's bands under the deal (16: b % nranks; below: rank 0 takes share/16 of a
+    share, tiles.band_row_ids) put back in their rows give the full frame."""
     import torch
+
+    from raytracebvh_amd.tiles import band_row_ids
     d = load_scene_fixture("Test")
     s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
     W, H = 640, 357
@@ -953,24 +957,26 @@ def test_band_split_reassembles_full_frame(nranks):
         c.set_camera(wvp, wv)
         c.compute_bvh(W, H, 1)
         full = c.read_framebuffer()
+        c.set_band_deal(share)
         frame = np.zeros_like(full)
         for r in range(nranks):
-            rows = rt.lib().rtbvh_band_rows(H, r, nranks)
+            rows = rt.lib().rtbvh_deal_rows(H, r, nranks, share)
             buf = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda:0")
             torch.cuda.synchronize()   # the fill runs on torch's stream, not the context's
             c.trace_band_async(W, H, 1, r, nranks, buf.data_ptr())
             c.synchronize()
             got = buf.cpu().numpy()
-            ys = [y for b in range(r, (H + 7) // 8, nranks) for y in range(8 * b, min(8 * b + 8, H))]
+            ys = band_row_ids(H, r, nranks, share)
+            assert len(ys) == rows
             frame[ys] = got
     np.testing.assert_array_equal(frame, full)
 
 
-@pytest.mark.parametrize("nranks", [2, 3, 8])
-def test_assemble_bands_matches_full_frame(nranks):
+@pytest.mark.parametrize("nranks,share", [(2, 16), (3, 16), (8, 16), (3, 11), (8, 13)])
+def test_assemble_bands_matches_full_frame(nranks, share):
     """rtbvh_assemble_bands (rank 0's step of rtbvh_trace_tiles): the ranks' band buffers,
-    stacked as RCCL delivers them, give the full frame; after a band trace the context
-    reports that its framebuffer is not a frame."""
+    stacked as RCCL delivers them, give the full frame, under the even and the uneven deal;
+    after a band trace the context reports that its framebuffer is not a frame."""
     import torch
     d = load_scene_fixture("Test")
     s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
@@ -980,7 +986,8 @@ def test_assemble_bands_matches_full_frame(nranks):
         c.set_camera(*rt.camera_reference(W, H))
         c.compute_bvh(W, H, 1)
         full = c.read_framebuffer()
-        rows0 = rt.lib().rtbvh_band_rows(H, 0, nranks)
+        c.set_band_deal(share)
+        rows0 = max(rt.lib().rtbvh_deal_rows(H, r, nranks, share) for r in range(nranks))
         bands = torch.full((nranks, rows0, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
         torch.cuda.synchronize()   # the fill runs on torch's stream, not the context's
         for r in range(nranks):
