@@ -546,6 +546,33 @@ def main():
                 reb["mrays_s" + key] = round(rk / dt / 1e6, 1)
                 reb["frames" + key] = nfr
             reb["rays_per_frame"] = int(rk)
+            # the same frames pipelined: two contexts (two BVHs, two streams) take alternate frames, each
+            # frame still a full rebuild + trace of its own (Graphics.cpp:56 semantics per frame, no
+            # work skipped), frame i + 1's build running beside frame i's trace; wall time per frame
+            ctx.set_flags(rt.FLAG_TIMING | mode_flags)
+            ctx.synchronize()
+            with rt.Context(device=local, flags=mode_flags) as cb:
+                cb.set_scene(scene)
+                cb.set_camera(wvp, wv)
+                pair = [ctx, cb]
+                for c in pair:   # warm-up
+                    c.build(sync=False)
+                    c.trace(W, H, bounces, sync=False)
+                for c in pair:
+                    c.synchronize()
+                nfr = max(10, args.steps)
+                t0 = time.perf_counter()
+                for i in range(nfr):
+                    c = pair[i % 2]
+                    c.build(sync=False)
+                    c.trace(W, H, bounces, sync=False)
+                for c in pair:
+                    c.synchronize()
+                dtp = (time.perf_counter() - t0) / nfr
+                reb["ms_per_frame_pipelined2"] = round(dtp * 1e3, 4)
+                reb["mrays_s_pipelined2"] = round(rk / dtp / 1e6, 1)
+                reb["frames_pipelined2"] = nfr
+                reb["pipelined2_frames_identical"] = bool(np.array_equal(cb.read_framebuffer(), ctx.read_framebuffer()))
             extras["c5_frame_rebuild" if args.workload == "c5" else "frame_rebuild"] = reb
             ctx.set_flags(rt.FLAG_TIMING | mode_flags)
         if world == 1 and not args.no_extras and args.workload == "c5":
