@@ -10,7 +10,7 @@ scene and builds the same BVH (replicas, deterministic); the frame is split in
 over RCCL (torch.distributed "nccl") and assembled into the frame.
 
 One step = trace of this rank's bands (primary kernel + bounce kernels) + the
-RCCL gather + assembly on rank 0.  Three frames are in flight per rank (--inflight 3):
+RCCL gather + assembly on rank 0.  Four frames are in flight per rank (--inflight 4):
 frame i is traced on stream i % 3 (the context gives each caller stream a trace-buffer
 set of its own over the one BVH: rtbvh_trace_band_async), so frame i+1's primary pass
 fills the GPU while frame i's bounce walk drains its last long walks; two band buffers keep one gather in flight
@@ -239,7 +239,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip the C4 build / C3 side measurements")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the bench); gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--inflight", type=int, default=3, choices=[1, 2, 3],
+    ap.add_argument("--inflight", type=int, default=4, choices=[1, 2, 3, 4],
                     help="frames in flight per rank (one context + stream each)")
     ap.add_argument("--traversal", default="auto", choices=["auto", "reference"],
                     help="auto: report nearest-first when its frame is identical to the reference order's")

@@ -532,7 +532,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
 #ifndef RTBVH_BOUNCE_GRID
 #define RTBVH_BOUNCE_GRID (256 * BOUNCE_WAVES)
 #endif
-    const uint32_t tblocks = P < (1u << 22) ? 1024 : RTBVH_BOUNCE_GRID;
+    uint32_t tblocks = P < (1u << 22) ? 1024 : RTBVH_BOUNCE_GRID;
+    if (const char* e = getenv("RTBVH_BOUNCE_BLOCKS")) {   // tuning override (A/B runs)
+        const int v = atoi(e);
+        if (v > 0) tblocks = (uint32_t)v;
+    }
     if (records) {
         if (c->cap_rec < P) {
             drop_graph(c);
