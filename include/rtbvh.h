@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RTBVH_ABI_VERSION 4
+#define RTBVH_ABI_VERSION 5
 
 typedef enum {
     RTBVH_OK = 0,
@@ -137,6 +137,12 @@ enum {
                                              scratch, compared on the device; the key's later frames take the
                                              fast walks only if nothing differed (stats walk_state /
                                              walk_checks / walk_fallbacks) */
+    RTBVH_FLAG_BINNED_PRIMARY = 1u << 9,  /* primary rays: every leaf listed in the 32 x 32 screen tiles its box
+                                             covers (the set of orthographic primary rays a box passes is a
+                                             pixel rectangle), then per tile each listed leaf tested against
+                                             the pixels of its rectangle whose bound its min.z does not exceed,
+                                             the (t, leaf) keys in LDS: the lexicographic minimum of the
+                                             4-wide walks, with no dependent record fetches */
     RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
                                               build instead of the one-workgroup build (same output) */
     /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n
@@ -197,6 +203,9 @@ typedef struct {
     /* RTBVH_FLAG_AUTO_WALK: device checks run (one per new frame key) and those that found the
      * fast walks' frame differing from the reference order's (the key stays on the reference order) */
     uint64_t walk_checks, walk_fallbacks;
+    /* RTBVH_FLAG_COUNT_VISITS, RTBVH_FLAG_BINNED_PRIMARY: (leaf, screen tile) bin entries of the primary
+     * pass [0] and those that passed the tile's 8 x 8-block bound test [1] (one leaf-record fetch each) */
+    uint64_t bin_entries[2];
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 

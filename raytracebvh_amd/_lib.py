@@ -21,6 +21,7 @@ FLAG_TIMING, FLAG_COUNT_VISITS, FLAG_REFRACT_RECORDS, FLAG_SORT_BOUNCE, FLAG_NEA
 FLAG_PACKET_PRIMARY = 1 << 5
 FLAG_REFILL_BOUNCE = 1 << 6
 FLAG_WIDE_BVH = 1 << 7
+FLAG_BINNED_PRIMARY = 1 << 9   # primary rays by screen-tile bins of the leaves (include/rtbvh.h)
 FLAG_MULTI_KERNEL_BUILD = 1 << 16
 FLAG_AUTO_WALK = 1 << 8   # walks chosen by scene size (include/rtbvh.h)
 FLAG_SPLIT_SHIFT = 17   # trace chains: (n << FLAG_SPLIT_SHIFT), 0 = automatic
@@ -78,7 +79,8 @@ class Stats(ctypes.Structure):
                 ("trav_max_steps", ctypes.c_uint64), ("trav_steps_log2", ctypes.c_uint64 * 32),
                 ("graph_captures", ctypes.c_uint64), ("walk_flags", ctypes.c_uint32),
                 ("walk_state", ctypes.c_uint32), ("packet_steps", ctypes.c_uint64 * 2),
-                ("walk_checks", ctypes.c_uint64), ("walk_fallbacks", ctypes.c_uint64)]
+                ("walk_checks", ctypes.c_uint64), ("walk_fallbacks", ctypes.c_uint64),
+                ("bin_entries", ctypes.c_uint64 * 2)]
 
     def as_dict(self) -> dict:
         d = {}

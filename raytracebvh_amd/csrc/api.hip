@@ -86,6 +86,13 @@ struct rtbvh_ctx {
     hipStream_t sub[MAXSPLIT] = {};
     hipEvent_t ev_fork = nullptr, ev_join[MAXSPLIT] = {};
     uint32_t nsplit = 1;                      // pipelines of the last trace
+    // RTBVH_FLAG_BINNED_PRIMARY, per buffer set (chain / frames-in-flight slot): leaf footprints,
+    // tile counts / offsets, fill cursors and the bins (trace.hip k_pb_bin)
+    struct PbBufs {
+        uint4* fp = nullptr;
+        uint32_t *off = nullptr, *cur = nullptr, *bins = nullptr;
+        uint32_t cap_T = 0, cap_tiles = 0, cap_bins = 0;
+    } pb[MAXSPLIT];
     unsigned long long* d_counters = nullptr; // [64]: see rtbvh_get_stats
     bool traced = false;
     bool frame_here = false;                 // d_color holds the last trace's whole frame
@@ -273,6 +280,27 @@ rtbvh_status ensure_split_capacity(rtbvh_ctx* c, uint32_t nsplit, size_t rays) {
     return RTBVH_OK;
 }
 
+// Binned primary buffers of buffer set b for T leaves and `tiles` screen tiles.  The bins hold
+// BINS_PER_LEAF entries per leaf (C5: 1.37 tiles per leaf); a tile whose bins would pass the end is
+// traced by the 4-wide packet walk instead (trace.hip pb_gate), so the capacity is a speed knob only.
+constexpr uint32_t BINS_PER_LEAF = 3;
+rtbvh_status ensure_pb_capacity(rtbvh_ctx* c, uint32_t b, uint32_t T, uint32_t tiles) {
+    rtbvh_ctx::PbBufs& p = c->pb[b];
+    const uint32_t bins = BINS_PER_LEAF * T + 16 * tiles;
+    if (T <= p.cap_T && tiles <= p.cap_tiles && bins <= p.cap_bins && p.fp) return RTBVH_OK;
+    drop_graph(c);
+    const uint32_t nT = std::max(T, p.cap_T), nt = std::max(tiles, p.cap_tiles);
+    const uint32_t nb = std::max(BINS_PER_LEAF * nT + 16 * nt, p.cap_bins);
+    HIPC(c, dalloc(p.fp, nT));
+    HIPC(c, dalloc(p.off, (size_t)nt + 1));
+    HIPC(c, dalloc(p.cur, nt));
+    HIPC(c, dalloc(p.bins, nb));
+    p.cap_T = nT;
+    p.cap_tiles = nt;
+    p.cap_bins = nb;
+    return RTBVH_OK;
+}
+
 BuildArgs build_args(rtbvh_ctx* c) {
     BuildArgs a{};
     a.opos = c->d_opos;
@@ -422,8 +450,8 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
 // nearest-first walks (C5: 3.4x the reference order) for a frame key once a frame of that key
 // traced both ways compared equal on the device (enqueue_trace), the reference order otherwise.
 constexpr uint32_t AUTO_WALK_MAX_TRIS = 1u << 16;
-constexpr uint32_t WALK_FLAGS =
-    RTBVH_FLAG_NEAREST_FIRST | RTBVH_FLAG_PACKET_PRIMARY | RTBVH_FLAG_REFILL_BOUNCE | RTBVH_FLAG_WIDE_BVH;
+constexpr uint32_t WALK_FLAGS = RTBVH_FLAG_NEAREST_FIRST | RTBVH_FLAG_PACKET_PRIMARY | RTBVH_FLAG_REFILL_BOUNCE |
+                                RTBVH_FLAG_WIDE_BVH | RTBVH_FLAG_BINNED_PRIMARY;
 bool auto_checked(const rtbvh_ctx* c) {
     return (c->cfg.flags & RTBVH_FLAG_AUTO_WALK) && c->T > AUTO_WALK_MAX_TRIS;
 }
@@ -441,6 +469,7 @@ Walks choose_walks(uint32_t f) {
     w.primary = packet ? (wide ? PrimaryKind::PACKET_WIDE : nearest ? PrimaryKind::PACKET_NEAREST
                                                                     : PrimaryKind::PACKET_REFERENCE)
                        : (nearest ? PrimaryKind::LANE_NEAREST : PrimaryKind::LANE_REFERENCE);
+    if (f & RTBVH_FLAG_BINNED_PRIMARY) w.primary = PrimaryKind::BINNED;
     // the ray records are written by k_primary and k_bounce_shade: the split bounce path
     w.refill = (f & (RTBVH_FLAG_REFILL_BOUNCE | RTBVH_FLAG_WIDE_BVH | RTBVH_FLAG_REFRACT_RECORDS)) != 0;
     w.bounce = wide ? BounceWalk::WIDE_QUANTIZED : nearest ? BounceWalk::NEAREST : BounceWalk::REFERENCE;
@@ -517,6 +546,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (deal) {
         a.my_bands = deal->off[rank + 1] - deal->off[rank];
         a.band_list = deal->d + deal->off[rank];
+        a.band_slots = deal->d + (H + 7) / 8;
     }
     a.counters = c->d_counters + 64 * slot;
     HIPC(c, hipMemsetAsync(a.counters, 0, 64 * sizeof(unsigned long long), s));
@@ -554,7 +584,12 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t my_bands = a.my_bands;
     uint32_t nsplit = trace_split(c, (size_t)W * 8 * my_bands);
     // the coherence sort has one set of buffers; frames-in-flight slots use the chains' buffers
-    if (sort || my_bands < nsplit || slot || c->slots_used) nsplit = 1;
+    // the binned primary pass covers the rank's whole frame in one chain; its footprints pack columns
+    // and compact rows in 16 bits
+    const uint32_t rows = P / W;
+    const bool binned = wk.primary == PrimaryKind::BINNED;
+    const PrimaryKind pkind = binned && (W > 65535u || rows > 65535u) ? PrimaryKind::PACKET_WIDE : wk.primary;
+    if (sort || my_bands < nsplit || slot || c->slots_used || binned) nsplit = 1;
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
@@ -576,7 +611,15 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         uint32_t* qc = c->d_qcount + 32 * b;
         uint32_t* nx = c->d_next + (size_t)NEXT_WORDS * b;
         const bool tg = timing && g == 0;   // stage events: chain 0's kernels
-        launch_primary(ag, q[0], &qc[0], count, bounces > 0, wk.primary, sg);
+        if (pkind == PrimaryKind::BINNED) {
+            const uint32_t ntx = pb_tiles_x(W), nty = pb_tiles_y(rows);
+            st = ensure_pb_capacity(c, b, c->T, ntx * nty);
+            if (st) return st;
+            const rtbvh_ctx::PbBufs& pbb = c->pb[b];
+            const PrimBins pb{pbb.fp, pbb.off, pbb.cur, pbb.bins, pbb.cap_bins, ntx, nty};
+            launch_primary_binned(ag, pb, rows, q[0], &qc[0], count, bounces > 0, sg);
+        } else
+            launch_primary(ag, q[0], &qc[0], count, bounces > 0, pkind, sg);
         if (tg) HIPC(c, hipEventRecord(ev[1], sg));
         for (uint32_t b = 0; b < bounces; b++) {
             const uint32_t* perm = nullptr;
@@ -808,6 +851,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
         dfree(c->d_qs[g][0]); dfree(c->d_qs[g][1]); dfree(c->d_hits[g]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    for (auto& p : c->pb) { dfree(p.fp); dfree(p.off); dfree(p.cur); dfree(p.bins); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode);
@@ -1458,10 +1502,12 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
     }
     out->graph_captures = c->graph_captures;
     if (c->traced && c->d_counters) {
-        unsigned long long w[2];
+        unsigned long long w[4];
         HIPC(c, hipMemcpy(w, c->d_counters + 64 * c->last_slot + 14, sizeof(w), hipMemcpyDeviceToHost));
         out->packet_steps[0] = w[0];
         out->packet_steps[1] = w[1];
+        out->bin_entries[0] = w[2];
+        out->bin_entries[1] = w[3];
     }
     resolve_walk_check(c, true);
     out->walk_flags = c->last_walk;

@@ -103,6 +103,11 @@ struct TraceArgs {
     uint32_t band0, bstep;    // this launch traces the rank's bands band0, band0 + bstep, ... (trace chains)
     uint32_t my_bands;        // the rank's bands under the deal (rtbvh_deal_bands)
     const uint32_t* band_list;   // the rank's bands in order (a weighted deal), or null: k * nranks + rank
+    const uint32_t* band_slots;  // a weighted deal: band b is rank r's k-th band, slots[b] = r << 24 | k (or null)
+    // k_primary behind k_primary_binned: the bins' tile offsets (null: k_primary traces every block),
+    // their capacity and the tiles per row
+    const uint32_t* pb_gate;
+    uint32_t pb_cap, pb_ntx;
     Mat4 wv;
     float4* color;            // output pixels (compacted band rows when nranks > 1)
     float* intensity;         // optional, same indexing as color
@@ -119,11 +124,27 @@ struct TraceArgs {
 };
 // primary-ray walks (trace.hip k_primary): per lane in reference order / nearest-first, wave
 // packets in reference order / nearest-first, 4-wide wave packets (axis-parallel box test)
-enum class PrimaryKind { LANE_REFERENCE, LANE_NEAREST, PACKET_REFERENCE, PACKET_NEAREST, PACKET_WIDE };
+enum class PrimaryKind { LANE_REFERENCE, LANE_NEAREST, PACKET_REFERENCE, PACKET_NEAREST, PACKET_WIDE, BINNED };
 // bounce walks of the persistent refill kernel (k_bounce_trav)
 enum class BounceWalk { REFERENCE, NEAREST, WIDE_QUANTIZED };
 void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, PrimaryKind kind,
                     hipStream_t s);
+// binned primary rays (trace.hip k_primary_binned): the rank's frame in PB_TILE x PB_TILE screen
+// tiles (columns x compact band rows), every leaf listed in the tiles its box covers
+constexpr uint32_t PB_TILE = 32;
+struct PrimBins {
+    uint4* fp;        // [T] leaf footprints: {x0 | x1 << 16, row0 | row1 << 16, min.z, general}
+    uint32_t* off;    // [tiles + 1] leaves per tile, then their offsets (exclusive scan), [tiles] the total
+    uint32_t* cur;    // [tiles] fill cursors
+    uint32_t* bins;   // [cap] sorted leaf ids, tile by tile
+    uint32_t cap, ntx, nty;
+};
+inline uint32_t pb_tiles_x(uint32_t W) { return (W + PB_TILE - 1) / PB_TILE; }
+inline uint32_t pb_tiles_y(uint32_t rows) { return (rows + PB_TILE - 1) / PB_TILE; }
+// footprints, bins, the binned kernel, then k_primary (4-wide packets) behind it for any tile whose
+// bins overflowed `cap`; rows = the rank's compact rows
+void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
+                           bool count, bool emit, hipStream_t s);
 // one ray per lane bounce pass (reference order or nearest-first), shading included
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
                    uint32_t* qout_count, bool count, bool emit, bool nearest, hipStream_t s);

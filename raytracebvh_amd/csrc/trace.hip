@@ -648,8 +648,9 @@ __device__ __forceinline__ uint32_t wave_append(bool active, uint32_t* counter) 
 
 // counters: [base] internal visits, [base+1] leaf visits, [base+2] hits (base 2 primary,
 // 5 bounce), [8] stack overflows / guard trips (also added to *overflow), [9] textured hits,
-// [14] / [15] internal / leaf wave steps of the primary packet walks (one record fetch each)
-template <bool COUNT>
+// [14] / [15] internal / leaf wave steps of the primary packet walks (one record fetch each),
+// [16] / [17] bin entries of k_primary_binned and those it fetched a leaf record for
+template <bool COUNT, bool BINS = false>
 __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c, uint32_t hits, uint32_t tex,
                                              int base) {
     unsigned long long v[7] = {c.internal, c.leaf, hits, c.overflow, tex, c.wint, c.wleaf};
@@ -663,9 +664,9 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
             atomicAdd(&a.counters[base + 1], v[1]);
             atomicAdd(&a.counters[base + 2], v[2]);
             atomicAdd(&a.counters[9], v[4]);
-            if (v[5] | v[6]) {   // wave steps of the primary packet walks
-                atomicAdd(&a.counters[14], v[5]);
-                atomicAdd(&a.counters[15], v[6]);
+            if (v[5] | v[6]) {   // wave steps of the primary packet walks, or bin entries (k_primary_binned)
+                atomicAdd(&a.counters[base == 2 && BINS ? 16 : 14], v[5]);
+                atomicAdd(&a.counters[base == 2 && BINS ? 17 : 15], v[6]);
             }
         }
         if (v[3]) {
@@ -673,6 +674,51 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
             atomicAdd(a.overflow, v[3]);
         }
     }
+}
+
+// RayTraceLaunch.hlsl:40-86 for one pixel of the frame, from its closest hit (phit: sorted leaf bl
+// at distance best): colour, intensity, the RayPresent records, and the reflection ray in e
+// (returns whether it is live, i.e. traced by RayTraceReflection.hlsl:17-18)
+__device__ __forceinline__ bool primary_pixel(const TraceArgs& a, size_t out, f3 o, f3 d, bool phit, float best,
+                                              uint32_t bl, uint32_t& hits, uint32_t& tex, RayQ& e) {
+    float4 color;
+    float intensity = 0.f;
+    bool live = false;
+    if (phit) {
+        hits = 1;
+        const HitInfo h = shade_hit(a, bl, o, d, best);
+        tex = h.textured;
+        intensity = h.shininess / 1000.f * 1;   // :48 (REFLECTION_DECAY 1)
+        color = h.color;
+        if (0 < intensity) {   // traced by RayTraceReflection.hlsl:17-18 only when > INTENSITY_MIN
+            const f3 ro = add(h.hitp, mul(h.nrm, .001f));   // RAY_OFFSET .001
+            const f3 rd = normalize(reflect(d, h.nrm));
+            e.idx = (uint32_t)out;
+            e.intensity = intensity;
+            e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
+            e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
+            live = true;
+        }
+        if (a.refl_rec) {   // :48-67 (the ray is set only when the intensity is not 0)
+            const bool rr = intensity != 0;
+            put_record(a.refl_rec, out, intensity, rr, rr ? add(h.hitp, mul(h.nrm, .001f)) : o,
+                       rr ? normalize(reflect(d, h.nrm)) : d, color);
+        }
+        if (a.refr_rec) {   // :70-80, REFRACTION_DECAY 1
+            const float ri = (1.f - h.alpha) * 1;
+            const bool rr = ri != 0;
+            put_record(a.refr_rec, out, ri, rr, rr ? sub(h.hitp, mul(h.nrm, .001f)) : o,
+                       rr ? normalize(refract_hlsl(d, h.nrm, h.optical_density)) : d,
+                       make_float4(1.f, 1.f, 1.f, 1.f));
+        }
+    } else {
+        color = make_float4(.5f, .5f, .5f, 1.f);   // getBackground, :85-86
+        if (a.refl_rec) put_record(a.refl_rec, out, 0.f, false, o, d, color);   // clearRayPresent
+        if (a.refr_rec) put_record(a.refr_rec, out, 0.f, false, o, d, color);
+    }
+    a.color[out] = color;
+    if (a.intensity) a.intensity[out] = intensity;
+    return live;
 }
 
 // RayTraceLaunch.hlsl:6-93.  LIM: a run-time stack limit (rtbvh_config.stack_limit); without
@@ -688,6 +734,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t k = a.band0 + blockIdx.y * a.bstep;   // the rank's k-th band
+    // behind k_primary_binned: trace only the blocks whose 32 x 32 screen tile overflowed its bins
+    if (a.pb_gate && a.pb_gate[((k * 8) >> 5) * a.pb_ntx + blockIdx.x + 1] <= a.pb_cap) return;
     const uint32_t band = a.band_list ? a.band_list[k] : k * a.nranks + a.rank;
     const uint32_t y = band * 8 + (lane >> 3);
     const bool valid = x < a.W && y < a.H;
@@ -710,47 +758,345 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
         phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, lim, best, bl, c,
                                                    s_pst + w * PST);
     if (valid) {
-        float4 color;
-        float intensity = 0.f;
-        if (PW::PACKET ? phit
-                       : traverse<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, lim, best, bl, c)) {
-            hits = 1;
-            const HitInfo h = shade_hit(a, bl, o, d, best);
-            tex = h.textured;
-            intensity = h.shininess / 1000.f * 1;   // :48 (REFLECTION_DECAY 1)
-            color = h.color;
-            if (0 < intensity) {   // traced by RayTraceReflection.hlsl:17-18 only when > INTENSITY_MIN
-                const f3 ro = add(h.hitp, mul(h.nrm, .001f));   // RAY_OFFSET .001
-                const f3 rd = normalize(reflect(d, h.nrm));
-                e.idx = (uint32_t)out;
-                e.intensity = intensity;
-                e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
-                e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
-                live = true;
-            }
-            if (a.refl_rec) {   // :48-67 (the ray is set only when the intensity is not 0)
-                const bool rr = intensity != 0;
-                put_record(a.refl_rec, out, intensity, rr, rr ? add(h.hitp, mul(h.nrm, .001f)) : o,
-                           rr ? normalize(reflect(d, h.nrm)) : d, color);
-            }
-            if (a.refr_rec) {   // :70-80, REFRACTION_DECAY 1
-                const float ri = (1.f - h.alpha) * 1;
-                const bool rr = ri != 0;
-                put_record(a.refr_rec, out, ri, rr, rr ? sub(h.hitp, mul(h.nrm, .001f)) : o,
-                           rr ? normalize(refract_hlsl(d, h.nrm, h.optical_density)) : d,
-                           make_float4(1.f, 1.f, 1.f, 1.f));
-            }
-        } else {
-            color = make_float4(.5f, .5f, .5f, 1.f);   // getBackground, :85-86
-            if (a.refl_rec) put_record(a.refl_rec, out, 0.f, false, o, d, color);   // clearRayPresent
-            if (a.refr_rec) put_record(a.refr_rec, out, 0.f, false, o, d, color);
-        }
-        a.color[out] = color;
-        if (a.intensity) a.intensity[out] = intensity;
+        const bool h = PW::PACKET ? phit : traverse<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, lim, best, bl, c);
+        live = primary_pixel(a, out, o, d, h, best, bl, hits, tex, e);
     }
     const uint32_t slot = wave_append(emit && live, qcount);
     if (emit && live) q[slot] = e;
     flush_counts<COUNT>(a, c, hits, tex, 2);
+}
+
+// ---- binned primary rays (RTBVH_FLAG_BINNED_PRIMARY) ----------------------------------------
+// The primary rays are orthographic: pixel (x, y) is the ray o = ((x - W/2) / 4, (y - H/2) / 4, 0),
+// d = (0, 0, 1) (RayTraceLaunch.hlsl:16-30).  The 4-wide packet walk (traverse_packet4) returns, per
+// pixel, the lexicographic (t, leaf) minimum over the leaves whose box passes the axis-parallel test
+// -- min.x < o.x < max.x, min.y < o.y < max.y (the general slab test for a box whose bit is set) --
+// and whose triangle it hits; its box tests on the way down and its z pruning (min.z <= bound) only
+// skip leaves that cannot beat the bound (containment).  For a regular pixel grid the
+// set of pixels a box passes is a rectangle, computed exactly from the box (pb_range): so the same
+// minimum is found by listing every leaf in the 32 x 32 screen tiles its rectangle covers (the
+// leaf level of the BVH in slot order, two streaming passes) and, per tile, testing each listed
+// leaf against the pixels of its rectangle whose current bound its min.z does not exceed, with the
+// per-pixel (t, leaf) keys in LDS.  Order only changes which tests the bound skips, not the minimum.
+// At C5 that is 13.7M (leaf, tile) entries and 26M triangle tests per frame, all independent, in
+// place of 17.9M dependent record fetches of 8x8-pixel packets.  The outputs (shading, RayPresent
+// records, the bounce queue) are k_primary's, written per 8 x 8 sub-tile.  A tile whose bins
+// overflowed the buffer is traced by k_primary (4-wide packets) behind this kernel (pb_gate).
+
+// pixels c in [0, n) whose coordinate (c - half) / 4 passes lo < . < hi (fast: the packet walk's
+// exact test, (c - half) / 4 is exact) or, for a general box, the closed superset lo <= . <= hi
+// (the per-pixel slab test decides); [a, b], empty when a > b
+__device__ __forceinline__ void pb_range(float lo, float hi, uint32_t half, uint32_t n, bool general, int& a, int& b) {
+    const float r = 4.f * lo, R = 4.f * hi;   // exact (powers of two); +-inf past the float range
+    float fa, fb;
+    if (!general) {
+        fa = floorf(r) + 1.f;   // smallest integer > r (inexact only far outside any frame)
+        fb = ceilf(R) - 1.f;    // largest integer < R
+    } else if (r == r && R == R) {
+        fa = ceilf(fminf(r, R));
+        fb = floorf(fmaxf(r, R));
+    } else {   // a NaN corner: every pixel is a candidate
+        fa = -INFINITY;
+        fb = INFINITY;
+    }
+    a = (int)fminf(fmaxf(fa + (float)half, 0.f), (float)n);
+    b = (int)fminf(fmaxf(fb + (float)half, -1.f), (float)n - 1.f);
+}
+// k of band b in this rank's deal (its compact rows k*8 .. k*8+7), or -1 when another rank has it
+__device__ __forceinline__ int pb_band_pos(const TraceArgs& a, uint32_t b) {
+    if (a.band_slots) {
+        const uint32_t s = a.band_slots[b];
+        return (s >> 24) == a.rank ? (int)(s & 0xFFFFFFu) : -1;
+    }
+    return b % a.nranks == a.rank ? (int)(b / a.nranks) : -1;
+}
+// the rank's compact rows among image rows [y0, y1] (an order-preserving map, so a range [c0, c1])
+__device__ __forceinline__ void pb_rows(const TraceArgs& a, int y0, int y1, int& c0, int& c1) {
+    if (a.nranks == 1 || y0 > y1) { c0 = y0; c1 = y1; return; }
+    c0 = 1; c1 = 0;
+    const int b0 = y0 >> 3, b1 = y1 >> 3;
+    int b = b0;
+    for (; b <= b1; b++) {
+        const int k = pb_band_pos(a, (uint32_t)b);
+        if (k >= 0) { c0 = b == b0 ? k * 8 + (y0 & 7) : k * 8; break; }
+    }
+    if (b > b1) return;   // none of the bands is the rank's
+    for (b = b1; b >= b0; b--) {
+        const int k = pb_band_pos(a, (uint32_t)b);
+        if (k >= 0) { c1 = b == b1 ? k * 8 + (y1 & 7) : k * 8 + 7; break; }
+    }
+}
+// image row of the rank's compact row
+__device__ __forceinline__ uint32_t pb_image_row(const TraceArgs& a, uint32_t crow) {
+    const uint32_t k = crow >> 3;
+    return (a.band_list ? a.band_list[k] : k * a.nranks + a.rank) * 8 + (crow & 7u);
+}
+
+// The active lanes grouped by key, one group per distinct key of the wave: ctr[key] += the group's
+// size by its first lane, with no return value (RETURN false), or (RETURN true) every lane's
+// position among all entries of its key -- the group's base from the atomic plus the lane's rank
+// in the group.  The atomics of all groups are issued before any result is read (one round trip).
+template <bool RETURN>
+__device__ __forceinline__ uint32_t wave_add_by_key(uint32_t* ctr, uint32_t key, bool act) {
+    const uint32_t lane = lane_id();
+    uint64_t todo = __ballot(act);
+    uint32_t mine = 0, leader = 0, rank = 0;
+    while (todo) {
+        const int l = __ffsll((unsigned long long)todo) - 1;
+        const uint32_t k = __builtin_amdgcn_readlane(key, l);
+        const uint64_t m = __ballot(act && key == k) & todo;
+        if ((int)lane == l) {
+            if (RETURN) mine = atomicAdd(&ctr[k], (uint32_t)__popcll(m));
+            else (void)atomicAdd(&ctr[k], (uint32_t)__popcll(m));
+        }
+        if ((m >> lane) & 1u) {
+            leader = (uint32_t)l;
+            rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        }
+        todo &= ~m;
+    }
+    if (!RETURN) return 0;
+    return (uint32_t)__shfl((int)mine, (int)leader, 64) + rank;
+}
+
+// pass 1 (FILL false): leaf j's footprint -- its pixel columns and the rank's compact rows, min.z,
+// the general bit -- and one count per screen tile it covers; pass 2 (FILL true): j into those
+// tiles' bins at the scanned offsets.  Leaves in sorted order: a wave's leaves are neighbours in
+// space and share their tiles (one atomic per tile and wave).
+template <bool FILL>
+__global__ __launch_bounds__(BLOCK) void k_pb_bin(TraceArgs a, uint4* __restrict__ fp, uint32_t* __restrict__ off,
+                                                  uint32_t* __restrict__ cur, uint32_t* __restrict__ bins, uint32_t cap,
+                                                  uint32_t ntx) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    int x0 = 1, x1 = 0, c0 = 1, c1 = 0;
+    if (j < a.T) {
+        if (!FILL) {
+            const float4 r2 = a.leaf[4 * (size_t)j + 2], r3 = a.leaf[4 * (size_t)j + 3];   // {e2.z, tri, min.xy}, {min.z, max}
+            const bool gen = (__float_as_uint(r2.y) & LEAF_BIT) != 0;   // build.hip leaf_tri_word
+            int y0, y1;
+            pb_range(r2.z, r3.y, a.W >> 1, a.W, gen, x0, x1);
+            pb_range(r2.w, r3.z, a.H >> 1, a.H, gen, y0, y1);
+            pb_rows(a, y0, y1, c0, c1);
+            if (x0 > x1 || c0 > c1) { x0 = 1; x1 = 0; c0 = 1; c1 = 0; }
+            fp[j] = make_uint4((uint32_t)x0 | (uint32_t)x1 << 16, (uint32_t)c0 | (uint32_t)c1 << 16,
+                               __float_as_uint(r3.x), gen ? 1u : 0u);
+        } else {
+            const uint4 f = fp[j];
+            x0 = (int)(f.x & 0xFFFFu); x1 = (int)(f.x >> 16);
+            c0 = (int)(f.y & 0xFFFFu); c1 = (int)(f.y >> 16);
+        }
+    }
+    const bool some = x0 <= x1 && c0 <= c1;
+    const uint32_t tx0 = (uint32_t)x0 / PB_TILE, ty0 = (uint32_t)c0 / PB_TILE;
+    const uint32_t nxt = some ? (uint32_t)x1 / PB_TILE - tx0 + 1 : 0;
+    const uint32_t ntl = some ? nxt * ((uint32_t)c1 / PB_TILE - ty0 + 1) : 0;
+    for (uint32_t s = 0; __ballot(s < ntl) != 0; s++) {
+        const bool act = s < ntl;
+        const uint32_t t = act ? (ty0 + s / nxt) * ntx + tx0 + s % nxt : 0;
+        if (FILL) {
+            const uint32_t base = act ? off[t] : 0u;
+            const uint32_t e = base + wave_add_by_key<true>(cur, t, act);
+            if (act && e < cap) bins[e] = j;
+        } else {
+            (void)wave_add_by_key<false>(off, t, act);
+        }
+    }
+}
+
+// exclusive scan of the n tile counts in place, off[n] = the total; the fill cursors zeroed
+__global__ __launch_bounds__(1024) void k_pb_scan(uint32_t* __restrict__ off, uint32_t* __restrict__ cur, uint32_t n) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += 1024) {
+        const uint32_t i = base + tid;
+        const uint32_t v = i < n ? off[i] : 0u;
+        uint32_t x = v;   // inclusive wave scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if ((int)lane >= d) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t before = s_carry;
+        for (uint32_t k = 0; k < w; k++) before += s_w[k];
+        if (i < n) { off[i] = before + x - v; cur[i] = 0; }
+        __syncthreads();
+        if (tid == 1023) s_carry = before + x;
+        __syncthreads();
+    }
+    if (tid == 0) off[n] = s_carry;
+}
+
+// one 32 x 32 tile of the rank's frame per workgroup: the (t, leaf) keys of its pixels in LDS and
+// the largest bound of each 8 x 8 block.  A wave takes its bins in batches of 64 entries, one per lane:
+//  1. coarse: an entry whose min.z exceeds the largest bound of every block its rectangle touches
+//     cannot win any of its pixels (C5: 71% of the entries end here, before any leaf-record fetch);
+//  2. the survivors' triangles (v0, e1, e2), one vector load per lane;
+//  3. fine: per survivor, its rectangle's pixels as lanes; those whose bound min.z does not exceed go
+//     to the wave's queue of (entry, pixel) tests;
+//  4. the queue, 64 tests at a time (every lane a test: the triangle from its entry's lane by
+//     ds_bpermute, the bound re-read), folded into the keys with an LDS atomic min;
+//  then the block maxima are refreshed, and at the end the pixels take k_primary's outputs.
+// A stale bound (another wave's newer key, a maximum refreshed later) only tests more, never less.
+constexpr uint32_t PB_QCAP = 256;   // queued tests per wave
+static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 16 blocks of 8 x 8 (4 lanes each)");
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const uint4* __restrict__ fp,
+                                                             const uint32_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ bins, uint32_t cap,
+                                                             uint32_t ntx, uint32_t rows, RayQ* __restrict__ q,
+                                                             uint32_t* __restrict__ qcount, int emit) {
+    __shared__ unsigned long long s_key[PB_TILE * PB_TILE];
+    __shared__ float s_bmax[(PB_TILE / 8) * (PB_TILE / 8)];
+    __shared__ uint32_t s_q[BLOCK / 64][PB_QCAP];
+    const uint32_t* s_t = reinterpret_cast<const uint32_t*>(s_key);   // [2 i + 1]: pixel i's bound (t bits)
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.y * ntx + blockIdx.x;
+    const uint32_t X0 = blockIdx.x * PB_TILE, C0 = blockIdx.y * PB_TILE;
+    const uint32_t beg = off[tile], end = off[tile + 1];
+    if (end > cap) return;   // bins overflowed: k_primary traces this tile (pb_gate)
+    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += BLOCK) s_key[i] = NO_HIT;
+    if (threadIdx.x < (PB_TILE / 8) * (PB_TILE / 8)) s_bmax[threadIdx.x] = INFINITY;
+    __syncthreads();
+    const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
+    const f3 d = mk(0.f, 0.f, 1.f);
+    const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    uint32_t* sq = s_q[w];
+    Counts c = {0, 0, 0, 0, 0};
+    // this lane's block of the maxima refresh: block lane / 4, rows 2 (lane % 4) .. +1 of it
+    const uint32_t mb = lane >> 2, mbx = (mb % (PB_TILE / 8)) * 8, mby = (mb / (PB_TILE / 8)) * 8 + 2 * (lane & 3u);
+    for (uint32_t e0 = beg + w * 64; e0 < end; e0 += 4 * 64) {
+        const uint32_t e = e0 + lane;
+        const bool ve = e < end;
+        const uint32_t j = ve ? bins[e] : 0u;
+        const uint4 f = ve ? fp[j] : make_uint4(0, 0, 0, 0);
+        // the entry's rectangle in tile coordinates (it overlaps the tile by construction)
+        const int rx0 = max((int)(f.x & 0xFFFFu), (int)X0) - (int)X0, rx1 = min((int)(f.x >> 16), (int)X0 + 31) - (int)X0;
+        const int ry0 = max((int)(f.y & 0xFFFFu), (int)C0) - (int)C0, ry1 = min((int)(f.y >> 16), (int)C0 + 31) - (int)C0;
+        const float zmin = __uint_as_float(f.z);
+        const bool gen = f.w != 0;
+        // 1: coarse
+        bool surv = false;
+        if (ve) {
+            float m = -INFINITY;
+            for (int by = ry0 >> 3; by <= ry1 >> 3; by++)
+                for (int bx = rx0 >> 3; bx <= rx1 >> 3; bx++) m = fmaxf(m, s_bmax[by * (PB_TILE / 8) + bx]);
+            surv = gen || zmin <= m;
+        }
+        if (COUNT) {
+            const uint32_t nv = (uint32_t)__popcll(__ballot(ve)), ns = (uint32_t)__popcll(__ballot(surv));
+            if (lane == 0) { c.wint += nv; c.wleaf += ns; }
+        }
+        // 2: the survivors' triangles (and a general box)
+        float4 r0 = make_float4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
+        if (surv) {
+            const float4* r = a.leaf + 4 * (size_t)j;
+            r0 = r[0]; r1 = r[1]; r2 = r[2];
+            if (gen) r3 = r[3];
+        }
+        // 4: the queued tests, every lane one (entry lane k, pixel pi)
+        uint32_t qn = 0;
+        const auto flush = [&]() {
+            for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
+                const bool act = q0 + lane < qn;
+                const uint32_t v = act ? sq[q0 + lane] : 0u;
+                const int k = (int)(v >> 10);
+                const uint32_t pi = v & 1023u;
+#define BP(x) __uint_as_float((uint32_t)__shfl((int)__float_as_uint(x), k, 64))
+                const f3 p0 = mk(BP(r0.x), BP(r0.y), BP(r0.z)), e1 = mk(BP(r0.w), BP(r1.x), BP(r1.y));
+                const f3 e2 = mk(BP(r1.z), BP(r1.w), BP(r2.x));
+                const float kz = BP(zmin);
+                const uint32_t kj = (uint32_t)__shfl((int)j, k, 64);
+                const bool kg = __shfl((int)gen, k, 64) != 0;
+                f2v blo = {0.f, 0.f}, bhi = {0.f, 0.f};
+                float blz = 0.f, bhz = 0.f;
+                if (__ballot(act && kg)) {
+                    blo = f2v{BP(r2.z), BP(r2.w)};
+                    bhi = f2v{BP(r3.y), BP(r3.z)};
+                    blz = BP(r3.x);
+                    bhz = BP(r3.w);
+                }
+#undef BP
+                const uint32_t px = pi & (PB_TILE - 1), py = pi / PB_TILE;
+                const f3 o = mk(((float)(X0 + px) - hw) / 4.f, ((float)pb_image_row(a, C0 + (act ? py : 0u)) - hh) / 4.f,
+                                0.f);
+                bool in = false;
+                if (act) {
+                    if (kg) {   // the general slab test, no pruning (traverse_packet4's leaf step, bound aside)
+                        float tt;
+                        in = ray_box_xy(o, inv, blo, bhi, blz, bhz, false, 0.f, tt);
+                    } else {
+                        in = kz <= __uint_as_float(s_t[2 * pi + 1]);
+                    }
+                }
+                if (COUNT) c.leaf += in;
+                const float t = ray_triangle_flat(o, d, p0, e1, e2, in);
+                if (t != -1.f) atomicMin(&s_key[pi], (unsigned long long)__float_as_uint(t) << 32 | kj);
+            }
+            qn = 0;
+        };
+        // 3: fine, survivor by survivor
+        for (uint64_t todo = __ballot(surv); todo; todo &= todo - 1) {
+            const int k = __ffsll((unsigned long long)todo) - 1;
+            const bool sg = __builtin_amdgcn_readlane((int)gen, k) != 0;
+            const int sx0 = __builtin_amdgcn_readlane(rx0, k), sx1 = __builtin_amdgcn_readlane(rx1, k);
+            const int sy0 = __builtin_amdgcn_readlane(ry0, k), sy1 = __builtin_amdgcn_readlane(ry1, k);
+            const float sz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(zmin), k));
+            const int lw = sx1 - sx0 + 1;
+            const int cs = lw <= 8 ? 3 : lw <= 16 ? 4 : 5;   // lanes as 8x8, 16x4 or 32x2 pixels
+            const int col = (int)(lane & ((1u << cs) - 1)), px = sx0 + col;
+            for (int y0 = sy0; y0 <= sy1; y0 += 64 >> cs) {
+                const int y = y0 + (int)(lane >> cs);
+                const bool ok = col < lw && y <= sy1;
+                const uint32_t pi = (uint32_t)(y * (int)PB_TILE + px);
+                const bool need = ok && (sg || sz <= __uint_as_float(s_t[2 * pi + 1]));
+                const uint64_t nm = __ballot(need);
+                if (qn + (uint32_t)__popcll(nm) > PB_QCAP) flush();
+                if (need) sq[qn + (uint32_t)__popcll(nm & ((1ull << lane) - 1))] = (uint32_t)k << 10 | pi;
+                qn += (uint32_t)__popcll(nm);
+            }
+        }
+        flush();
+        // the block maxima from the keys (pixels outside the frame do not count)
+        float m = -INFINITY;
+#pragma unroll
+        for (uint32_t r = 0; r < 2; r++)
+#pragma unroll
+            for (uint32_t x = 0; x < 8; x++) {
+                const uint32_t px = mbx + x, py = mby + r;
+                if (X0 + px < a.W && C0 + py < rows) m = fmaxf(m, __uint_as_float(s_t[2 * (py * PB_TILE + px) + 1]));
+            }
+        m = fmaxf(m, __shfl_xor(m, 1, 64));
+        m = fmaxf(m, __shfl_xor(m, 2, 64));
+        if ((lane & 3u) == 0) s_bmax[mb] = m;
+    }
+    __syncthreads();
+    // k_primary's outputs, per 8 x 8 sub-tile (a wave takes sub-tiles w, w + 4, ...)
+    uint32_t hits = 0, tex = 0;
+    for (uint32_t st = w; st < (PB_TILE / 8) * (PB_TILE / 8); st += 4) {
+        const uint32_t px = (st % (PB_TILE / 8)) * 8 + (lane & 7u), py = (st / (PB_TILE / 8)) * 8 + (lane >> 3);
+        const uint32_t x = X0 + px, crow = C0 + py;
+        const bool valid = x < a.W && crow < rows;
+        bool live = false;
+        RayQ e;
+        if (valid) {
+            const uint64_t key = s_key[py * PB_TILE + px];
+            const f3 o = mk(((float)x - hw) / 4.f, ((float)pb_image_row(a, crow) - hh) / 4.f, 0.f);
+            const bool phit = key != NO_HIT;
+            uint32_t h1 = 0, t1 = 0;
+            live = primary_pixel(a, (size_t)crow * a.W + x, o, d, phit, phit ? key_t(key) : 0.f,
+                                 phit ? (uint32_t)key : 0u, h1, t1, e);
+            hits += h1;
+            tex += t1;
+        }
+        const uint32_t slot = wave_append(emit && live, qcount);
+        if (emit && live) q[slot] = e;
+    }
+    flush_counts<COUNT, true>(a, c, hits, tex, 2);
 }
 
 // RayTraceReflection.hlsl:6-62 over the compacted queue of live rays (in `perm`
@@ -1398,6 +1744,30 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
             break;
         default: launch_primary_c<0>(a, q, qcount, count, emit, grid, s); break;
     }
+}
+
+void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
+                           bool count, bool emit, hipStream_t s) {
+    if (rows == 0 || a.W == 0 || a.T == 0) return;
+    const uint32_t tiles = pb.ntx * pb.nty;
+    (void)hipMemsetAsync(pb.off, 0, ((size_t)tiles + 1) * sizeof(uint32_t), s);
+    const dim3 lg((a.T + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL((k_pb_bin<false>), lg, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
+    hipLaunchKernelGGL(k_pb_scan, dim3(1), dim3(1024), 0, s, pb.off, pb.cur, tiles);
+    hipLaunchKernelGGL((k_pb_bin<true>), lg, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
+    const dim3 grid(pb.ntx, pb.nty);
+    if (count)
+        hipLaunchKernelGGL((k_primary_binned<true>), grid, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.bins, pb.cap, pb.ntx,
+                           rows, q, qcount, (int)emit);
+    else
+        hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.bins, pb.cap,
+                           pb.ntx, rows, q, qcount, (int)emit);
+    // the tiles whose bins overflowed: the 4-wide packet walk (every other block returns at once)
+    TraceArgs g = a;
+    g.pb_gate = pb.off;
+    g.pb_cap = pb.cap;
+    g.pb_ntx = pb.ntx;
+    launch_primary(g, q, qcount, count, emit, PrimaryKind::PACKET_WIDE, s);
 }
 
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,

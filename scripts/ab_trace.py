@@ -44,6 +44,9 @@ def main():
         variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),
                     ("nearest+wide", base | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH),
                     ("wide (left-to-right packets)", base | rt.FLAG_WIDE_BVH)]
+    if os.environ.get("AB_SET") == "binned":   # primary pass: 4-wide packets vs screen-tile bins
+        base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+        variants = [("nearest-first-wide", base), ("binned", base | rt.FLAG_BINNED_PRIMARY)]
     scene = rt.synthetic(ntris, seed=0x5EED0005, half_extent=(100, 100, 50))
     ctx = rt.Context(device=0, flags=rt.FLAG_TIMING | rt.FLAG_WIDE_BVH)
     ctx.set_scene(scene)
@@ -75,7 +78,7 @@ def main():
             st = ctx.stats()
             print(json.dumps({"variant": v, "packet_steps": list(st["packet_steps"]),
                               "internal_visits": list(st["internal_visits"]), "leaf_visits": list(st["leaf_visits"]),
-                              "trav_wave_steps": st["trav_wave_steps"]}))
+                              "trav_wave_steps": st["trav_wave_steps"], "bin_entries": list(st["bin_entries"])}))
     for (v, srt), xs in res.items():
         a = np.array(xs)
         print(json.dumps({"variant": v, "primary_ms_med": float(np.median(a[:, 0])),

@@ -207,6 +207,8 @@ TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest":
                "nearest+packet+wide": rt.FLAG_NEAREST_FIRST | rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
                "packet+wide": rt.FLAG_PACKET_PRIMARY | rt.FLAG_WIDE_BVH,
                "wide+sort": rt.FLAG_WIDE_BVH | rt.FLAG_SORT_BOUNCE,
+               "binned": rt.FLAG_BINNED_PRIMARY,
+               "binned+wide+refill": WALK_FLAGS | rt.FLAG_BINNED_PRIMARY,
                "auto": rt.FLAG_AUTO_WALK}
 
 
@@ -237,7 +239,7 @@ def test_trace_matches_oracle_on_obj(name, W, H, bounces, mode):
     np.testing.assert_array_equal(inten, oint)
     assert sum(st["hits"]) == ost["hits"] and st["textured_hits"] == ost["textured_hits"]
     assert st["bounce_rays"] == ost["bounce"] and st["stack_overflows"] == 0
-    if "nearest" not in mode and "wide" not in mode and mode != "auto":   # reference order: the oracle's steps
+    if not any(k in mode for k in ("nearest", "wide", "binned", "auto")):   # reference order: the oracle's steps
         assert sum(st["internal_visits"]) == ost["internal_visits"]
         assert sum(st["leaf_visits"]) == ost["leaf_visits"]
     else:
@@ -423,7 +425,7 @@ def test_10m_tree_matches_oracle(cfg):
         assert np.array_equal(nodes[f], onodes[f]), f
 
 
-@pytest.mark.parametrize("mode", ["nearest+packet+wide", "auto"])
+@pytest.mark.parametrize("mode", ["nearest+packet+wide", "binned+wide+refill", "auto"])
 def test_c5_frame_matches_oracle_sampled_rows(mode):
     """The headline frame at full size (C5: 10M triangles, 3840x2160, primary + 1 bounce) in the
     bench's walk, against the oracle tracing 1 row in 4 on its OWN tree (OpenMP over rows):
@@ -970,6 +972,68 @@ def test_band_split_reassembles_full_frame(nranks, share):
             assert len(ys) == rows
             frame[ys] = got
     np.testing.assert_array_equal(frame, full)
+
+
+BINNED_FAST = WALK_FLAGS | rt.FLAG_BINNED_PRIMARY
+
+
+@pytest.mark.parametrize("nranks,share", [(1, 16), (2, 16), (3, 11), (8, 13)])
+def test_binned_band_traces_match_oracle(nranks, share):
+    """RTBVH_FLAG_BINNED_PRIMARY on a rank's bands (the footprints in the rank's compact rows, a
+    ragged 357-row frame, the even and the weighted deal): every rank's bands put back in their
+    rows give the oracle's frame (C4 at 1/16 size: a dense random scene, many leaves per tile)."""
+    import torch
+
+    from raytracebvh_amd.tiles import band_row_ids
+    s = rt.synthetic(200_000, seed=0x5EED0004, half_extent=(50.0, 50.0, 50.0))
+    W, H = 640, 357
+    wvp, wv = rt.camera_reference(W, H)
+    os_ = _oscene(s)
+    with rt.Context(device=0, flags=BINNED_FAST) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        nodes = c.read_bvh()
+        ofb, _, _ = orc.trace(os_, nodes, wvp, wv, W, H, 1)
+        np.testing.assert_array_equal(c.read_framebuffer(), ofb)
+        c.set_band_deal(share)
+        frame = np.zeros_like(ofb)
+        for r in range(nranks):
+            rows = rt.lib().rtbvh_deal_rows(H, r, nranks, share)
+            buf = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda:0")
+            torch.cuda.synchronize()
+            c.trace_band_async(W, H, 1, r, nranks, buf.data_ptr())
+            c.synchronize()
+            frame[band_row_ids(H, r, nranks, share)] = buf.cpu().numpy()
+    np.testing.assert_array_equal(frame, ofb)
+
+
+def test_binned_primary_bins_overflow_falls_back_to_the_packet_walk():
+    """Leaves whose boxes cover most of the frame overflow the bins (3 entries per leaf + 16 per
+    tile): the overflowed tiles are traced by the 4-wide packet walk behind the binned kernel, the
+    others by the bins, and the frame is the oracle's, pixel for pixel."""
+    rng = np.random.default_rng(11)
+    n = 3000
+    c0 = rng.uniform(-40, 40, (n, 1, 3)).astype(np.float32)
+    tri = (c0 + rng.uniform(-60, 60, (n, 3, 3)).astype(np.float32)).reshape(-1, 3)
+    verts = np.zeros((3 * n, 8), np.float32)
+    verts[:, :3] = tri
+    verts[:, 5] = 1.0
+    d = load_scene_fixture("Test")
+    s = rt.Scene(verts, np.arange(3 * n, dtype=np.uint32), np.zeros(n, np.uint32), d["material_blob"])
+    W, H = 800, 600
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=BINNED_FAST | rt.FLAG_COUNT_VISITS) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        fb = c.read_framebuffer()
+        st = c.stats()
+        nodes = c.read_bvh()
+    ofb, _, ost = orc.trace(_oscene(s), nodes, wvp, wv, W, H, 1)
+    np.testing.assert_array_equal(fb, ofb)
+    assert st["packet_steps"][0] > 0   # the packet walk traced the overflowed tiles
+    assert ost["hits"] > 100_000
 
 
 @pytest.mark.parametrize("nranks,share", [(2, 16), (3, 16), (8, 16), (3, 11), (8, 13)])

@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol():
     L = rt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.rtbvh_abi_version() == 4
+    assert L.rtbvh_abi_version() == 5
 
 
 def test_layout_sizes():
