@@ -90,8 +90,11 @@ struct rtbvh_ctx {
     // tile counts / offsets, fill cursors and the bins (trace.hip k_pb_bin)
     struct PbBufs {
         uint4* fp = nullptr;
-        uint32_t *off = nullptr, *cur = nullptr, *bins = nullptr;
+        uint32_t *off = nullptr, *cur = nullptr, *sums = nullptr;
+        uint4* bins = nullptr;
+        unsigned long long* keys = nullptr;
         uint32_t cap_T = 0, cap_tiles = 0, cap_bins = 0;
+        size_t cap_px = 0;
     } pb[MAXSPLIT];
     unsigned long long* d_counters = nullptr; // [64]: see rtbvh_get_stats
     bool traced = false;
@@ -284,16 +287,21 @@ rtbvh_status ensure_split_capacity(rtbvh_ctx* c, uint32_t nsplit, size_t rays) {
 // BINS_PER_LEAF entries per leaf (C5: 1.37 tiles per leaf); a tile whose bins would pass the end is
 // traced by the 4-wide packet walk instead (trace.hip pb_gate), so the capacity is a speed knob only.
 constexpr uint32_t BINS_PER_LEAF = 3;
-rtbvh_status ensure_pb_capacity(rtbvh_ctx* c, uint32_t b, uint32_t T, uint32_t tiles) {
+rtbvh_status ensure_pb_capacity(rtbvh_ctx* c, uint32_t b, uint32_t T, uint32_t tiles, size_t pixels) {
     rtbvh_ctx::PbBufs& p = c->pb[b];
     const uint32_t bins = BINS_PER_LEAF * T + 16 * tiles;
-    if (T <= p.cap_T && tiles <= p.cap_tiles && bins <= p.cap_bins && p.fp) return RTBVH_OK;
+    if (T <= p.cap_T && tiles <= p.cap_tiles && bins <= p.cap_bins && pixels <= p.cap_px && p.fp) return RTBVH_OK;
     drop_graph(c);
+    if (pixels > p.cap_px) {
+        HIPC(c, dalloc(p.keys, pixels));
+        p.cap_px = pixels;
+    }
     const uint32_t nT = std::max(T, p.cap_T), nt = std::max(tiles, p.cap_tiles);
     const uint32_t nb = std::max(BINS_PER_LEAF * nT + 16 * nt, p.cap_bins);
     HIPC(c, dalloc(p.fp, nT));
-    HIPC(c, dalloc(p.off, (size_t)nt + 1));
-    HIPC(c, dalloc(p.cur, nt));
+    HIPC(c, dalloc(p.off, (size_t)nt * PB_NZ + 1));
+    HIPC(c, dalloc(p.cur, (size_t)nt * PB_NZ));
+    HIPC(c, dalloc(p.sums, (size_t)nt * PB_NZ / 1024 + 1));
     HIPC(c, dalloc(p.bins, nb));
     p.cap_T = nT;
     p.cap_tiles = nt;
@@ -411,6 +419,7 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.inner = c->d_rec;
     a.leaf = c->d_leaf;
     a.qnode = c->d_qnode;
+    a.rootbox = c->d_rootbox;
     a.tclip = c->d_tclip;
     a.verts = c->d_verts;
     a.idx = c->d_idx;
@@ -613,10 +622,10 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         const bool tg = timing && g == 0;   // stage events: chain 0's kernels
         if (pkind == PrimaryKind::BINNED) {
             const uint32_t ntx = pb_tiles_x(W), nty = pb_tiles_y(rows);
-            st = ensure_pb_capacity(c, b, c->T, ntx * nty);
+            st = ensure_pb_capacity(c, b, c->T, ntx * nty, (size_t)W * rows);
             if (st) return st;
             const rtbvh_ctx::PbBufs& pbb = c->pb[b];
-            const PrimBins pb{pbb.fp, pbb.off, pbb.cur, pbb.bins, pbb.cap_bins, ntx, nty};
+            const PrimBins pb{pbb.fp, pbb.off, pbb.cur, pbb.bins, pbb.keys, pbb.sums, pbb.cap_bins, ntx, nty};
             launch_primary_binned(ag, pb, rows, q[0], &qc[0], count, bounces > 0, sg);
         } else
             launch_primary(ag, q[0], &qc[0], count, bounces > 0, pkind, sg);
@@ -851,7 +860,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
         dfree(c->d_qs[g][0]); dfree(c->d_qs[g][1]); dfree(c->d_hits[g]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    for (auto& p : c->pb) { dfree(p.fp); dfree(p.off); dfree(p.cur); dfree(p.bins); }
+    for (auto& p : c->pb) { dfree(p.fp); dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode);

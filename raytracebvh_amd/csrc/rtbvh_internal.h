@@ -108,6 +108,7 @@ struct TraceArgs {
     // their capacity and the tiles per row
     const uint32_t* pb_gate;
     uint32_t pb_cap, pb_ntx;
+    const float* rootbox;     // [6] the BVH root's box (min xyz, max xyz): the bins' depth buckets
     Mat4 wv;
     float4* color;            // output pixels (compacted band rows when nranks > 1)
     float* intensity;         // optional, same indexing as color
@@ -132,11 +133,15 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 // binned primary rays (trace.hip k_primary_binned): the rank's frame in PB_TILE x PB_TILE screen
 // tiles (columns x compact band rows), every leaf listed in the tiles its box covers
 constexpr uint32_t PB_TILE = 32;
+constexpr uint32_t PB_NZ = 16;   // depth buckets per tile: a tile's bins are listed nearest bucket first
 struct PrimBins {
     uint4* fp;        // [T] leaf footprints: {x0 | x1 << 16, row0 | row1 << 16, min.z, general}
-    uint32_t* off;    // [tiles + 1] leaves per tile, then their offsets (exclusive scan), [tiles] the total
-    uint32_t* cur;    // [tiles] fill cursors
-    uint32_t* bins;   // [cap] sorted leaf ids, tile by tile
+    uint32_t* off;    // [tiles * PB_NZ + 1] leaves per (tile, depth bucket), then their offsets (exclusive
+                      //   scan), [tiles * PB_NZ] the total
+    uint32_t* cur;    // [tiles * PB_NZ] fill cursors
+    uint4* bins;      // [cap] (footprint, leaf) entries, tile by tile, nearest depth bucket first
+    unsigned long long* keys;   // [W x rows] the frame's (t, leaf) keys (k_primary_binned -> k_pb_shade)
+    uint32_t* sums;   // [tiles * PB_NZ / 1024 + 1] the scan's block totals
     uint32_t cap, ntx, nty;
 };
 inline uint32_t pb_tiles_x(uint32_t W) { return (W + PB_TILE - 1) / PB_TILE; }

@@ -735,7 +735,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t k = a.band0 + blockIdx.y * a.bstep;   // the rank's k-th band
     // behind k_primary_binned: trace only the blocks whose 32 x 32 screen tile overflowed its bins
-    if (a.pb_gate && a.pb_gate[((k * 8) >> 5) * a.pb_ntx + blockIdx.x + 1] <= a.pb_cap) return;
+    if (a.pb_gate && a.pb_gate[(((k * 8) >> 5) * a.pb_ntx + blockIdx.x + 1) * PB_NZ] <= a.pb_cap) return;
     const uint32_t band = a.band_list ? a.band_list[k] : k * a.nranks + a.rank;
     const uint32_t y = band * 8 + (lane >> 3);
     const bool valid = x < a.W && y < a.H;
@@ -832,135 +832,198 @@ __device__ __forceinline__ uint32_t pb_image_row(const TraceArgs& a, uint32_t cr
     return (a.band_list ? a.band_list[k] : k * a.nranks + a.rank) * 8 + (crow & 7u);
 }
 
-// The active lanes grouped by key, one group per distinct key of the wave: ctr[key] += the group's
-// size by its first lane, with no return value (RETURN false), or (RETURN true) every lane's
-// position among all entries of its key -- the group's base from the atomic plus the lane's rank
-// in the group.  The atomics of all groups are issued before any result is read (one round trip).
-template <bool RETURN>
-__device__ __forceinline__ uint32_t wave_add_by_key(uint32_t* ctr, uint32_t key, bool act) {
-    const uint32_t lane = lane_id();
-    uint64_t todo = __ballot(act);
-    uint32_t mine = 0, leader = 0, rank = 0;
-    while (todo) {
-        const int l = __ffsll((unsigned long long)todo) - 1;
-        const uint32_t k = __builtin_amdgcn_readlane(key, l);
-        const uint64_t m = __ballot(act && key == k) & todo;
-        if ((int)lane == l) {
-            if (RETURN) mine = atomicAdd(&ctr[k], (uint32_t)__popcll(m));
-            else (void)atomicAdd(&ctr[k], (uint32_t)__popcll(m));
-        }
-        if ((m >> lane) & 1u) {
-            leader = (uint32_t)l;
-            rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
-        }
-        todo &= ~m;
-    }
-    if (!RETURN) return 0;
-    return (uint32_t)__shfl((int)mine, (int)leader, 64) + rank;
-}
-
 // pass 1 (FILL false): leaf j's footprint -- its pixel columns and the rank's compact rows, min.z,
-// the general bit -- and one count per screen tile it covers; pass 2 (FILL true): j into those
-// tiles' bins at the scanned offsets.  Leaves in sorted order: a wave's leaves are neighbours in
-// space and share their tiles (one atomic per tile and wave).
+// the general bit -- and its count in every (screen tile, depth bucket) bin it covers; pass 2 (FILL
+// true): the footprint with j into those bins at the scanned offsets (16-B entries: the binned pass
+// streams them with no dependent fetch).  A workgroup takes PB_LEAVES consecutive sorted leaves --
+// neighbours in space, sharing their bins -- and counts them per bin in an LDS table first, so the
+// global atomics are one per bin and workgroup instead of one per wave and bin; in pass 2 the
+// table's returned bases and LDS cursors place every entry.  A bin the full table cannot hold takes
+// a global atomic of its own (correct either way).
+constexpr uint32_t PB_LEAVES = 1024;      // leaves per workgroup (4 per thread)
+constexpr uint32_t PB_HASH = 1024;        // LDS table slots
+constexpr uint32_t PB_EMPTY = 0xFFFFFFFFu;
+__device__ __forceinline__ int pb_slot_of(uint32_t* h_key, uint32_t key, bool insert) {
+    uint32_t h = (key * 2654435761u) >> 22;   // 10 bits
+    for (int probe = 0; probe < 32; probe++) {
+        const uint32_t k = insert ? atomicCAS(&h_key[h], PB_EMPTY, key) : h_key[h];
+        if (k == key || (insert && k == PB_EMPTY)) return (int)h;
+        if (!insert && k == PB_EMPTY) return -1;
+        h = (h + 1) & (PB_HASH - 1);
+    }
+    return -1;
+}
 template <bool FILL>
 __global__ __launch_bounds__(BLOCK) void k_pb_bin(TraceArgs a, uint4* __restrict__ fp, uint32_t* __restrict__ off,
-                                                  uint32_t* __restrict__ cur, uint32_t* __restrict__ bins, uint32_t cap,
+                                                  uint32_t* __restrict__ cur, uint4* __restrict__ bins, uint32_t cap,
                                                   uint32_t ntx) {
-    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
-    int x0 = 1, x1 = 0, c0 = 1, c1 = 0;
-    if (j < a.T) {
+    __shared__ uint32_t h_key[PB_HASH], h_cnt[PB_HASH], h_base[FILL ? PB_HASH : 1];
+    for (uint32_t i = threadIdx.x; i < PB_HASH; i += BLOCK) { h_key[i] = PB_EMPTY; h_cnt[i] = 0; }
+    __syncthreads();
+    constexpr uint32_t LPT = PB_LEAVES / BLOCK;
+    uint4 f[LPT];
+    uint32_t zb[LPT];
+    const float zlo = a.rootbox[2], zhi = a.rootbox[5];
+#pragma unroll
+    for (uint32_t i = 0; i < LPT; i++) {
+        const uint32_t j = blockIdx.x * PB_LEAVES + i * BLOCK + threadIdx.x;
+        f[i] = make_uint4(1, 1, 0, 0);   // empty: x0 = 1 > x1 = 0
+        if (j < a.T) {
+            if (!FILL) {
+                const float4 r2 = a.leaf[4 * (size_t)j + 2], r3 = a.leaf[4 * (size_t)j + 3];   // {e2.z, tri, min.xy}, {min.z, max}
+                const bool gen = (__float_as_uint(r2.y) & LEAF_BIT) != 0;   // build.hip leaf_tri_word
+                int x0, x1, y0, y1, c0, c1;
+                pb_range(r2.z, r3.y, a.W >> 1, a.W, gen, x0, x1);
+                pb_range(r2.w, r3.z, a.H >> 1, a.H, gen, y0, y1);
+                pb_rows(a, y0, y1, c0, c1);
+                if (x0 > x1 || c0 > c1) { x0 = 1; x1 = 0; c0 = 1; c1 = 0; }
+                f[i] = make_uint4((uint32_t)x0 | (uint32_t)x1 << 16, (uint32_t)c0 | (uint32_t)c1 << 16,
+                                  __float_as_uint(r3.x), gen ? 1u : 0u);
+                fp[j] = f[i];
+            } else {
+                f[i] = fp[j];
+            }
+        }
+        // the depth bucket of min.z in the root box's depth range (general boxes first: they always test)
+        const float u = (__uint_as_float(f[i].z) - zlo) / (zhi - zlo) * (float)PB_NZ;
+        zb[i] = f[i].w ? 0u : (uint32_t)fminf(fmaxf(u, 0.f), (float)(PB_NZ - 1));   // NaN: 0
+    }
+    // the (leaf, bin) pairs of item i, visited by `body(key)`
+    const auto pairs = [&](uint32_t i, auto&& body) {
+        const uint32_t x0 = f[i].x & 0xFFFFu, x1 = f[i].x >> 16, c0 = f[i].y & 0xFFFFu, c1 = f[i].y >> 16;
+        if (x0 > x1 || c0 > c1) return;
+        for (uint32_t ty = c0 / PB_TILE; ty <= c1 / PB_TILE; ty++)
+            for (uint32_t tx = x0 / PB_TILE; tx <= x1 / PB_TILE; tx++) body((ty * ntx + tx) * PB_NZ + zb[i]);
+    };
+    // counts per bin in the table (or straight to the global count when the table is full)
+#pragma unroll
+    for (uint32_t i = 0; i < LPT; i++)
+        pairs(i, [&](uint32_t key) {
+            const int sl = pb_slot_of(h_key, key, true);
+            if (sl >= 0) atomicAdd(&h_cnt[sl], 1u);
+            else if (!FILL) atomicAdd(&off[key], 1u);
+        });
+    __syncthreads();
+    for (uint32_t sl = threadIdx.x; sl < PB_HASH; sl += BLOCK) {
+        const uint32_t key = h_key[sl];
+        if (key == PB_EMPTY) continue;
         if (!FILL) {
-            const float4 r2 = a.leaf[4 * (size_t)j + 2], r3 = a.leaf[4 * (size_t)j + 3];   // {e2.z, tri, min.xy}, {min.z, max}
-            const bool gen = (__float_as_uint(r2.y) & LEAF_BIT) != 0;   // build.hip leaf_tri_word
-            int y0, y1;
-            pb_range(r2.z, r3.y, a.W >> 1, a.W, gen, x0, x1);
-            pb_range(r2.w, r3.z, a.H >> 1, a.H, gen, y0, y1);
-            pb_rows(a, y0, y1, c0, c1);
-            if (x0 > x1 || c0 > c1) { x0 = 1; x1 = 0; c0 = 1; c1 = 0; }
-            fp[j] = make_uint4((uint32_t)x0 | (uint32_t)x1 << 16, (uint32_t)c0 | (uint32_t)c1 << 16,
-                               __float_as_uint(r3.x), gen ? 1u : 0u);
+            atomicAdd(&off[key], h_cnt[sl]);
         } else {
-            const uint4 f = fp[j];
-            x0 = (int)(f.x & 0xFFFFu); x1 = (int)(f.x >> 16);
-            c0 = (int)(f.y & 0xFFFFu); c1 = (int)(f.y >> 16);
+            h_base[sl] = off[key] + atomicAdd(&cur[key], h_cnt[sl]);
+            h_cnt[sl] = 0;
         }
     }
-    const bool some = x0 <= x1 && c0 <= c1;
-    const uint32_t tx0 = (uint32_t)x0 / PB_TILE, ty0 = (uint32_t)c0 / PB_TILE;
-    const uint32_t nxt = some ? (uint32_t)x1 / PB_TILE - tx0 + 1 : 0;
-    const uint32_t ntl = some ? nxt * ((uint32_t)c1 / PB_TILE - ty0 + 1) : 0;
-    for (uint32_t s = 0; __ballot(s < ntl) != 0; s++) {
-        const bool act = s < ntl;
-        const uint32_t t = act ? (ty0 + s / nxt) * ntx + tx0 + s % nxt : 0;
-        if (FILL) {
-            const uint32_t base = act ? off[t] : 0u;
-            const uint32_t e = base + wave_add_by_key<true>(cur, t, act);
-            if (act && e < cap) bins[e] = j;
-        } else {
-            (void)wave_add_by_key<false>(off, t, act);
-        }
+    if (!FILL) return;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < LPT; i++) {
+        const uint32_t j = blockIdx.x * PB_LEAVES + i * BLOCK + threadIdx.x;
+        const uint4 entry = make_uint4(f[i].x, f[i].y, f[i].z, j | (f[i].w ? LEAF_BIT : 0u));
+        pairs(i, [&](uint32_t key) {
+            const int sl = pb_slot_of(h_key, key, false);
+            const uint32_t e = sl >= 0 ? h_base[sl] + atomicAdd(&h_cnt[sl], 1u) : off[key] + atomicAdd(&cur[key], 1u);
+            if (e < cap) bins[e] = entry;
+        });
     }
 }
 
-// exclusive scan of the n tile counts in place, off[n] = the total; the fill cursors zeroed
-__global__ __launch_bounds__(1024) void k_pb_scan(uint32_t* __restrict__ off, uint32_t* __restrict__ cur, uint32_t n) {
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_carry;
+// exclusive scan of the n bin counts in place, off[n] = the total, the fill cursors zeroed: blocks of
+// PB_SCAN counts, first each block's total (k_pb_sums), then each block adds the totals of the blocks
+// before it to its own scan (k_pb_scan; C5: 130,560 counts, 128 blocks)
+constexpr uint32_t PB_SCAN = 1024;
+__device__ __forceinline__ uint32_t block_sum_1024(uint32_t v, uint32_t* s_w) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    if (tid == 0) s_carry = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < n; base += 1024) {
-        const uint32_t i = base + tid;
-        const uint32_t v = i < n ? off[i] : 0u;
-        uint32_t x = v;   // inclusive wave scan
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if ((int)lane >= d) x += y;
-        }
-        if (lane == 63) s_w[w] = x;
-        __syncthreads();
-        uint32_t before = s_carry;
-        for (uint32_t k = 0; k < w; k++) before += s_w[k];
-        if (i < n) { off[i] = before + x - v; cur[i] = 0; }
-        __syncthreads();
-        if (tid == 1023) s_carry = before + x;
-        __syncthreads();
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane == 0) s_w[w] = v;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) t += s_w[k];
+    return t;
+}
+__global__ __launch_bounds__(1024) void k_pb_sums(const uint32_t* __restrict__ off, uint32_t* __restrict__ sums,
+                                                  uint32_t n) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t i = blockIdx.x * PB_SCAN + threadIdx.x;
+    const uint32_t t = block_sum_1024(i < n ? off[i] : 0u, s_w);
+    if (threadIdx.x == 0) sums[blockIdx.x] = t;
+}
+__global__ __launch_bounds__(1024) void k_pb_scan(uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                                                  const uint32_t* __restrict__ sums, uint32_t n) {
+    __shared__ uint32_t s_w[16], s_v[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    // the totals of the blocks before this one
+    uint32_t p = 0;
+    for (uint32_t k = tid; k < blockIdx.x; k += 1024) p += sums[k];
+    const uint32_t before = block_sum_1024(p, s_v);
+    const uint32_t i = blockIdx.x * PB_SCAN + tid;
+    const uint32_t v = i < n ? off[i] : 0u;
+    uint32_t x = v;   // inclusive scan over the wave, then over the waves
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if ((int)lane >= d) x += y;
     }
-    if (tid == 0) off[n] = s_carry;
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t run = before + x - v;
+    for (uint32_t k = 0; k < w; k++) run += s_w[k];
+    if (i < n) { off[i] = run; cur[i] = 0; }
+    if (i == n - 1) off[n] = run + v;
 }
 
 // one 32 x 32 tile of the rank's frame per workgroup: the (t, leaf) keys of its pixels in LDS and
-// the largest bound of each 8 x 8 block.  A wave takes its bins in batches of 64 entries, one per lane:
+// the largest bound of each 8 x 8 block.  The waves claim the tile's bins in batches of 64 entries
+// (one per lane; nearest depth bucket first; the next batch's entries load while this one runs):
 //  1. coarse: an entry whose min.z exceeds the largest bound of every block its rectangle touches
-//     cannot win any of its pixels (C5: 71% of the entries end here, before any leaf-record fetch);
+//     cannot win any of its pixels (C5: two thirds of the entries end here, before any leaf fetch);
 //  2. the survivors' triangles (v0, e1, e2), one vector load per lane;
 //  3. fine: per survivor, its rectangle's pixels as lanes; those whose bound min.z does not exceed go
 //     to the wave's queue of (entry, pixel) tests;
 //  4. the queue, 64 tests at a time (every lane a test: the triangle from its entry's lane by
 //     ds_bpermute, the bound re-read), folded into the keys with an LDS atomic min;
-//  then the block maxima are refreshed, and at the end the pixels take k_primary's outputs.
+//  then the block maxima are refreshed.  The keys go to `keys` (the frame's (t, leaf) per pixel);
+//  k_pb_shade turns them into k_primary's outputs.
 // A stale bound (another wave's newer key, a maximum refreshed later) only tests more, never less.
 constexpr uint32_t PB_QCAP = 256;   // queued tests per wave
+// a pixel's key slot: rows 36 keys apart, so that the 8 rows of an 8 x 8 lane block fall in different
+// LDS banks (a 32-key row is 64 words: every row on the same banks, 8-way conflicts)
+constexpr uint32_t PB_KS = 36;
+__device__ __forceinline__ uint32_t pb_slot(uint32_t pi) { return (pi / PB_TILE) * PB_KS + (pi % PB_TILE); }
 static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 16 blocks of 8 x 8 (4 lanes each)");
+// RTBVH_PB_PROF builds: shader-clock cycles per phase of k_primary_binned, summed over the waves into
+// counters[32..39] (read back as rtbvh_stats.trav_steps_log2[0..7]; scripts/pb_phases.py)
+#ifdef RTBVH_PB_PROF
+#define PB_T(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); const uint64_t _t = clock64(); pt[i] += _t - pt_last; pt_last = _t; } while (0)
+#else
+#define PB_T(i) do { } while (0)
+#endif
 template <bool COUNT>
-__global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const uint4* __restrict__ fp,
-                                                             const uint32_t* __restrict__ off,
-                                                             const uint32_t* __restrict__ bins, uint32_t cap,
-                                                             uint32_t ntx, uint32_t rows, RayQ* __restrict__ q,
-                                                             uint32_t* __restrict__ qcount, int emit) {
-    __shared__ unsigned long long s_key[PB_TILE * PB_TILE];
+__global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
+                                                             const uint4* __restrict__ bins, uint32_t cap,
+                                                             uint32_t ntx, uint32_t rows,
+                                                             unsigned long long* __restrict__ keys) {
+    __shared__ unsigned long long s_key[PB_TILE * PB_KS];
     __shared__ float s_bmax[(PB_TILE / 8) * (PB_TILE / 8)];
     __shared__ uint32_t s_q[BLOCK / 64][PB_QCAP];
-    const uint32_t* s_t = reinterpret_cast<const uint32_t*>(s_key);   // [2 i + 1]: pixel i's bound (t bits)
+    __shared__ uint32_t s_next;
+    const uint32_t* s_t = reinterpret_cast<const uint32_t*>(s_key);   // [2 slot + 1]: a pixel's bound (t bits)
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.y * ntx + blockIdx.x;
     const uint32_t X0 = blockIdx.x * PB_TILE, C0 = blockIdx.y * PB_TILE;
-    const uint32_t beg = off[tile], end = off[tile + 1];
+    const uint32_t beg = off[tile * PB_NZ], end = off[(tile + 1) * PB_NZ];
     if (end > cap) return;   // bins overflowed: k_primary traces this tile (pb_gate)
-    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += BLOCK) s_key[i] = NO_HIT;
+#ifdef RTBVH_PB_PROF
+    uint64_t pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt_last = clock64();
+#endif
+    // keys of the pixels outside the frame (or the rank's rows) start at t = 0: no entry covers them,
+    // and they never raise a block's largest bound
+    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_KS; i += BLOCK)
+        s_key[i] = X0 + i % PB_KS < a.W && C0 + i / PB_KS < rows ? NO_HIT : 0ull;
     if (threadIdx.x < (PB_TILE / 8) * (PB_TILE / 8)) s_bmax[threadIdx.x] = INFINITY;
+    if (threadIdx.x == 0) s_next = 0;
     __syncthreads();
     const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
     const f3 d = mk(0.f, 0.f, 1.f);
@@ -969,16 +1032,31 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
     Counts c = {0, 0, 0, 0, 0};
     // this lane's block of the maxima refresh: block lane / 4, rows 2 (lane % 4) .. +1 of it
     const uint32_t mb = lane >> 2, mbx = (mb % (PB_TILE / 8)) * 8, mby = (mb / (PB_TILE / 8)) * 8 + 2 * (lane & 3u);
-    for (uint32_t e0 = beg + w * 64; e0 < end; e0 += 4 * 64) {
-        const uint32_t e = e0 + lane;
-        const bool ve = e < end;
-        const uint32_t j = ve ? bins[e] : 0u;
-        const uint4 f = ve ? fp[j] : make_uint4(0, 0, 0, 0);
+    const uint32_t nbatch = (end - beg + 63) / 64;
+    const auto claim = [&]() {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(&s_next, 1u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane(b);
+    };
+    const auto fetch = [&](uint32_t b) {
+        const uint32_t e = beg + b * 64 + lane;
+        return b < nbatch && e < end ? bins[e] : make_uint4(0, 0, 0, INVALID);
+    };
+    uint32_t bn = claim();
+    uint4 fn = fetch(bn);
+    PB_T(7);
+    while (bn < nbatch) {
+        const uint4 f = fn;
+        bn = claim();
+        fn = fetch(bn);   // the next batch's entries, in flight during this one
+        const bool ve = f.w != INVALID;
+        const uint32_t j = f.w & ~LEAF_BIT;
+        const bool gen = ve && (f.w & LEAF_BIT) != 0;
         // the entry's rectangle in tile coordinates (it overlaps the tile by construction)
         const int rx0 = max((int)(f.x & 0xFFFFu), (int)X0) - (int)X0, rx1 = min((int)(f.x >> 16), (int)X0 + 31) - (int)X0;
         const int ry0 = max((int)(f.y & 0xFFFFu), (int)C0) - (int)C0, ry1 = min((int)(f.y >> 16), (int)C0 + 31) - (int)C0;
         const float zmin = __uint_as_float(f.z);
-        const bool gen = f.w != 0;
+        PB_T(0);
         // 1: coarse
         bool surv = false;
         if (ve) {
@@ -991,16 +1069,17 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
             const uint32_t nv = (uint32_t)__popcll(__ballot(ve)), ns = (uint32_t)__popcll(__ballot(surv));
             if (lane == 0) { c.wint += nv; c.wleaf += ns; }
         }
-        // 2: the survivors' triangles (and a general box)
-        float4 r0 = make_float4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
+        // 2: the survivors' triangles
+        float4 r0 = make_float4(0, 0, 0, 0), r1 = r0, r2 = r0;
         if (surv) {
             const float4* r = a.leaf + 4 * (size_t)j;
             r0 = r[0]; r1 = r[1]; r2 = r[2];
-            if (gen) r3 = r[3];
         }
+        PB_T(1);
         // 4: the queued tests, every lane one (entry lane k, pixel pi)
         uint32_t qn = 0;
         const auto flush = [&]() {
+            PB_T(3);
             for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
                 const bool act = q0 + lane < qn;
                 const uint32_t v = act ? sq[q0 + lane] : 0u;
@@ -1010,34 +1089,29 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
                 const f3 p0 = mk(BP(r0.x), BP(r0.y), BP(r0.z)), e1 = mk(BP(r0.w), BP(r1.x), BP(r1.y));
                 const f3 e2 = mk(BP(r1.z), BP(r1.w), BP(r2.x));
                 const float kz = BP(zmin);
-                const uint32_t kj = (uint32_t)__shfl((int)j, k, 64);
-                const bool kg = __shfl((int)gen, k, 64) != 0;
-                f2v blo = {0.f, 0.f}, bhi = {0.f, 0.f};
-                float blz = 0.f, bhz = 0.f;
-                if (__ballot(act && kg)) {
-                    blo = f2v{BP(r2.z), BP(r2.w)};
-                    bhi = f2v{BP(r3.y), BP(r3.z)};
-                    blz = BP(r3.x);
-                    bhz = BP(r3.w);
-                }
 #undef BP
-                const uint32_t px = pi & (PB_TILE - 1), py = pi / PB_TILE;
+                const uint32_t kw = (uint32_t)__shfl((int)f.w, k, 64);
+                const uint32_t kj = kw & ~LEAF_BIT;
+                const bool kg = (kw & LEAF_BIT) != 0;
+                const uint32_t px = pi % PB_TILE, py = pi / PB_TILE;
                 const f3 o = mk(((float)(X0 + px) - hw) / 4.f, ((float)pb_image_row(a, C0 + (act ? py : 0u)) - hh) / 4.f,
                                 0.f);
                 bool in = false;
                 if (act) {
-                    if (kg) {   // the general slab test, no pruning (traverse_packet4's leaf step, bound aside)
+                    if (kg) {   // the general slab test on the leaf's box, no pruning (traverse_packet4's leaf step)
+                        const float4 b2 = a.leaf[4 * (size_t)kj + 2], b3 = a.leaf[4 * (size_t)kj + 3];
                         float tt;
-                        in = ray_box_xy(o, inv, blo, bhi, blz, bhz, false, 0.f, tt);
+                        in = ray_box_xy(o, inv, f2v{b2.z, b2.w}, f2v{b3.y, b3.z}, b3.x, b3.w, false, 0.f, tt);
                     } else {
-                        in = kz <= __uint_as_float(s_t[2 * pi + 1]);
+                        in = kz <= __uint_as_float(s_t[2 * pb_slot(pi) + 1]);
                     }
                 }
                 if (COUNT) c.leaf += in;
                 const float t = ray_triangle_flat(o, d, p0, e1, e2, in);
-                if (t != -1.f) atomicMin(&s_key[pi], (unsigned long long)__float_as_uint(t) << 32 | kj);
+                if (t != -1.f) atomicMin(&s_key[pb_slot(pi)], (unsigned long long)__float_as_uint(t) << 32 | kj);
             }
             qn = 0;
+            PB_T(4);
         };
         // 3: fine, survivor by survivor
         for (uint64_t todo = __ballot(surv); todo; todo &= todo - 1) {
@@ -1053,7 +1127,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
                 const int y = y0 + (int)(lane >> cs);
                 const bool ok = col < lw && y <= sy1;
                 const uint32_t pi = (uint32_t)(y * (int)PB_TILE + px);
-                const bool need = ok && (sg || sz <= __uint_as_float(s_t[2 * pi + 1]));
+                const bool need = ok && (sg || sz <= __uint_as_float(s_t[2 * pb_slot(pi) + 1]));
                 const uint64_t nm = __ballot(need);
                 if (qn + (uint32_t)__popcll(nm) > PB_QCAP) flush();
                 if (need) sq[qn + (uint32_t)__popcll(nm & ((1ull << lane) - 1))] = (uint32_t)k << 10 | pi;
@@ -1061,42 +1135,108 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
             }
         }
         flush();
-        // the block maxima from the keys (pixels outside the frame do not count)
-        float m = -INFINITY;
+        PB_T(3);
+        // the block maxima from the keys (pixels outside the frame hold t = 0)
+        float m = 0.f;
+        const uint32_t* bt = s_t + 2 * (mby * PB_KS + mbx) + 1;
 #pragma unroll
         for (uint32_t r = 0; r < 2; r++)
 #pragma unroll
-            for (uint32_t x = 0; x < 8; x++) {
-                const uint32_t px = mbx + x, py = mby + r;
-                if (X0 + px < a.W && C0 + py < rows) m = fmaxf(m, __uint_as_float(s_t[2 * (py * PB_TILE + px) + 1]));
-            }
+            for (uint32_t x = 0; x < 8; x++) m = fmaxf(m, __uint_as_float(bt[2 * (r * PB_KS + x)]));
         m = fmaxf(m, __shfl_xor(m, 1, 64));
         m = fmaxf(m, __shfl_xor(m, 2, 64));
         if ((lane & 3u) == 0) s_bmax[mb] = m;
+        PB_T(5);
     }
     __syncthreads();
-    // k_primary's outputs, per 8 x 8 sub-tile (a wave takes sub-tiles w, w + 4, ...)
-    uint32_t hits = 0, tex = 0;
-    for (uint32_t st = w; st < (PB_TILE / 8) * (PB_TILE / 8); st += 4) {
-        const uint32_t px = (st % (PB_TILE / 8)) * 8 + (lane & 7u), py = (st / (PB_TILE / 8)) * 8 + (lane >> 3);
-        const uint32_t x = X0 + px, crow = C0 + py;
-        const bool valid = x < a.W && crow < rows;
+    // the tile's keys, row segments of 32 pixels
+    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += BLOCK) {
+        const uint32_t px = i % PB_TILE, py = i / PB_TILE;
+        if (X0 + px < a.W && C0 + py < rows) keys[(size_t)(C0 + py) * a.W + X0 + px] = s_key[py * PB_KS + px];
+    }
+#ifdef RTBVH_PB_PROF
+    PB_T(6);
+    if (lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&a.counters[32 + i], (unsigned long long)pt[i]);
+#endif
+    flush_counts<COUNT, true>(a, c, 0, 0, 2);
+}
+
+// k_primary's outputs from the binned pass's keys, one 32 x 32 tile per block (a wave takes its
+// 8 x 8 sub-tiles w, w + 4, ...).  The reflection rays go to the bounce queue with ONE atomic per
+// block: its live rays are counted first (hit and shininess > 0, RayTraceLaunch.hlsl:48 and
+// RayTraceReflection.hlsl:17-18), the block's base claimed, then every pixel shaded and its ray
+// written at base + its rank.  (One atomic per wave -- k_primary's wave_append -- is 130K claims on
+// one counter per C5 frame, ~1.2 ms at the ~100 claims per us one address takes.)  Tiles whose bins
+// overflowed return (k_primary traced them).
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_pb_shade(TraceArgs a, const uint32_t* __restrict__ off, uint32_t cap,
+                                                    uint32_t ntx, uint32_t rows,
+                                                    const unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
+                                                    uint32_t* __restrict__ qcount, int emit) {
+    __shared__ uint32_t s_cnt[(PB_TILE / 8) * (PB_TILE / 8)];
+    __shared__ uint32_t s_base;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.y * ntx + blockIdx.x;
+    if (off[(tile + 1) * PB_NZ] > cap) return;
+    const uint32_t X0 = blockIdx.x * PB_TILE, C0 = blockIdx.y * PB_TILE;
+    constexpr uint32_t NST = (PB_TILE / 8) * (PB_TILE / 8) / (BLOCK / 64);   // sub-tiles per wave
+    uint32_t x[NST], crow[NST];
+    uint64_t key[NST];
+    bool valid[NST];
+    uint64_t livem[NST];
+#pragma unroll
+    for (uint32_t i = 0; i < NST; i++) {
+        const uint32_t st = w + i * (BLOCK / 64);
+        x[i] = X0 + (st % (PB_TILE / 8)) * 8 + (lane & 7u);
+        crow[i] = C0 + (st / (PB_TILE / 8)) * 8 + (lane >> 3);
+        valid[i] = x[i] < a.W && crow[i] < rows;
+        key[i] = valid[i] ? keys[(size_t)crow[i] * a.W + x[i]] : NO_HIT;
+    }
+    // the live reflection rays: hit, and the hit material's shininess > 0
+#pragma unroll
+    for (uint32_t i = 0; i < NST; i++) {
         bool live = false;
-        RayQ e;
-        if (valid) {
-            const uint64_t key = s_key[py * PB_TILE + px];
-            const f3 o = mk(((float)x - hw) / 4.f, ((float)pb_image_row(a, crow) - hh) / 4.f, 0.f);
-            const bool phit = key != NO_HIT;
+        if (emit && key[i] != NO_HIT) {
+            const uint32_t tri = __float_as_uint(a.leaf[4 * (size_t)(uint32_t)key[i] + 2].y) & ~LEAF_BIT;
+            const uint32_t mi = TCS == 4 ? __float_as_uint(a.tclip[TCS * (size_t)tri + 3].w) : a.matidx[tri];
+            live = 0 < a.mats[mi].shininess / 1000.f * 1;
+        }
+        livem[i] = __ballot(live);
+        if (lane == 0) s_cnt[w + i * (BLOCK / 64)] = (uint32_t)__popcll(livem[i]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < (PB_TILE / 8) * (PB_TILE / 8); k++) {
+            const uint32_t v = s_cnt[k];
+            s_cnt[k] = run;
+            run += v;
+        }
+        s_base = run && emit ? atomicAdd(qcount, run) : 0u;
+    }
+    __syncthreads();
+    const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
+    uint32_t hits = 0, tex = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < NST; i++) {
+        if (valid[i]) {
+            const f3 o = mk(((float)x[i] - hw) / 4.f, ((float)pb_image_row(a, crow[i]) - hh) / 4.f, 0.f);
+            const bool phit = key[i] != NO_HIT;
             uint32_t h1 = 0, t1 = 0;
-            live = primary_pixel(a, (size_t)crow * a.W + x, o, d, phit, phit ? key_t(key) : 0.f,
-                                 phit ? (uint32_t)key : 0u, h1, t1, e);
+            RayQ e;
+            const bool live = primary_pixel(a, (size_t)crow[i] * a.W + x[i], o, mk(0.f, 0.f, 1.f), phit,
+                                            phit ? key_t(key[i]) : 0.f, phit ? (uint32_t)key[i] : 0u, h1, t1, e);
             hits += h1;
             tex += t1;
+            if (emit && live)
+                q[s_base + s_cnt[w + i * (BLOCK / 64)] + (uint32_t)__popcll(livem[i] & ((1ull << lane) - 1))] = e;
         }
-        const uint32_t slot = wave_append(emit && live, qcount);
-        if (emit && live) q[slot] = e;
     }
-    flush_counts<COUNT, true>(a, c, hits, tex, 2);
+    if (COUNT) {
+        Counts c = {0, 0, 0, 0, 0};
+        flush_counts<COUNT>(a, c, hits, tex, 2);
+    }
 }
 
 // RayTraceReflection.hlsl:6-62 over the compacted queue of live rays (in `perm`
@@ -1749,19 +1889,27 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
                            bool count, bool emit, hipStream_t s) {
     if (rows == 0 || a.W == 0 || a.T == 0) return;
-    const uint32_t tiles = pb.ntx * pb.nty;
-    (void)hipMemsetAsync(pb.off, 0, ((size_t)tiles + 1) * sizeof(uint32_t), s);
-    const dim3 lg((a.T + BLOCK - 1) / BLOCK);
+    const uint32_t keys = pb.ntx * pb.nty * PB_NZ;
+    (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
+    const dim3 lg((a.T + PB_LEAVES - 1) / PB_LEAVES);
     hipLaunchKernelGGL((k_pb_bin<false>), lg, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
-    hipLaunchKernelGGL(k_pb_scan, dim3(1), dim3(1024), 0, s, pb.off, pb.cur, tiles);
+    const uint32_t sb = (keys + PB_SCAN - 1) / PB_SCAN;
+    hipLaunchKernelGGL(k_pb_sums, dim3(sb), dim3(PB_SCAN), 0, s, pb.off, pb.sums, keys);
+    hipLaunchKernelGGL(k_pb_scan, dim3(sb), dim3(PB_SCAN), 0, s, pb.off, pb.cur, pb.sums, keys);
     hipLaunchKernelGGL((k_pb_bin<true>), lg, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
     const dim3 grid(pb.ntx, pb.nty);
     if (count)
-        hipLaunchKernelGGL((k_primary_binned<true>), grid, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.bins, pb.cap, pb.ntx,
-                           rows, q, qcount, (int)emit);
+        hipLaunchKernelGGL((k_primary_binned<true>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
+                           pb.keys);
     else
-        hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.bins, pb.cap,
-                           pb.ntx, rows, q, qcount, (int)emit);
+        hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
+                           pb.keys);
+    if (count)
+        hipLaunchKernelGGL((k_pb_shade<true>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
+                           qcount, (int)emit);
+    else
+        hipLaunchKernelGGL((k_pb_shade<false>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
+                           qcount, (int)emit);
     // the tiles whose bins overflowed: the 4-wide packet walk (every other block returns at once)
     TraceArgs g = a;
     g.pb_gate = pb.off;
