@@ -82,6 +82,16 @@ def make_scene(rt, wl):
     return rt.synthetic(wl["ntris"], seed=wl["seed"], half_extent=wl["half"])
 
 
+def binned_bytes(st, ntris):
+    """Algorithmic bytes of the binned primary pass (RTBVH_FLAG_BINNED_PRIMARY): the
+    leaf records' 64-B lines once (footprints), the 16-B footprints written and read back, the 16-B
+    bin entries written and streamed, the 48-B triangle of every entry past the block test, the 8-B
+    per-pixel keys written and read, then the pixel outputs and the bounce queue."""
+    entries, survivors = st["bin_entries"]
+    return (L_REC * ntris + 2 * 16 * ntris + 2 * 16 * entries + 48 * survivors + 2 * 8 * st["primary_rays"]
+            + L_PRIMARY_PIXEL * st["primary_rays"] + L_QUEUE * st["bounce_rays"])
+
+
 def layout_bytes(st, kernel, wide_primary=False):
     """Algorithmic bytes of one launch in this layout: the records its walk requests (one 64-B
     record per lane step in the per-lane bounce walk; one 64-B record -- two for a 4-wide
@@ -376,7 +386,8 @@ def main():
     # build above serves all three (one node layout)
     FAST = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE   # same results as the plain kernels (tests)
     modes = {"reference-order": FAST, "nearest-first": FAST | rt.FLAG_NEAREST_FIRST,
-             "nearest-first-wide": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH}
+             "nearest-first-wide": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH,
+             "nearest-first-wide-binned": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH | rt.FLAG_BINNED_PRIMARY}
     res = {m: timed(f) for m, f in modes.items()}
     ref = res["reference-order"]
     traversal = {"frames_identical": {}}
@@ -397,7 +408,7 @@ def main():
     # the profiled mode (its PMC file prices the roofline's traffic) unless another identical mode
     # is clearly faster: within 2% the step times are noise (a gloo rehearsal's step is its host-side
     # gather), and the headline is then the profiled mode's own, never a faster one's
-    pref = "nearest-first-wide"
+    pref = "nearest-first-wide-binned"
     if use_name != pref and traversal["frames_identical"].get(pref) and args.traversal != "reference" \
             and res[pref]["ms_step"] <= 1.02 * res[use_name]["ms_step"]:
         use_name = pref
@@ -440,7 +451,10 @@ def main():
     rst = counts(modes["reference-order"])
     ctx.set_flags(rt.FLAG_TIMING)
     wide = use_name.endswith("wide")
-    kern = {"k_primary": dict(ms=tst["ms_stage"][5], bytes=layout_bytes(cst, "k_primary", wide_primary=wide))}
+    binned = use_name.endswith("binned")
+    kern = {"k_primary": dict(ms=tst["ms_stage"][5],
+                              bytes=binned_bytes(cst, scene.num_tris) if binned
+                              else layout_bytes(cst, "k_primary", wide_primary=wide))}
     if bounces:   # 1 bounce: the first pass's traversal kernel has its own events
         kern["k_bounce_trav"] = dict(ms=tst["ms_stage"][7], bytes=layout_bytes(cst, "k_bounce_trav"))
         kern["k_bounce_shade"] = dict(ms=tst["ms_stage"][6] - tst["ms_stage"][7],
@@ -449,7 +463,8 @@ def main():
     # HBM traffic: the PMC bytes of each kernel from the rocprofv3 passes of the same mode at N = 1
     # (profiles/pmc_c5_<mode>.json), per record fetch x this launch's record fetches (at N = 1 the
     # profiled launch itself; at N > 1 a rank's launch fetches fewer records)
-    recs = {"k_primary": sum(cst["packet_steps"]) or (cst["internal_visits"][0] + cst["leaf_visits"][0]),
+    recs = {"k_primary": (cst["bin_entries"][0] if binned else
+                          sum(cst["packet_steps"]) or (cst["internal_visits"][0] + cst["leaf_visits"][0])),
             "k_bounce_trav": cst["internal_visits"][1] + cst["leaf_visits"][1],
             "k_bounce_shade": cst["bounce_rays"]}
     # per kernel: "requested" = this layout's algorithmic bytes (what the walk asks the memory system
@@ -458,7 +473,8 @@ def main():
     for k, v in kern.items():
         v["requested_gbs"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else 0.0
         v["requested_frac"] = v["requested_gbs"] / PEAK_HBM_GBS
-        pm = load_pmc(args.workload, use_name, k)
+        # the binned primary pass is several kernels: their summed PMC bytes (make_pmc_json.py)
+        pm = load_pmc(args.workload, use_name, "k_primary_pass" if k == "k_primary" and binned else k)
         v["traffic"] = None
         v["frac"] = None
         if pm and pm.get("records_per_launch") and recs.get(k):

@@ -45,6 +45,25 @@ for k, cs in acc.items():
             "k_bounce_shade": counts["bounce_rays"]}.get(base)
     if base not in kern or e["hbm_bytes_per_launch"] > kern[base]["hbm_bytes_per_launch"]:
         kern[base] = e
+# the binned primary pass (RTBVH_FLAG_BINNED_PRIMARY) as one entry: every instance of its kernels
+# summed per launch (the footprint/count and fill passes, the scan, the binned kernel, the shading, and
+# the gated packet walk behind them), priced per bin entry
+PASS = ("k_pb_bin", "k_pb_sums", "k_pb_scan", "k_primary_binned", "k_pb_shade")
+inst = {}
+for k, cs in acc.items():
+    m = {c: sum(v) / len(v) for c, v in cs.items()}
+    g = lambda c: m.get(c, 0.0)  # noqa: E731
+    inst[k] = (128 * g("TCC_EA0_RDREQ_128B_sum") + 64 * g("TCC_EA0_RDREQ_64B_sum") + 32 * g("TCC_EA0_RDREQ_32B_sum"),
+               64 * g("TCC_EA0_WRREQ_64B_sum") + 32 * (g("TCC_EA0_WRREQ_sum") - g("TCC_EA0_WRREQ_64B_sum")))
+parts = [k for k in inst if k.split("<")[0] in PASS]
+if parts:
+    gated = [k for k in inst if k.startswith("k_primary<")]
+    parts += gated
+    rd = sum(inst[k][0] for k in parts)
+    wr = sum(inst[k][1] for k in parts)
+    kern["k_primary_pass"] = {"instance": parts, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                              "hbm_bytes_per_launch": rd + wr,
+                              "records_per_launch": counts["bin_entries"][0] if counts else None}
 json.dump({"workload": workload, "mode": mode, "source": d,
            "method": __doc__.split("Usage")[0].strip(), "kernels": kern}, open(out, "w"), indent=1)
 for k, v in kern.items():

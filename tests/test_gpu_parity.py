@@ -877,12 +877,13 @@ def test_verify_walk_and_auto_walk():
     """rtbvh_verify_walk: the fast walks render the reference-order frame (0 differing pixels);
     RTBVH_FLAG_AUTO_WALK takes the reference-order kernels on small scenes, and on large ones
     checks the first frame of a key on the device (walk_state 1, the reference frame) before the
-    4-wide nearest-first walks take over (walk_state 2), with the same frames throughout."""
+    fast walks (binned primary pass, 4-wide nearest-first bounce walk) take over (walk_state 2),
+    with the same frames throughout."""
     d = load_scene_fixture("Test")
     small = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
     big = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
     W, H = 960, 540
-    for s, walk in ((small, 0), (big, WALK_FLAGS)):
+    for s, walk in ((small, 0), (big, WALK_FLAGS | rt.FLAG_BINNED_PRIMARY)):
         with rt.Context(device=0) as ref, rt.Context(device=0, flags=rt.FLAG_AUTO_WALK) as auto, \
                 rt.Context(device=0, flags=TRACE_MODES["nearest+packet+wide"]) as fast:
             for c in (ref, auto, fast):
