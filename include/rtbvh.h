@@ -127,22 +127,26 @@ enum {
     RTBVH_FLAG_WIDE_BVH = 1u << 7,        /* trace: walk the node records 4-wide (a node's four grandchild
                                              boxes share one 128-B line), keeping the lexicographic
                                              (t, leaf) minimum as NEAREST_FIRST does */
-    RTBVH_FLAG_AUTO_WALK = 1u << 8,       /* choose the walks, ignoring the four walk flags above, and return
+    RTBVH_FLAG_AUTO_WALK = 1u << 8,       /* choose the walks, ignoring the walk flags (the four above and
+                                             BINNED_PRIMARY), and return
                                              the reference-order frame always: up to 65536 triangles the
                                              reference-order kernels (exact by construction; the fastest on the
                                              reference's own meshes); above that, per frame key (scene + camera
                                              of the build, camera, size, bounces, band), the first frame is
                                              traced in the reference order into the outputs AND with
-                                             NEAREST_FIRST | PACKET_PRIMARY | REFILL_BOUNCE | WIDE_BVH into
+                                             NEAREST_FIRST | PACKET_PRIMARY | REFILL_BOUNCE | WIDE_BVH |
+                                             BINNED_PRIMARY into
                                              scratch, compared on the device; the key's later frames take the
                                              fast walks only if nothing differed (stats walk_state /
                                              walk_checks / walk_fallbacks) */
     RTBVH_FLAG_BINNED_PRIMARY = 1u << 9,  /* primary rays: every leaf listed in the 32 x 32 screen tiles its box
                                              covers (the set of orthographic primary rays a box passes is a
-                                             pixel rectangle), then per tile each listed leaf tested against
-                                             the pixels of its rectangle whose bound its min.z does not exceed,
-                                             the (t, leaf) keys in LDS: the lexicographic minimum of the
-                                             4-wide walks, with no dependent record fetches */
+                                             pixel rectangle, recorded by the build), then per tile each listed
+                                             leaf tested against the pixels of its rectangle whose bound its
+                                             min.z does not exceed, nearest depth bucket first, the (t, leaf)
+                                             keys in LDS: the lexicographic minimum of the 4-wide walks, with no
+                                             dependent record fetches.  Frames up to 32768 pixels
+                                             a side (larger ones take the 4-wide packet walk) */
     RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
                                               build instead of the one-workgroup build (same output) */
     /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n

@@ -47,6 +47,7 @@ struct rtbvh_ctx {
     uint4* d_topo = nullptr;                 // Karras node: child ids + leaf range
     Inner* d_rec = nullptr;                  // node records in slots (rtbvh_device.h), 2T-1
     QNode* d_qnode = nullptr;                // quantized 4-wide nodes in slots (rtbvh_device.h), 2T-1
+    uint4* d_lfp = nullptr;                  // leaf footprints on the primary pixel grid (binned primary pass)
     uint32_t* d_texels = nullptr;            // textures (rtbvh_texture), concatenated RGBA8
     uint4* d_texinfo = nullptr;
     float* d_srgb = nullptr;
@@ -218,6 +219,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_topo, ni));
     HIPC(c, dalloc(c->d_rec, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_qnode, 2 * (size_t)n - 1));
+    HIPC(c, dalloc(c->d_lfp, n));
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
     HIPC(c, dalloc(c->d_cnt, ni));
@@ -338,6 +340,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.xcnt = c->d_xcnt;
     a.rootbox = c->d_rootbox;
     a.qnode = c->d_qnode;
+    a.lfp = c->d_lfp;
     return a;
 }
 
@@ -420,6 +423,7 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.leaf = c->d_leaf;
     a.qnode = c->d_qnode;
     a.rootbox = c->d_rootbox;
+    a.lfp = c->d_lfp;
     a.tclip = c->d_tclip;
     a.verts = c->d_verts;
     a.idx = c->d_idx;
@@ -593,11 +597,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t my_bands = a.my_bands;
     uint32_t nsplit = trace_split(c, (size_t)W * 8 * my_bands);
     // the coherence sort has one set of buffers; frames-in-flight slots use the chains' buffers
-    // the binned primary pass covers the rank's whole frame in one chain; its footprints pack columns
-    // and compact rows in 16 bits
+    // the binned primary pass covers the rank's whole frame in one chain; the build's leaf footprints
+    // are exact for frames of up to 32768 pixels a side (rtbvh_device.h leaf_footprint)
     const uint32_t rows = P / W;
     const bool binned = wk.primary == PrimaryKind::BINNED;
-    const PrimaryKind pkind = binned && (W > 65535u || rows > 65535u) ? PrimaryKind::PACKET_WIDE : wk.primary;
+    const PrimaryKind pkind = binned && (W > 32768u || H > 32768u) ? PrimaryKind::PACKET_WIDE : wk.primary;
     if (sort || my_bands < nsplit || slot || c->slots_used || binned) nsplit = 1;
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
@@ -863,7 +867,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     for (auto& p : c->pb) { dfree(p.fp); dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_lfp);
     dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);

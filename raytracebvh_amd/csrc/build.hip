@@ -712,7 +712,10 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     uint32_t e = INVALID;
     {
         float4 r[4] = {};
-        if (i < T) leaf_record_words(a, i, lo, hi, r);
+        if (i < T) {
+            leaf_record_words(a, i, lo, hi, r);
+            a.lfp[i] = leaf_footprint(lo, hi);
+        }
         const uint32_t w0 = base + (tid & ~63u);   // this wave's first leaf
         staged_records(a.leaf + 4 * (size_t)w0, T > w0 ? min(64u, T - w0) : 0u, r,
                        reinterpret_cast<float4*>(&s_box[0][0][0]) + 128 * (tid >> 6));
@@ -1000,6 +1003,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
     for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
         f3 lo, hi;
         leaf_record(a, i, lo, hi);
+        a.lfp[i] = leaf_footprint(lo, hi);
         if (i + 1 < T) karras_node<MODE>(codes, T, i, a.topo, a.pleaf, a.pint);
     }
     if (tid == 0 && T > 1) a.pint[0] = INVALID;

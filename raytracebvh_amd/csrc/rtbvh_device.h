@@ -129,6 +129,40 @@ __device__ __forceinline__ float recip(float x) {
     return r;
 }
 __device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
+
+// A leaf box's footprint on the primary rays' pixel grid (RayTraceLaunch.hlsl:23-24: pixel x is the
+// ray at ((x - W/2) / 4, (y - H/2) / 4, 0), d = (0, 0, 1)), as pixel OFFSETS n = x - W/2 (so it does
+// not depend on the frame size): the n with lo < n / 4 < hi on each axis -- exactly the rays the 4-wide
+// packet walk's axis-parallel test lets through (n / 4 is exact) -- or, for a box that needs the
+// general slab test (`general`), the closed superset lo <= n / 4 <= hi (every n when a corner is NaN).
+// Written by the build, one 16-B record per sorted leaf: {nx0 | nx1 << 16, ny0 | ny1 << 16, min.z, general},
+// offsets as int16 clamped to +-32767 (exact for frames of up to 32768 pixels a side: a clamped bound lies
+// outside every such frame).  Read by the binned primary pass (trace.hip k_pb_bin).
+__device__ __forceinline__ void footprint_axis(float lo, float hi, bool general, int& a, int& b) {
+    const float r = 4.f * lo, R = 4.f * hi;   // exact (powers of two); +-inf past the float range
+    float fa, fb;
+    if (!general) {
+        fa = floorf(r) + 1.f;   // smallest integer > r (inexact only far outside any frame)
+        fb = ceilf(R) - 1.f;    // largest integer < R
+    } else if (r == r && R == R) {
+        fa = ceilf(fminf(r, R));
+        fb = floorf(fmaxf(r, R));
+    } else {
+        fa = -INFINITY;
+        fb = INFINITY;
+    }
+    a = (int)fminf(fmaxf(fa, -32767.f), 32767.f);
+    b = (int)fminf(fmaxf(fb, -32767.f), 32767.f);
+}
+__device__ __forceinline__ uint4 leaf_footprint(f3 lo, f3 hi) {
+    // the general bit of build.hip leaf_tri_word
+    const bool general = !(lo.x < hi.x && lo.y < hi.y && lo.z <= hi.z && 0.f <= hi.z && hi.z < INFINITY);
+    int x0, x1, y0, y1;
+    footprint_axis(lo.x, hi.x, general, x0, x1);
+    footprint_axis(lo.y, hi.y, general, y0, y1);
+    return make_uint4((uint32_t)(x0 & 0xFFFF) | (uint32_t)x1 << 16, (uint32_t)(y0 & 0xFFFF) | (uint32_t)y1 << 16,
+                      __float_as_uint(lo.z), general ? 1u : 0u);
+}
 __device__ __forceinline__ float lerpf(float a, float b, float s) { return a + s * (b - a); }
 
 // mul(float4(p,1), M), row-major M (row-vector convention)

@@ -66,6 +66,7 @@ struct BuildArgs {
     uint32_t* xcnt;           // [T / RBLOCK + 1] their counts
     float* rootbox;           // [6]
     QNode* qnode;             // [2T-1] quantized 4-wide nodes in slots (rtbvh_device.h), from rec
+    uint4* lfp;               // [T] leaf footprints on the primary pixel grid (rtbvh_device.h leaf_footprint)
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
@@ -109,6 +110,7 @@ struct TraceArgs {
     const uint32_t* pb_gate;
     uint32_t pb_cap, pb_ntx;
     const float* rootbox;     // [6] the BVH root's box (min xyz, max xyz): the bins' depth buckets
+    const uint4* lfp;         // [T] leaf footprints (BuildArgs::lfp)
     Mat4 wv;
     float4* color;            // output pixels (compacted band rows when nranks > 1)
     float* intensity;         // optional, same indexing as color

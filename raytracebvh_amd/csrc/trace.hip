@@ -772,36 +772,19 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
 // pixel, the lexicographic (t, leaf) minimum over the leaves whose box passes the axis-parallel test
 // -- min.x < o.x < max.x, min.y < o.y < max.y (the general slab test for a box whose bit is set) --
 // and whose triangle it hits; its box tests on the way down and its z pruning (min.z <= bound) only
-// skip leaves that cannot beat the bound (containment).  For a regular pixel grid the
-// set of pixels a box passes is a rectangle, computed exactly from the box (pb_range): so the same
-// minimum is found by listing every leaf in the 32 x 32 screen tiles its rectangle covers (the
-// leaf level of the BVH in slot order, two streaming passes) and, per tile, testing each listed
-// leaf against the pixels of its rectangle whose current bound its min.z does not exceed, with the
-// per-pixel (t, leaf) keys in LDS.  Order only changes which tests the bound skips, not the minimum.
-// At C5 that is 13.7M (leaf, tile) entries and 26M triangle tests per frame, all independent, in
-// place of 17.9M dependent record fetches of 8x8-pixel packets.  The outputs (shading, RayPresent
-// records, the bounce queue) are k_primary's, written per 8 x 8 sub-tile.  A tile whose bins
-// overflowed the buffer is traced by k_primary (4-wide packets) behind this kernel (pb_gate).
+// skip leaves that cannot beat the bound (containment).  On a regular pixel grid the
+// pixels a box passes form a rectangle, which the build records exactly per leaf (rtbvh_device.h
+// leaf_footprint).  So the same minimum is found level-synchronously at the leaves: every leaf is
+// listed in the (32 x 32 screen tile, depth bucket) bins its rectangle covers (k_pb_bin, two passes
+// streaming the leaves in slot order), then per tile (k_primary_binned) each listed leaf is tested
+// against the pixels of its rectangle whose current bound its min.z does not exceed, nearest depth
+// bucket first, the per-pixel (t, leaf) keys in LDS -- the bound carried from bucket to bucket.  Order
+// only changes which tests the bound skips, never the minimum.  At C5: 13.7M (leaf, tile) entries,
+// a third of them past the 8 x 8-block bound test, 35M triangle tests, all independent, in place of
+// 17.9M dependent record fetches of 8x8-pixel packets.  k_pb_shade then writes k_primary's outputs
+// (shading, RayPresent records, the bounce queue).  A tile whose bins overflowed the buffer is
+// traced by k_primary (4-wide packets) behind these kernels (pb_gate).
 
-// pixels c in [0, n) whose coordinate (c - half) / 4 passes lo < . < hi (fast: the packet walk's
-// exact test, (c - half) / 4 is exact) or, for a general box, the closed superset lo <= . <= hi
-// (the per-pixel slab test decides); [a, b], empty when a > b
-__device__ __forceinline__ void pb_range(float lo, float hi, uint32_t half, uint32_t n, bool general, int& a, int& b) {
-    const float r = 4.f * lo, R = 4.f * hi;   // exact (powers of two); +-inf past the float range
-    float fa, fb;
-    if (!general) {
-        fa = floorf(r) + 1.f;   // smallest integer > r (inexact only far outside any frame)
-        fb = ceilf(R) - 1.f;    // largest integer < R
-    } else if (r == r && R == R) {
-        fa = ceilf(fminf(r, R));
-        fb = floorf(fmaxf(r, R));
-    } else {   // a NaN corner: every pixel is a candidate
-        fa = -INFINITY;
-        fb = INFINITY;
-    }
-    a = (int)fminf(fmaxf(fa + (float)half, 0.f), (float)n);
-    b = (int)fminf(fmaxf(fb + (float)half, -1.f), (float)n - 1.f);
-}
 // k of band b in this rank's deal (its compact rows k*8 .. k*8+7), or -1 when another rank has it
 __device__ __forceinline__ int pb_band_pos(const TraceArgs& a, uint32_t b) {
     if (a.band_slots) {
@@ -870,15 +853,15 @@ __global__ __launch_bounds__(BLOCK) void k_pb_bin(TraceArgs a, uint4* __restrict
         f[i] = make_uint4(1, 1, 0, 0);   // empty: x0 = 1 > x1 = 0
         if (j < a.T) {
             if (!FILL) {
-                const float4 r2 = a.leaf[4 * (size_t)j + 2], r3 = a.leaf[4 * (size_t)j + 3];   // {e2.z, tri, min.xy}, {min.z, max}
-                const bool gen = (__float_as_uint(r2.y) & LEAF_BIT) != 0;   // build.hip leaf_tri_word
-                int x0, x1, y0, y1, c0, c1;
-                pb_range(r2.z, r3.y, a.W >> 1, a.W, gen, x0, x1);
-                pb_range(r2.w, r3.z, a.H >> 1, a.H, gen, y0, y1);
-                pb_rows(a, y0, y1, c0, c1);
-                if (x0 > x1 || c0 > c1) { x0 = 1; x1 = 0; c0 = 1; c1 = 0; }
-                f[i] = make_uint4((uint32_t)x0 | (uint32_t)x1 << 16, (uint32_t)c0 | (uint32_t)c1 << 16,
-                                  __float_as_uint(r3.x), gen ? 1u : 0u);
+                // the build's footprint (pixel offsets from the frame centre) on this frame and rank
+                const uint4 l = a.lfp[j];
+                const int hw = (int)(a.W >> 1), hh = (int)(a.H >> 1);
+                const int x0 = max((int)(int16_t)(l.x & 0xFFFFu) + hw, 0), x1 = min((int)(int16_t)(l.x >> 16) + hw, (int)a.W - 1);
+                const int y0 = max((int)(int16_t)(l.y & 0xFFFFu) + hh, 0), y1 = min((int)(int16_t)(l.y >> 16) + hh, (int)a.H - 1);
+                int c0 = 1, c1 = 0;
+                if (x0 <= x1) pb_rows(a, y0, y1, c0, c1);
+                if (x0 <= x1 && c0 <= c1)
+                    f[i] = make_uint4((uint32_t)x0 | (uint32_t)x1 << 16, (uint32_t)c0 | (uint32_t)c1 << 16, l.z, l.w);
                 fp[j] = f[i];
             } else {
                 f[i] = fp[j];
@@ -988,11 +971,12 @@ __global__ __launch_bounds__(1024) void k_pb_scan(uint32_t* __restrict__ off, ui
 //  k_pb_shade turns them into k_primary's outputs.
 // A stale bound (another wave's newer key, a maximum refreshed later) only tests more, never less.
 constexpr uint32_t PB_QCAP = 256;   // queued tests per wave
-// a pixel's key slot: rows 36 keys apart, so that the 8 rows of an 8 x 8 lane block fall in different
-// LDS banks (a 32-key row is 64 words: every row on the same banks, 8-way conflicts)
-constexpr uint32_t PB_KS = 36;
+// a pixel's key slot: rows 40 keys (80 words, 16 banks) apart, so that the t words read by the lanes
+// of an 8 x 8, 16 x 4 or 32 x 2 pixel block spread over the 32 odd banks two to a bank, the fewest
+// (a 32-key row is 64 words: every row on the same banks, 8-way conflicts)
+constexpr uint32_t PB_KS = 40;
 __device__ __forceinline__ uint32_t pb_slot(uint32_t pi) { return (pi / PB_TILE) * PB_KS + (pi % PB_TILE); }
-static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 16 blocks of 8 x 8 (4 lanes each)");
+static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 4 x 4 blocks of 8 x 8, a row per half-wave");
 // RTBVH_PB_PROF builds: shader-clock cycles per phase of k_primary_binned, summed over the waves into
 // counters[32..39] (read back as rtbvh_stats.trav_steps_log2[0..7]; scripts/pb_phases.py)
 #ifdef RTBVH_PB_PROF
@@ -1030,8 +1014,6 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
     const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
     uint32_t* sq = s_q[w];
     Counts c = {0, 0, 0, 0, 0};
-    // this lane's block of the maxima refresh: block lane / 4, rows 2 (lane % 4) .. +1 of it
-    const uint32_t mb = lane >> 2, mbx = (mb % (PB_TILE / 8)) * 8, mby = (mb / (PB_TILE / 8)) * 8 + 2 * (lane & 3u);
     const uint32_t nbatch = (end - beg + 63) / 64;
     const auto claim = [&]() {
         uint32_t b = 0;
@@ -1136,16 +1118,25 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
         }
         flush();
         PB_T(3);
-        // the block maxima from the keys (pixels outside the frame hold t = 0)
-        float m = 0.f;
-        const uint32_t* bt = s_t + 2 * (mby * PB_KS + mbx) + 1;
+        // the block maxima from the keys (pixels outside the frame hold t = 0): lane l reads column
+        // l % 32 of rows l / 32, + 2, + 4, ... (two whole rows per read: 2-way bank conflicts at most),
+        // one running maximum per block row, then the maxima of the 8 lanes of a block column and of
+        // the two half-waves
+        float m[PB_TILE / 8] = {0.f, 0.f, 0.f, 0.f};
+        const uint32_t* bt = s_t + 2 * ((lane / 32) * PB_KS + lane % 32) + 1;
 #pragma unroll
-        for (uint32_t r = 0; r < 2; r++)
+        for (uint32_t r = 0; r < PB_TILE / 2; r++) m[r / 4] = fmaxf(m[r / 4], __uint_as_float(bt[2 * (2 * r * PB_KS)]));
 #pragma unroll
-            for (uint32_t x = 0; x < 8; x++) m = fmaxf(m, __uint_as_float(bt[2 * (r * PB_KS + x)]));
-        m = fmaxf(m, __shfl_xor(m, 1, 64));
-        m = fmaxf(m, __shfl_xor(m, 2, 64));
-        if ((lane & 3u) == 0) s_bmax[mb] = m;
+        for (uint32_t by = 0; by < PB_TILE / 8; by++) {
+            m[by] = fmaxf(m[by], __shfl_xor(m[by], 1, 64));
+            m[by] = fmaxf(m[by], __shfl_xor(m[by], 2, 64));
+            m[by] = fmaxf(m[by], __shfl_xor(m[by], 4, 64));
+            m[by] = fmaxf(m[by], __shfl_xor(m[by], 32, 64));
+        }
+        if (lane < PB_TILE && (lane & 7u) == 0) {
+#pragma unroll
+            for (uint32_t by = 0; by < PB_TILE / 8; by++) s_bmax[by * (PB_TILE / 8) + lane / 8] = m[by];
+        }
         PB_T(5);
     }
     __syncthreads();
