@@ -44,6 +44,9 @@ def main():
         variants = [("nearest+refill", base | rt.FLAG_NEAREST_FIRST),
                     ("nearest+wide", base | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH),
                     ("wide (left-to-right packets)", base | rt.FLAG_WIDE_BVH)]
+    if os.environ.get("AB_SET") == "binnedbase":   # the binned mode only (A/B of two builds via RTBVH_LIB)
+        variants = [("binned", rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+                     | rt.FLAG_BINNED_PRIMARY)]
     if os.environ.get("AB_SET") == "binned":   # primary pass: 4-wide packets vs screen-tile bins
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
         variants = [("nearest-first-wide", base), ("binned", base | rt.FLAG_BINNED_PRIMARY)]

@@ -646,7 +646,7 @@ def _general_box_scene(seed=11):
     return rt.Scene(verts, idx, mats, base.materials)
 
 
-@pytest.mark.parametrize("mode", ["packet+wide", "nearest+packet+wide", "packet"])
+@pytest.mark.parametrize("mode", ["packet+wide", "nearest+packet+wide", "packet", "binned", "binned+wide+refill"])
 def test_primary_general_boxes(mode):
     """Flat and behind-the-eye boxes (record word 15 set) in the axis-parallel primary walk:
     frames identical to the oracle's, and the record bits as the tree's boxes say."""
@@ -661,6 +661,50 @@ def test_primary_general_boxes(mode):
         c.build()
         w4 = c.read_wide()
     assert np.count_nonzero(w4[:, 15]) > 100   # the general path is taken
+
+
+@pytest.mark.parametrize("W,H", [(64, 64), (97, 53)])
+def test_binned_primary_boxes_on_the_pixel_grid(W, H):
+    """The binned pass's rectangles at their edges: with the identity camera, clip space is object
+    space and the primary rays sit at multiples of 1/4 (RayTraceLaunch.hlsl:23-24), so triangles
+    with vertices ON that grid put box edges exactly on rays -- the strict min < o < max of the
+    axis-parallel test excludes them, and the build's footprint (leaf_footprint) must agree pixel
+    for pixel.  Plus thin triangles (boxes narrower than a pixel, between two rays or through one),
+    and an odd frame (W/2 rounds down).  Frames vs the CPU oracle, bit for bit: the primary pass
+    alone with the fast walks (their 4-wide bounce walk meets containment failures on this grid of
+    coincident vertices -- DESIGN.md 3 -- in the packet walk's frames as in the binned pass's), and
+    primary + bounce with the binned pass beside the reference-order bounce."""
+    from tests.containment import identity_camera
+    rng = np.random.default_rng(5)
+    tris = []
+    for _ in range(4000):   # vertices on the quarter grid, boxes of 0..12 rays
+        c = rng.integers(-4 * W // 8, 4 * W // 8, 2)
+        p = (c[None, :] + rng.integers(-6, 7, (3, 2))) / 4.0
+        tris.append(np.concatenate([p, rng.uniform(1, 60, (3, 1))], 1))
+    for _ in range(1000):   # thin in x: width 0, 1/8 or 1/4 around a ray or between two
+        x = rng.integers(-W // 2, W // 2) / 4.0 + rng.choice([0.0, 0.125, -0.125])
+        wd = rng.choice([0.0, 0.125, 0.25])
+        p = np.stack([[x, x + wd, x + wd / 2], rng.uniform(-H / 8, H / 8, 3), rng.uniform(1, 60, 3)], 1)
+        tris.append(p)
+    pos = np.concatenate(tris).astype(np.float32)
+    v = np.zeros((len(pos), 8), np.float32)
+    v[:, :3] = pos
+    v[:, 5] = -1.0
+    d = load_scene_fixture("Test")
+    n = len(pos) // 3
+    s = rt.Scene(v, np.arange(len(pos), dtype=np.uint32), (np.arange(n) % 3).astype(np.uint32), d["material_blob"])
+    wvp, wv = identity_camera()
+    os_ = _oscene(s)
+    for flags, bounces in ((BINNED_FAST, 0), (rt.FLAG_BINNED_PRIMARY, 1)):
+        with rt.Context(device=0, flags=flags) as c:
+            c.set_scene(s)
+            c.set_camera(wvp, wv)
+            c.compute_bvh(W, H, bounces)
+            fb = c.read_framebuffer()
+            nodes = c.read_bvh()
+        ofb, _, ost = orc.trace(os_, nodes, wvp, wv, W, H, bounces)
+        np.testing.assert_array_equal(fb, ofb)
+        assert ost["hits"] > W * H // 4
 
 
 @pytest.mark.parametrize("mode", ["nearest+packet+wide", "reference", "nearest+packet+refill"])
