@@ -562,7 +562,6 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         a.band_slots = deal->d + (H + 7) / 8;
     }
     a.counters = c->d_counters + 64 * slot;
-    HIPC(c, hipMemsetAsync(a.counters, 0, 64 * sizeof(unsigned long long), s));
     hipEvent_t* ev = c->evt[c->n_traces % rtbvh_ctx::RING];
     const Walks wk = choose_walks(flags);
     const bool sort = wk.sort, refill = wk.refill;
@@ -606,10 +605,27 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
-    HIPC(c, hipMemsetAsync(c->d_qcount + 32 * slot, 0, 32 * nsplit * sizeof(uint32_t), s));
-    if (refill && bounces)
-        HIPC(c, hipMemsetAsync(c->d_next + (size_t)NEXT_WORDS * slot, 0,
-                               (size_t)NEXT_WORDS * nsplit * sizeof(uint32_t), s));
+    // the binned pass's buffers (one chain: buffer set `slot`)
+    const uint32_t ntx = pb_tiles_x(W), nty = pb_tiles_y(rows);
+    if (pkind == PrimaryKind::BINNED) {
+        st = ensure_pb_capacity(c, slot, c->T, ntx * nty, (size_t)W * rows);
+        if (st) return st;
+    }
+    // the trace's counters, queue counts, bounce work counters and bin counts: one launch
+    ZeroList z{};
+    z.ptr[0] = reinterpret_cast<uint32_t*>(a.counters);
+    z.words[0] = 64 * 2;
+    z.ptr[1] = c->d_qcount + 32 * slot;
+    z.words[1] = 32 * nsplit;
+    if (refill && bounces) {
+        z.ptr[2] = c->d_next + (size_t)NEXT_WORDS * slot;
+        z.words[2] = (size_t)NEXT_WORDS * nsplit;
+    }
+    if (pkind == PrimaryKind::BINNED) {
+        z.ptr[3] = c->pb[slot].off;
+        z.words[3] = (size_t)ntx * nty * PB_NZ + 1;
+    }
+    launch_zero(z, s);
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (nsplit > 1) HIPC(c, hipEventRecord(c->ev_fork, s));
     for (uint32_t g = 0; g < nsplit; g++) {
@@ -625,12 +641,9 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         uint32_t* nx = c->d_next + (size_t)NEXT_WORDS * b;
         const bool tg = timing && g == 0;   // stage events: chain 0's kernels
         if (pkind == PrimaryKind::BINNED) {
-            const uint32_t ntx = pb_tiles_x(W), nty = pb_tiles_y(rows);
-            st = ensure_pb_capacity(c, b, c->T, ntx * nty, (size_t)W * rows);
-            if (st) return st;
             const rtbvh_ctx::PbBufs& pbb = c->pb[b];
             const PrimBins pb{pbb.fp, pbb.off, pbb.cur, pbb.bins, pbb.keys, pbb.sums, pbb.cap_bins, ntx, nty};
-            launch_primary_binned(ag, pb, rows, q[0], &qc[0], count, bounces > 0, sg);
+            launch_primary_binned(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, sg);
         } else
             launch_primary(ag, q[0], &qc[0], count, bounces > 0, pkind, sg);
         if (tg) HIPC(c, hipEventRecord(ev[1], sg));

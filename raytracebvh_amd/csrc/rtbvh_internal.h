@@ -151,7 +151,14 @@ inline uint32_t pb_tiles_y(uint32_t rows) { return (rows + PB_TILE - 1) / PB_TIL
 // footprints, bins, the binned kernel, then k_primary (4-wide packets) behind it for any tile whose
 // bins overflowed `cap`; rows = the rank's compact rows
 void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
-                           bool count, bool emit, hipStream_t s);
+                           bool count, bool emit, bool zeroed, hipStream_t s);
+// up to N arrays of 32-bit words zeroed by one launch (null / 0 words: unused)
+struct ZeroList {
+    static constexpr int N = 4;
+    uint32_t* ptr[N];
+    size_t words[N];
+};
+void launch_zero(const ZeroList& z, hipStream_t s);
 // one ray per lane bounce pass (reference order or nearest-first), shading included
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
                    uint32_t* qout_count, bool count, bool emit, bool nearest, hipStream_t s);
@@ -159,7 +166,7 @@ void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_coun
 // NEXT_SEGS zeroed work counters NEXT_STRIDE words apart (one per queue segment);
 // `blocks` persistent workgroups (0: 2048)
 #ifndef RTBVH_NEXT_SEGS
-#define RTBVH_NEXT_SEGS 32
+#define RTBVH_NEXT_SEGS 64
 #endif
 constexpr uint32_t NEXT_SEGS = RTBVH_NEXT_SEGS;
 constexpr uint32_t NEXT_STRIDE = 32;                          // one 128-B line per counter

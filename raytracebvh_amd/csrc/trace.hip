@@ -766,6 +766,13 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     flush_counts<COUNT>(a, c, hits, tex, 2);
 }
 
+// the trace's counters and bin counts zeroed by one launch instead of a memset each (blockIdx.y: the array)
+__global__ __launch_bounds__(BLOCK) void k_zero(ZeroList z) {
+    uint32_t* p = z.ptr[blockIdx.y];
+    const size_t n = z.words[blockIdx.y];
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) p[i] = 0;
+}
+
 // ---- binned primary rays (RTBVH_FLAG_BINNED_PRIMARY) ----------------------------------------
 // The primary rays are orthographic: pixel (x, y) is the ray o = ((x - W/2) / 4, (y - H/2) / 4, 0),
 // d = (0, 0, 1) (RayTraceLaunch.hlsl:16-30).  The 4-wide packet walk (traverse_packet4) returns, per
@@ -1877,11 +1884,20 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
     }
 }
 
+void launch_zero(const ZeroList& z, hipStream_t s) {
+    size_t most = 0;
+    for (int k = 0; k < ZeroList::N; k++) most = most > z.words[k] ? most : z.words[k];
+    if (most == 0) return;
+    size_t blocks = (most + BLOCK - 1) / BLOCK;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(k_zero, dim3((uint32_t)blocks, ZeroList::N), dim3(BLOCK), 0, s, z);
+}
+
 void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
-                           bool count, bool emit, hipStream_t s) {
+                           bool count, bool emit, bool zeroed, hipStream_t s) {
     if (rows == 0 || a.W == 0 || a.T == 0) return;
     const uint32_t keys = pb.ntx * pb.nty * PB_NZ;
-    (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
+    if (!zeroed) (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
     const dim3 lg((a.T + PB_LEAVES - 1) / PB_LEAVES);
     hipLaunchKernelGGL((k_pb_bin<false>), lg, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
     const uint32_t sb = (keys + PB_SCAN - 1) / PB_SCAN;

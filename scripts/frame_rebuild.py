@@ -9,7 +9,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import raytracebvh_amd as rt  # noqa: E402
 
-flags = (rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+flags = (rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH | rt.FLAG_BINNED_PRIMARY
          | int(os.environ.get("FRAME_FLAGS", "0"), 0))
 scene = rt.synthetic(10_000_000, seed=0x5EED0005, half_extent=(100, 100, 50))
 W, H = 3840, 2160
