@@ -63,6 +63,14 @@ struct rtbvh_ctx {
     unsigned long long ovf_seen = 0;
     float* d_bounds = nullptr;
     float* d_rootbox = nullptr;
+    float* d_zpart = nullptr;
+    // rtbvh_compute_bvh: the binned primary pass of the frame starts on `side` once the build's
+    // leaves are written (ev_leaf, between k_zrange and k_refit_top) and joins the context stream
+    // (ev_prim) before the packet walk of its overflowed tiles, which reads the whole BVH
+    hipStream_t side = nullptr;
+    hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
+    bool leaf_want = false;      // the next build records ev_leaf
+    bool leaf_pending = false;   // ev_leaf recorded and nothing enqueued on the stream since
     SortResult sorted{nullptr, nullptr};
 
     // trace buffers (capacity cap_P pixels)
@@ -225,6 +233,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_cnt, ni));
     HIPC(c, dalloc(c->d_xlist, n));
     HIPC(c, dalloc(c->d_xcnt, refit_blocks(T)));
+    HIPC(c, dalloc(c->d_zpart, 2 * (size_t)refit_blocks(T)));
     HIPC(c, dalloc(c->d_bounds, BOUNDS_WORDS));
     HIPC(c, dalloc(c->d_rootbox, 8));
     c->cap_T = T;
@@ -341,6 +350,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.rootbox = c->d_rootbox;
     a.qnode = c->d_qnode;
     a.lfp = c->d_lfp;
+    a.zpart = c->d_zpart;
     return a;
 }
 
@@ -544,6 +554,8 @@ rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
 // RTBVH_FLAG_TIMING asks for them).
 rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
                            float4* color, float* inten, hipStream_t s, uint32_t slot, uint32_t flags, bool timed) {
+    const bool leaf_pending = c->leaf_pending;   // (this trace is the first after the build or none is)
+    c->leaf_pending = false;
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
     if (W == 0 || H == 0 || nranks == 0 || rank >= nranks || bounces > 14)
         return fail(c, RTBVH_ERR_INVALID_ARG, "bad trace dimensions");
@@ -625,8 +637,16 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         z.ptr[3] = c->pb[slot].off;
         z.words[3] = (size_t)ntx * nty * PB_NZ + 1;
     }
-    launch_zero(z, s);
-    if (timing) HIPC(c, hipEventRecord(ev[0], s));
+    // rtbvh_compute_bvh: the binned pass (and the zeroing before it) on the side stream, concurrent
+    // with the build's crossing nodes (launch_refit_tail)
+    const bool overlap = pkind == PrimaryKind::BINNED && leaf_pending && s == c->stream && slot == 0 && nsplit == 1;
+    hipStream_t sp = s;
+    if (overlap) {
+        sp = c->side;
+        HIPC(c, hipStreamWaitEvent(sp, c->ev_leaf, 0));
+    }
+    launch_zero(z, sp);
+    if (timing) HIPC(c, hipEventRecord(ev[0], sp));
     if (nsplit > 1) HIPC(c, hipEventRecord(c->ev_fork, s));
     for (uint32_t g = 0; g < nsplit; g++) {
         hipStream_t sg = g ? c->sub[g] : s;
@@ -643,7 +663,17 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (pkind == PrimaryKind::BINNED) {
             const rtbvh_ctx::PbBufs& pbb = c->pb[b];
             const PrimBins pb{pbb.fp, pbb.off, pbb.cur, pbb.bins, pbb.keys, pbb.sums, pbb.cap_bins, ntx, nty};
-            launch_primary_binned(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, sg);
+            if (rows) {
+                launch_pb_pass(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, overlap ? sp : sg);
+                if (overlap) {
+                    HIPC(c, hipEventRecord(c->ev_prim, sp));
+                    HIPC(c, hipStreamWaitEvent(sg, c->ev_prim, 0));
+                }
+                launch_pb_gate(ag, pb, q[0], &qc[0], count, bounces > 0, sg);
+            } else if (overlap) {   // (nothing traced: the zeroing still joins)
+                HIPC(c, hipEventRecord(c->ev_prim, sp));
+                HIPC(c, hipStreamWaitEvent(sg, c->ev_prim, 0));
+            }
         } else
             launch_primary(ag, q[0], &qc[0], count, bounces > 0, pkind, sg);
         if (tg) HIPC(c, hipEventRecord(ev[1], sg));
@@ -877,12 +907,18 @@ void rtbvh_destroy(rtbvh_ctx* c) {
         dfree(c->d_qs[g][0]); dfree(c->d_qs[g][1]); dfree(c->d_hits[g]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+    }
+    if (c->ev_leaf) (void)hipEventDestroy(c->ev_leaf);
+    if (c->ev_prim) (void)hipEventDestroy(c->ev_prim);
     for (auto& p : c->pb) { dfree(p.fp); dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_lfp);
     dfree(c->d_band);
-    dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox);
+    dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
     dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);
@@ -1022,6 +1058,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         a.sorted_vals = c->d_va;
         launch_build_small(a, s);
         launch_qnodes(a, s);
+        c->leaf_pending = false;
         if (timing) for (int k = 1; k <= 5; k++) HIPC(c, hipEventRecord(ev[k], s));
         if (timing) c->n_builds++;
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
@@ -1041,7 +1078,22 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     a.sorted_vals = c->sorted.vals;
     launch_karras(a, s);
     if (timing) HIPC(c, hipEventRecord(ev[4], s));
-    launch_refit(a, s);   // leaf records, boxes, node records and QNodes
+    // leaf records, boxes, node records and QNodes; rtbvh_compute_bvh's primary pass may start
+    // after the leaves (ev_leaf)
+    launch_refit_leaves(a, s);
+    c->leaf_pending = false;
+    if (c->leaf_want) {
+        if (!c->side) {   // high priority: its workgroups go first while the crossing nodes' fill the CUs
+            int lo = 0, hi = 0;
+            HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPC(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi));
+        }
+        if (!c->ev_leaf) HIPC(c, hipEventCreateWithFlags(&c->ev_leaf, hipEventDisableTiming));
+        if (!c->ev_prim) HIPC(c, hipEventCreateWithFlags(&c->ev_prim, hipEventDisableTiming));
+        HIPC(c, hipEventRecord(c->ev_leaf, s));
+        c->leaf_pending = true;
+    }
+    launch_refit_tail(a, s);
     if (timing) HIPC(c, hipEventRecord(ev[5], s));
     if (timing) c->n_builds++;
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
@@ -1082,13 +1134,17 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
                              (uint64_t)c->slots_used | (uint64_t)c->cfg.stack_limit << 1};
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
         drop_graph(c);
+        c->leaf_want = true;
         rtbvh_status st = rtbvh_build_async(c);
+        c->leaf_want = false;
         if (!st) st = rtbvh_trace_async(c, W, H, bounces);
         if (!st) st = rtbvh_synchronize(c);
         if (st && st != RTBVH_ERR_STACK_OVERFLOW) return st;
         HIPC(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         c->capturing = true;
+        c->leaf_want = true;
         st = rtbvh_build_async(c);
+        c->leaf_want = false;
         if (!st) st = rtbvh_trace_async(c, W, H, bounces);
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(c->stream, &g);
@@ -1131,7 +1187,9 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
 rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
     if (!c) return RTBVH_ERR_INVALID_ARG;
     if (c->cfg.flags & RTBVH_FLAG_GRAPH) return compute_graph(c, W, H, bounces);
+    c->leaf_want = true;
     rtbvh_status st = rtbvh_build_async(c);
+    c->leaf_want = false;
     if (st) return st;
     st = rtbvh_trace_async(c, W, H, bounces);
     if (st) return st;

@@ -698,6 +698,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     __shared__ uint32_t s_pint[RBLOCK];
     __shared__ uint32_t s_xn;
     __shared__ uint32_t s_own[RTBVH_REFIT_STAGE_SLOTS / 32];   // phase 4: staged slots of this round
+    __shared__ float s_topo_z[2 * (RBLOCK / 64)];
     const uint32_t T = a.T;
     const uint32_t base = blockIdx.x * RBLOCK, tid = threadIdx.x;
     const uint32_t i = base + tid;
@@ -728,7 +729,29 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
             e = a.pleaf[i];
         }
     }
+    {   // the block's depth range (min lo.z, max hi.z of its leaves) for k_zrange: the binned primary
+        // pass buckets by depth as soon as the leaves are written, before the climb above the blocks
+        float zl = i < T ? lo.z : INFINITY, zh = i < T ? hi.z : -INFINITY;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            zl = fminf(zl, __shfl_xor(zl, off, 64));
+            zh = fmaxf(zh, __shfl_xor(zh, off, 64));
+        }
+        if ((tid & 63u) == 0) {
+            s_topo_z[2 * (tid >> 6)] = zl;
+            s_topo_z[2 * (tid >> 6) + 1] = zh;
+        }
+    }
     __syncthreads();
+    if (tid == 0) {
+        float zl = INFINITY, zh = -INFINITY;
+        for (uint32_t w = 0; w < RBLOCK / 64; w++) {
+            zl = fminf(zl, s_topo_z[2 * w]);
+            zh = fmaxf(zh, s_topo_z[2 * w + 1]);
+        }
+        a.zpart[2 * blockIdx.x] = zl;
+        a.zpart[2 * blockIdx.x + 1] = zh;
+    }
     for (int level = 0; e != INVALID && level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
         bool cross = !(p >= base && p < end);   // p's index is outside the block: so is its range
@@ -1024,6 +1047,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
         if (T == 1) {
             a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
             a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+            a.rootbox[6] = lo.z; a.rootbox[7] = hi.z;   // (k_zrange's: the root box's depth range)
             continue;
         }
         uint32_t e = s_pleaf[i];
@@ -1046,6 +1070,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
             if (e == INVALID) {
                 a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
                 a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
+                a.rootbox[6] = lo.z; a.rootbox[7] = hi.z;
                 break;
             }
         }
@@ -1120,13 +1145,48 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_qnodes, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.rec, a.pint, a.qnode, a.T);
 }
 uint32_t refit_blocks(uint32_t T) { return (T + RBLOCK - 1) / RBLOCK; }
-void launch_refit(const BuildArgs& a, hipStream_t s) {
+// the leaves' depth range: rootbox[6..7] = min lo.z, max hi.z over k_refit's per-block ranges
+__global__ __launch_bounds__(1024) void k_zrange(const float* __restrict__ zpart, uint32_t nb, float* __restrict__ rootbox) {
+    __shared__ float s_z[2 * 16];
+    float zl = INFINITY, zh = -INFINITY;
+    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+        zl = fminf(zl, zpart[2 * b]);
+        zh = fmaxf(zh, zpart[2 * b + 1]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        zl = fminf(zl, __shfl_xor(zl, off, 64));
+        zh = fmaxf(zh, __shfl_xor(zh, off, 64));
+    }
+    if ((threadIdx.x & 63u) == 0) {
+        s_z[2 * (threadIdx.x >> 6)] = zl;
+        s_z[2 * (threadIdx.x >> 6) + 1] = zh;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < 16; w++) {
+            zl = fminf(zl, s_z[2 * w]);
+            zh = fmaxf(zh, s_z[2 * w + 1]);
+        }
+        rootbox[6] = zl;
+        rootbox[7] = zh;
+    }
+}
+void launch_refit_leaves(const BuildArgs& a, hipStream_t s) {
     const uint32_t nb = refit_blocks(a.T);
     hipLaunchKernelGGL(k_refit, dim3(nb), dim3(RBLOCK), 0, s, a);
+    hipLaunchKernelGGL(k_zrange, dim3(1), dim3(1024), 0, s, a.zpart, nb, a.rootbox);
+}
+void launch_refit_tail(const BuildArgs& a, hipStream_t s) {
+    const uint32_t nb = refit_blocks(a.T);
     if (a.T > RBLOCK) {   // the crossing nodes: climbed, then quantized (a few per workgroup of k_refit)
         hipLaunchKernelGGL(k_refit_top, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
         hipLaunchKernelGGL(k_qnodes_cross, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
     }
+}
+void launch_refit(const BuildArgs& a, hipStream_t s) {
+    launch_refit_leaves(a, s);
+    launch_refit_tail(a, s);
 }
 void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
     hipLaunchKernelGGL(k_export, dim3(blocks_for(2 * (size_t)a.T - 1)), dim3(BLOCK), 0, s, a, (RefNode*)out);

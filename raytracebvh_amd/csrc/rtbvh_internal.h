@@ -64,9 +64,10 @@ struct BuildArgs {
     uint32_t* refit_cnt;      // [T-1]
     uint32_t* xlist;          // [T] k_refit workgroup b's crossing nodes at [b * RBLOCK, ...)
     uint32_t* xcnt;           // [T / RBLOCK + 1] their counts
-    float* rootbox;           // [6]
+    float* rootbox;           // [8] the root box (min xyz, max xyz), then the leaves' depth range (k_zrange)
     QNode* qnode;             // [2T-1] quantized 4-wide nodes in slots (rtbvh_device.h), from rec
     uint4* lfp;               // [T] leaf footprints on the primary pixel grid (rtbvh_device.h leaf_footprint)
+    float* zpart;             // [2 * refit_blocks(T)] k_refit workgroup b's leaf depth range
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
@@ -74,6 +75,10 @@ void launch_morton(const BuildArgs& a, hipStream_t s);
 void launch_karras(const BuildArgs& a, hipStream_t s);
 // leaf records + refit + node records + QNodes (zeroes the tickets it uses)
 void launch_refit(const BuildArgs& a, hipStream_t s);
+// ... in two parts: the leaves (k_refit: leaf records, footprints, the in-workgroup nodes; then the
+// leaves' depth range rootbox[6..7]) -- all the binned primary pass reads -- and the crossing nodes
+void launch_refit_leaves(const BuildArgs& a, hipStream_t s);
+void launch_refit_tail(const BuildArgs& a, hipStream_t s);
 // size of BuildArgs::xcnt for T leaves
 uint32_t refit_blocks(uint32_t T);
 // qnode[k] of every internal node from the record pairs
@@ -152,6 +157,12 @@ inline uint32_t pb_tiles_y(uint32_t rows) { return (rows + PB_TILE - 1) / PB_TIL
 // bins overflowed `cap`; rows = the rank's compact rows
 void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
                            bool count, bool emit, bool zeroed, hipStream_t s);
+// ... in two parts: the binned pass (reads what launch_refit_leaves writes) and the packet walk of
+// the overflowed tiles (the whole BVH)
+void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
+                    bool emit, bool zeroed, hipStream_t s);
+void launch_pb_gate(const TraceArgs& a, const PrimBins& pb, RayQ* q, uint32_t* qcount, bool count, bool emit,
+                    hipStream_t s);
 // up to N arrays of 32-bit words zeroed by one launch (null / 0 words: unused)
 struct ZeroList {
     static constexpr int N = 4;

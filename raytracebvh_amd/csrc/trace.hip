@@ -853,7 +853,7 @@ __global__ __launch_bounds__(BLOCK) void k_pb_bin(TraceArgs a, uint4* __restrict
     constexpr uint32_t LPT = PB_LEAVES / BLOCK;
     uint4 f[LPT];
     uint32_t zb[LPT];
-    const float zlo = a.rootbox[2], zhi = a.rootbox[5];
+    const float zlo = a.rootbox[6], zhi = a.rootbox[7];   // the leaves' depth range (= the root box's)
 #pragma unroll
     for (uint32_t i = 0; i < LPT; i++) {
         const uint32_t j = blockIdx.x * PB_LEAVES + i * BLOCK + threadIdx.x;
@@ -1893,8 +1893,8 @@ void launch_zero(const ZeroList& z, hipStream_t s) {
     hipLaunchKernelGGL(k_zero, dim3((uint32_t)blocks, ZeroList::N), dim3(BLOCK), 0, s, z);
 }
 
-void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
-                           bool count, bool emit, bool zeroed, hipStream_t s) {
+void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
+                    bool emit, bool zeroed, hipStream_t s) {
     if (rows == 0 || a.W == 0 || a.T == 0) return;
     const uint32_t keys = pb.ntx * pb.nty * PB_NZ;
     if (!zeroed) (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
@@ -1917,12 +1917,24 @@ void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows
     else
         hipLaunchKernelGGL((k_pb_shade<false>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
                            qcount, (int)emit);
+}
+
+void launch_pb_gate(const TraceArgs& a, const PrimBins& pb, RayQ* q, uint32_t* qcount, bool count, bool emit,
+                    hipStream_t s) {
+    if (a.W == 0 || a.T == 0) return;
     // the tiles whose bins overflowed: the 4-wide packet walk (every other block returns at once)
     TraceArgs g = a;
     g.pb_gate = pb.off;
     g.pb_cap = pb.cap;
     g.pb_ntx = pb.ntx;
     launch_primary(g, q, qcount, count, emit, PrimaryKind::PACKET_WIDE, s);
+}
+
+void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
+                           bool count, bool emit, bool zeroed, hipStream_t s) {
+    if (rows == 0) return;
+    launch_pb_pass(a, pb, rows, q, qcount, count, emit, zeroed, s);
+    launch_pb_gate(a, pb, q, qcount, count, emit, s);
 }
 
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,

@@ -1053,6 +1053,46 @@ def test_binned_band_traces_match_oracle(nranks, share):
     np.testing.assert_array_equal(frame, ofb)
 
 
+@pytest.mark.parametrize("tris", [3000, 300_000])
+def test_rebuilt_frame_overlap_matches_build_then_trace(tris):
+    """rtbvh_compute_bvh with the binned primary pass: the pass starts on a side stream once the
+    build's leaves are written (ev_leaf, after k_refit + k_zrange) and runs beside the crossing
+    nodes (k_refit_top, k_qnodes_cross); the packet walk of overflowed tiles and the bounce wait for
+    it.  Frame, intensities, counts and tree equal build() then trace() on one stream -- plain,
+    timed, and as a replayed hipGraph -- over frames and a scene change (3000 triangles: also the
+    oracle's frame)."""
+    W, H = 640, 360
+    wvp, wv = rt.camera_reference(W, H)
+    f = BINNED_FAST | rt.FLAG_MULTI_KERNEL_BUILD | rt.FLAG_COUNT_VISITS
+    scenes = [rt.synthetic(tris, seed=0x5EED0011), rt.synthetic(tris, seed=0x5EED0012, half_extent=(100, 100, 50))]
+    with rt.Context(device=0, flags=f) as a, rt.Context(device=0, flags=f | rt.FLAG_TIMING) as b, \
+            rt.Context(device=0, flags=f | rt.FLAG_GRAPH) as g:
+        for k, sc in enumerate(scenes):
+            for c in (a, b, g):
+                c.set_scene(sc)
+                c.set_camera(wvp, wv)
+            a.build()
+            a.trace(W, H, 1)
+            want, want_i, want_st = a.read_framebuffer(), a.read_intensity(), a.stats()
+            assert want_st["bounce_rays"] > 0 and sum(want_st["hits"]) > 0
+            if tris == 3000 and k == 0:
+                ofb, _, ost = orc.trace(_oscene(sc), a.read_bvh(), wvp, wv, W, H, 1)
+                np.testing.assert_array_equal(want, ofb)
+                assert sum(want_st["hits"]) == ost["hits"]
+            for c in (b, g):
+                for frame in range(3):
+                    c.compute_bvh(W, H, 1)
+                    np.testing.assert_array_equal(c.read_framebuffer(), want, err_msg=f"scene {k} frame {frame}")
+                    np.testing.assert_array_equal(c.read_intensity(), want_i)
+                    st = c.stats()
+                    for key in ("hits", "bounce_rays"):
+                        assert np.array_equal(np.asarray(st[key]), np.asarray(want_st[key])), key
+                    # the entries binned (entries past the block test depend on the tiles' claim order)
+                    assert st["bin_entries"][0] == want_st["bin_entries"][0]
+                np.testing.assert_array_equal(c.read_bvh()["bb_min"], a.read_bvh()["bb_min"])
+        assert g.stats()["graph_captures"] == 2
+
+
 def test_binned_primary_bins_overflow_falls_back_to_the_packet_walk():
     """Leaves whose boxes cover most of the frame overflow the bins (3 entries per leaf + 16 per
     tile): the overflowed tiles are traced by the 4-wide packet walk behind the binned kernel, the
