@@ -333,7 +333,9 @@ rtbvh_status rtbvh_read_bvh(rtbvh_ctx* ctx, rtbvh_node* out, uint32_t capacity);
  * c's children L and R as words {L.min.x, L.min.y, L.max.x, L.max.y, R.min.x, R.min.y,
  * R.max.x, R.max.y, L.min.z, L.max.z, R.min.z, R.max.z, id_L, id_R, c, 0}; ids: internal k,
  * or 0x80000000|j for sorted leaf j.  A leaf child c holds {its box as L and as R,
- * 0x80000000|c, ~0u, 0x80000000|c, 0}.  (The root's record follows at slot 2(n-1).) */
+ * 0x80000000|c, ~0u, 0x80000000|c, 0}.  (The root's record follows at slot 2(n-1).)  Only the
+ * packet primary walks read the leaf children's records: a build for other walks (binned, AUTO)
+ * leaves them out, and the first packet walk or this call writes them. */
 rtbvh_status rtbvh_read_wide(rtbvh_ctx* ctx, uint32_t* records, uint64_t capacity);
 /* Quantized 4-wide nodes of the bounce walk, one 64-B record (16 words) per slot (2n-1):
  * internal node k's at the slot of its record (2 * parent + side; the root's at 2n-2;

@@ -69,6 +69,7 @@ struct rtbvh_ctx {
     // (ev_prim) before the packet walk of its overflowed tiles, which reads the whole BVH
     hipStream_t side = nullptr;
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
+    bool pseudo_ok = false;      // the built tree has its leaf pseudo-records (read by the packet walks only)
     bool leaf_want = false;      // the next build records ev_leaf
     bool leaf_pending = false;   // ev_leaf recorded and nothing enqueued on the stream since
     SortResult sorted{nullptr, nullptr};
@@ -351,6 +352,11 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.qnode = c->d_qnode;
     a.lfp = c->d_lfp;
     a.zpart = c->d_zpart;
+    // the leaf pseudo-records cost the build 0.64 GB of writes at 10M triangles: written when the
+    // context's walks include a packet primary walk (AUTO and the binned pass take none)
+    // (choose_walks: a packet primary walk iff PACKET_PRIMARY without BINNED_PRIMARY)
+    const uint32_t f = c->cfg.flags;
+    a.pseudo = (f & RTBVH_FLAG_PACKET_PRIMARY) && !(f & (RTBVH_FLAG_BINNED_PRIMARY | RTBVH_FLAG_AUTO_WALK));
     return a;
 }
 
@@ -617,6 +623,16 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
+    if (!c->pseudo_ok && (pkind == PrimaryKind::PACKET_REFERENCE || pkind == PrimaryKind::PACKET_NEAREST ||
+                          pkind == PrimaryKind::PACKET_WIDE)) {
+        // a packet walk over a tree built without the leaf pseudo-records (the context's walks took
+        // none; set_flags since, or a frame past the binned pass's 32768 pixels a side): written now,
+        // on the context stream (no walk of a slot stream reads those slots)
+        launch_pseudo(build_args(c), c->stream);
+        c->pseudo_ok = true;
+        if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
+        if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+    }
     // the binned pass's buffers (one chain: buffer set `slot`)
     const uint32_t ntx = pb_tiles_x(W), nty = pb_tiles_y(rows);
     if (pkind == PrimaryKind::BINNED) {
@@ -1056,9 +1072,11 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         c->sorted = SortResult{c->d_ka, c->d_va};
         a.sorted_keys = c->d_ka;
         a.sorted_vals = c->d_va;
+        a.pseudo = 1;   // (the one-workgroup build writes them anyway)
         launch_build_small(a, s);
         launch_qnodes(a, s);
         c->leaf_pending = false;
+        c->pseudo_ok = true;
         if (timing) for (int k = 1; k <= 5; k++) HIPC(c, hipEventRecord(ev[k], s));
         if (timing) c->n_builds++;
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
@@ -1081,6 +1099,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     // leaf records, boxes, node records and QNodes; rtbvh_compute_bvh's primary pass may start
     // after the leaves (ev_leaf)
     launch_refit_leaves(a, s);
+    c->pseudo_ok = a.pseudo != 0;
     c->leaf_pending = false;
     if (c->leaf_want) {
         if (!c->side) {   // high priority: its workgroups go first while the crossing nodes' fill the CUs
@@ -1479,6 +1498,10 @@ rtbvh_status rtbvh_read_wide(rtbvh_ctx* c, uint32_t* out, uint64_t capacity) {
     const size_t total = c->T > 1 ? 2 * (size_t)(c->T - 1) : 0;
     if (capacity < total) return fail(c, RTBVH_ERR_INVALID_ARG, "read_wide: capacity < 2(n-1)");
     HIPC(c, hipSetDevice(c->cfg.device));
+    if (!c->pseudo_ok) {   // a build that wrote no leaf pseudo-records (binned / AUTO walks): now
+        launch_pseudo(build_args(c), c->stream);
+        c->pseudo_ok = true;
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     if (total) HIPC(c, hipMemcpy(out, c->d_rec, total * sizeof(Inner), hipMemcpyDeviceToHost));
     return RTBVH_OK;

@@ -451,8 +451,8 @@ __device__ __forceinline__ void complete_node(const BuildArgs& a, uint32_t p, ui
                                               f3& lo, f3& hi) {
     const uint4 ids = a.topo[p];
     store_record(a.rec + slot_of(e, a.T), l0, l1, r0, r1, ids.x, ids.y, p);
-    if (ids.x & LEAF_BIT) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
-    if (ids.y & LEAF_BIT) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
+    if (a.pseudo && (ids.x & LEAF_BIT)) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
+    if (a.pseudo && (ids.y & LEAF_BIT)) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
     lo = vmin(l0, r0);
     hi = vmax(l1, r1);
     if (e == INVALID) {
@@ -635,16 +635,27 @@ __device__ __forceinline__ void record_kids(const Inner* __restrict__ rec, uint3
     c0.b[0] = w0.x; c0.b[1] = w0.y; c0.b[2] = w2.x; c0.b[3] = w0.z; c0.b[4] = w0.w; c0.b[5] = w2.y;
     c1.b[0] = w1.x; c1.b[1] = w1.y; c1.b[2] = w2.z; c1.b[3] = w1.z; c1.b[4] = w1.w; c1.b[5] = w2.w;
 }
-// the QNode of the node whose record is at `slot`, from the records (crossing nodes, small builds)
-__device__ __forceinline__ void qnode_from_records(const Inner* __restrict__ rec, uint32_t slot, QNode* dst) {
+// the QNode of the node whose record is at `slot`, from the records (crossing nodes, small builds);
+// PSEUDO_NOGRID: a QNode without a grid gets its node's leaf pseudo-records (the bounce walk reads
+// that node's exact record pair, trace.hip qchildren), for a build that wrote none
+template <bool PSEUDO_NOGRID = false>
+__device__ __forceinline__ void qnode_from_records(Inner* __restrict__ rec, uint32_t slot, QNode* dst) {
     QEnt e0, e1;
     record_kids(rec, slot, e0, e1);
-    greedy_qnode(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { record_kids(rec, e.slot, c0, c1); }, dst);
+    float4 w[4];
+    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { record_kids(rec, e.slot, c0, c1); }, w);
+    store4(dst, w);
+    if (PSEUDO_NOGRID && w[0].w == 0.f) {
+        if (e0.id & LEAF_BIT)
+            store_pseudo_record(rec + e0.slot, e0.id, mk(e0.b[0], e0.b[1], e0.b[2]), mk(e0.b[3], e0.b[4], e0.b[5]));
+        if (e1.id & LEAF_BIT)
+            store_pseudo_record(rec + e1.slot, e1.id, mk(e1.b[0], e1.b[1], e1.b[2]), mk(e1.b[3], e1.b[4], e1.b[5]));
+    }
 }
 
 // QNodes of every internal node from the records (the one-workgroup build and
 // rtbvh_build_from_codes), one node per thread.
-__global__ __launch_bounds__(BLOCK) void k_qnodes(const Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
+__global__ __launch_bounds__(BLOCK) void k_qnodes(Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
                                                   QNode* __restrict__ qn, uint32_t T) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k + 1 >= T) return;
@@ -668,7 +679,8 @@ __device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f) {
 __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
     for_crossing(a, [&](uint32_t k) {
         const uint32_t slot = slot_of(a.pint[k], a.T);
-        qnode_from_records(a.rec, slot, a.qnode + slot);
+        if (a.pseudo) qnode_from_records<false>(a.rec, slot, a.qnode + slot);
+        else qnode_from_records<true>(a.rec, slot, a.qnode + slot);
     });
 }
 
@@ -686,6 +698,7 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
 // Against one pass per stage (round 1: records written during the divergent climb, then a
 // QNode pass re-reading every record pair) this writes each output once and reads no record
 // back except for the listed crossing nodes.
+template <bool PSEUDO>
 __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     __shared__ uint32_t s_cnt[RBLOCK];
     // node base + k: the boxes of its children (side 0, 1); before the climb, the staging
@@ -831,8 +844,9 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     }
     if (!RTBVH_REFIT_STAGE) {
         store4(a.rec + slot, rw);
-        if (q.x & LEAF_BIT) store_leaf_record(a.rec, i, 0, q.x, l0, l1);
-        if (q.y & LEAF_BIT) store_leaf_record(a.rec, i, 1, q.y, r0, r1);
+        const bool pw = mine && (PSEUDO || qw[0].w == 0.f);   // (no grid: the bounce walk reads them)
+        if (pw && (q.x & LEAF_BIT)) store_leaf_record(a.rec, i, 0, q.x, l0, l1);
+        if (pw && (q.y & LEAF_BIT)) store_leaf_record(a.rec, i, 1, q.y, r0, r1);
         store4(a.qnode + slot, qw);
         return;
     }
@@ -874,7 +888,9 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
                 }
             };
             if (rin) put(slot, kind ? qw : rw);
-            if (kind == 0 && mine) {
+            // the leaf children's pseudo-records: all (PSEUDO), or those of a node whose QNode has no
+            // grid (the bounce walk reads that node's exact record pair)
+            if (kind == 0 && mine && (PSEUDO || qw[0].w == 0.f)) {
                 float4 pw[4];
                 if (q.x & LEAF_BIT) { pseudo_words(q.x, l0, l1, pw); put(2 * i, pw); }
                 if (q.y & LEAF_BIT) { pseudo_words(q.y, r0, r1, pw); put(2 * i + 1, pw); }
@@ -1174,7 +1190,8 @@ __global__ __launch_bounds__(1024) void k_zrange(const float* __restrict__ zpart
 }
 void launch_refit_leaves(const BuildArgs& a, hipStream_t s) {
     const uint32_t nb = refit_blocks(a.T);
-    hipLaunchKernelGGL(k_refit, dim3(nb), dim3(RBLOCK), 0, s, a);
+    if (a.pseudo) hipLaunchKernelGGL(k_refit<true>, dim3(nb), dim3(RBLOCK), 0, s, a);
+    else hipLaunchKernelGGL(k_refit<false>, dim3(nb), dim3(RBLOCK), 0, s, a);
     hipLaunchKernelGGL(k_zrange, dim3(1), dim3(1024), 0, s, a.zpart, nb, a.rootbox);
 }
 void launch_refit_tail(const BuildArgs& a, hipStream_t s) {
@@ -1183,6 +1200,17 @@ void launch_refit_tail(const BuildArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_refit_top, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
         hipLaunchKernelGGL(k_qnodes_cross, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
     }
+}
+// leaf j's pseudo-record from its leaf record's box (the bytes k_refit<true> writes)
+__global__ __launch_bounds__(BLOCK) void k_pseudo(const float4* __restrict__ leaf, const uint32_t* __restrict__ pleaf,
+                                                  Inner* __restrict__ rec, uint32_t T) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= T) return;
+    const float4 b0 = leaf[4 * (size_t)j + 2], b1 = leaf[4 * (size_t)j + 3];
+    store_pseudo_record(rec + pleaf[j], LEAF_BIT | j, mk(b0.z, b0.w, b1.x), mk(b1.y, b1.z, b1.w));
+}
+void launch_pseudo(const BuildArgs& a, hipStream_t s) {
+    if (a.T > 1) hipLaunchKernelGGL(k_pseudo, dim3((a.T + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.leaf, a.pleaf, a.rec, a.T);
 }
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     launch_refit_leaves(a, s);

@@ -68,6 +68,7 @@ struct BuildArgs {
     QNode* qnode;             // [2T-1] quantized 4-wide nodes in slots (rtbvh_device.h), from rec
     uint4* lfp;               // [T] leaf footprints on the primary pixel grid (rtbvh_device.h leaf_footprint)
     float* zpart;             // [2 * refit_blocks(T)] k_refit workgroup b's leaf depth range
+    uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
@@ -79,6 +80,8 @@ void launch_refit(const BuildArgs& a, hipStream_t s);
 // leaves' depth range rootbox[6..7]) -- all the binned primary pass reads -- and the crossing nodes
 void launch_refit_leaves(const BuildArgs& a, hipStream_t s);
 void launch_refit_tail(const BuildArgs& a, hipStream_t s);
+// the leaves' pseudo-records alone, for a tree built without them (a.pseudo = 0)
+void launch_pseudo(const BuildArgs& a, hipStream_t s);
 // size of BuildArgs::xcnt for T leaves
 uint32_t refit_blocks(uint32_t T);
 // qnode[k] of every internal node from the record pairs

@@ -1478,7 +1478,8 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             h3 = h3 & (b3.y != INVALID);
         } else {
             // a node without a finite grid: its exact record pair (node = its slot; the
-            // pair of its children's records is at 2 * own, own = word 14 of its record)
+            // pair of its children's records is at 2 * own, own = word 14 of its record; the
+            // build writes the pseudo-records of such a node's leaf children whatever the flags)
             const uint32_t own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
             const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
             q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
@@ -1922,12 +1923,13 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
 void launch_pb_gate(const TraceArgs& a, const PrimBins& pb, RayQ* q, uint32_t* qcount, bool count, bool emit,
                     hipStream_t s) {
     if (a.W == 0 || a.T == 0) return;
-    // the tiles whose bins overflowed: the 4-wide packet walk (every other block returns at once)
+    // the tiles whose bins overflowed: the per-lane nearest-first walk (every other block returns at
+    // once); a binary walk, which reads no leaf pseudo-records (a binned build writes none)
     TraceArgs g = a;
     g.pb_gate = pb.off;
     g.pb_cap = pb.cap;
     g.pb_ntx = pb.ntx;
-    launch_primary(g, q, qcount, count, emit, PrimaryKind::PACKET_WIDE, s);
+    launch_primary(g, q, qcount, count, emit, PrimaryKind::LANE_NEAREST, s);
 }
 
 void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void k_chase(const uint4* __restrict__ a, uint
     if (s == 0x12345u) out[0] = s ^ r;
 }
 
-// k_chase with RECW-byte records (RECW = 16, 32, 64): does the rate follow the records
+// k_chase with RECW-byte records (RECW = 16, 32, 64, 128): does the rate follow the records
 // (requests) or the bytes / load instructions?
 template <int RECW>
 __global__ __launch_bounds__(256) void k_chase_w(const uint4* __restrict__ a, uint32_t nrec, uint32_t steps,
@@ -65,6 +65,12 @@ __global__ __launch_bounds__(256) void k_chase_w(const uint4* __restrict__ a, ui
         const uint4* p = a + (RECW / 16) * (size_t)r;
         uint4 v = p[0];
         if (RECW >= 32) { const uint4 w = p[1]; v.y ^= w.x; v.z ^= w.w; }
+        if (RECW >= 64) { const uint4 w = p[2], x = p[3]; v.y ^= w.x ^ x.y; v.z ^= w.w ^ x.z; }
+        if (RECW >= 128) {
+            const uint4 w = p[4], x = p[5], y = p[6], z = p[7];
+            v.y ^= w.x ^ x.y ^ y.z ^ z.w;
+            v.z ^= w.w ^ x.z ^ y.y ^ z.x;
+        }
         s ^= v.y ^ v.z;
         r = (v.x ^ (r * 0x85EBCA6Bu) ^ k) & (nrec - 1);
     }
@@ -105,21 +111,26 @@ int main(int argc, char** argv) {
     if (nrec2 < 256) return 1;
     const float ms_chase = timed([&] { k_chase<<<blocks, 256>>>(a, nrec2, steps, out); }, 5);
     // the same table as 16- and 32-B records (4x / 2x as many, same bytes)
-    uint32_t n16 = 1, n32 = 1;
+    uint32_t n16 = 1, n32 = 1, n64 = 1, n128 = 1;
     while (n16 * 2 <= (uint32_t)(bytes / 16)) n16 *= 2;
     while (n32 * 2 <= (uint32_t)(bytes / 32)) n32 *= 2;
+    while (n64 * 2 <= (uint32_t)(bytes / 64)) n64 *= 2;
+    while (n128 * 2 <= (uint32_t)(bytes / 128)) n128 *= 2;
     const float ms_c16 = timed([&] { k_chase_w<16><<<blocks, 256>>>(a, n16, steps, out); }, 5);
     const float ms_c32 = timed([&] { k_chase_w<32><<<blocks, 256>>>(a, n32, steps, out); }, 5);
+    const float ms_c64 = timed([&] { k_chase_w<64><<<blocks, 256>>>(a, n64, steps, out); }, 5);
+    const float ms_c128 = timed([&] { k_chase_w<128><<<blocks, 256>>>(a, n128, steps, out); }, 5);
     CHECK(hipDeviceSynchronize());
     const double lanes = (double)blocks * 256;
     const double recs = lanes * steps;
     printf("{\"cus\": %d, \"table_bytes\": %zu, \"stream_gbs\": %.1f, \"gather_records_per_s\": %.4g, "
            "\"gather_record_gbs\": %.1f, \"gather_line_gbs\": %.1f, \"chase_waves_per_simd\": %d, \"chase_lanes\": %.0f, "
            "\"chase_steps\": %u, \"chase_ms\": %.4f, \"chase_records_per_s\": %.4g, \"chase_record_gbs\": %.1f, "
-           "\"chase_step_latency_us\": %.3f, \"chase16_records_per_s\": %.4g, \"chase32_records_per_s\": %.4g}\n",
+           "\"chase_step_latency_us\": %.3f, \"chase16_records_per_s\": %.4g, \"chase32_records_per_s\": %.4g, "
+           "\"chase64w_records_per_s\": %.4g, \"chase128_records_per_s\": %.4g}\n",
            cus, bytes, bytes / (ms_stream * 1e-3) / 1e9, nrec2 / (ms_gather * 1e-3),
            nrec2 * 64.0 / (ms_gather * 1e-3) / 1e9, nrec2 * 128.0 / (ms_gather * 1e-3) / 1e9, wps, lanes, steps,
            ms_chase, recs / (ms_chase * 1e-3), recs * 64 / (ms_chase * 1e-3) / 1e9, ms_chase * 1e3 / steps,
-           recs / (ms_c16 * 1e-3), recs / (ms_c32 * 1e-3));
+           recs / (ms_c16 * 1e-3), recs / (ms_c32 * 1e-3), recs / (ms_c64 * 1e-3), recs / (ms_c128 * 1e-3));
     return 0;
 }

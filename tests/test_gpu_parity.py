@@ -1093,10 +1093,83 @@ def test_rebuilt_frame_overlap_matches_build_then_trace(tris):
         assert g.stats()["graph_captures"] == 2
 
 
-def test_binned_primary_bins_overflow_falls_back_to_the_packet_walk():
+def _far_scene(seed=5):
+    """A synthetic scene plus small triangles ~1e33 away: the nodes above them have corners past
+    2^100, so their QNodes carry no grid and the 4-wide bounce walk reads their exact records
+    (trace.hip qchildren), leaf children among them."""
+    base = rt.synthetic(6000, seed=seed, half_extent=(30, 30, 20))
+    rng = np.random.default_rng(seed)
+    tris = []
+    for k in range(64):
+        c = np.array([(1 if k % 2 else -1) * 1e33 * rng.uniform(1, 2), rng.uniform(-25, 25), rng.uniform(-20, 20)])
+        tris.append(c + rng.uniform(-0.5, 0.5, (3, 3)))
+    pos = np.concatenate(tris).astype(np.float32)
+    v = np.zeros((len(pos), 8), np.float32)
+    v[:, :3] = pos
+    v[:, 5] = -1.0
+    V0 = len(base.vertices)
+    verts = np.concatenate([base.vertices, v])
+    idx = np.concatenate([base.indices, V0 + np.arange(len(pos), dtype=np.uint32)])
+    mats = np.concatenate([base.mat_indices, np.zeros(len(pos) // 3, np.uint32)])
+    return rt.Scene(verts, idx, mats, base.materials)
+
+
+@pytest.mark.parametrize("mode", ["reference", "nearest+packet+wide", "binned+wide+refill"])
+def test_nodes_without_a_grid_trace_their_exact_records(mode):
+    """QNodes without a finite grid (corners past 2^100): the 4-wide bounce walk takes the node's
+    exact records -- a leaf child from the node's own record, as a binned build writes no leaf
+    pseudo-records -- and the frame equals the oracle's over two bounces."""
+    s = _far_scene()
+    W, H = 320, 240
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=TRACE_MODES[mode] | rt.FLAG_MULTI_KERNEL_BUILD | rt.FLAG_COUNT_VISITS) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 2)
+        fb, st = c.read_framebuffer(), c.stats()
+        nodes, q = c.read_bvh(), c.read_qnodes()
+    T = s.num_tris
+    internal = np.zeros(2 * T - 1, bool)
+    par, cl = nodes["parent"], nodes["child_l"]
+    for x in range(T + 1, 2 * T - 1):   # internal nodes but the root: their slots
+        p = par[x] - T
+        internal[2 * p + (0 if cl[par[x]] == x else 1)] = True
+    internal[2 * T - 2] = True
+    assert (q[internal, 3].view(np.float32) == 0).sum() >= 8   # nodes without a grid
+    ofb, _, ost = orc.trace(_oscene(s), nodes, wvp, wv, W, H, 2)
+    np.testing.assert_array_equal(fb, ofb)
+    assert st["bounce_rays"] == ost["bounce"] > 0 and sum(st["hits"]) == ost["hits"]
+
+
+def test_packet_walk_after_a_build_without_pseudo_records():
+    """A binned (or AUTO) context's build writes no leaf pseudo-records; a packet primary walk on
+    that tree (flags changed since) writes them first (rtbvh enqueue_walks), and its frame is the
+    oracle's -- then a rebuild under the packet flags writes them in the build."""
+    s = rt.synthetic(20_000, seed=0x5EED0013, half_extent=(30, 30, 20))
+    W, H = 320, 240
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=BINNED_FAST | rt.FLAG_MULTI_KERNEL_BUILD) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        nodes = c.read_bvh()
+        ofb, _, _ = orc.trace(_oscene(s), nodes, wvp, wv, W, H, 1)
+        np.testing.assert_array_equal(c.read_framebuffer(), ofb)
+        for f in (TRACE_MODES["nearest+packet+wide"], TRACE_MODES["packet"], TRACE_MODES["nearest+packet"]):
+            c.set_flags(f | rt.FLAG_MULTI_KERNEL_BUILD)
+            c.trace(W, H, 1)
+            np.testing.assert_array_equal(c.read_framebuffer(), ofb)
+            c.compute_bvh(W, H, 1)
+            np.testing.assert_array_equal(c.read_framebuffer(), ofb)
+            c.set_flags(BINNED_FAST | rt.FLAG_MULTI_KERNEL_BUILD)
+            c.compute_bvh(W, H, 1)
+            np.testing.assert_array_equal(c.read_framebuffer(), ofb)
+
+
+def test_binned_primary_bins_overflow_falls_back_to_a_walk():
     """Leaves whose boxes cover most of the frame overflow the bins (3 entries per leaf + 16 per
-    tile): the overflowed tiles are traced by the 4-wide packet walk behind the binned kernel, the
-    others by the bins, and the frame is the oracle's, pixel for pixel."""
+    tile): the overflowed tiles are traced by the per-lane nearest-first walk behind the binned
+    kernel, the others by the bins, and the frame is the oracle's, pixel for pixel."""
     rng = np.random.default_rng(11)
     n = 3000
     c0 = rng.uniform(-40, 40, (n, 1, 3)).astype(np.float32)
@@ -1117,7 +1190,7 @@ def test_binned_primary_bins_overflow_falls_back_to_the_packet_walk():
         nodes = c.read_bvh()
     ofb, _, ost = orc.trace(_oscene(s), nodes, wvp, wv, W, H, 1)
     np.testing.assert_array_equal(fb, ofb)
-    assert st["packet_steps"][0] > 0   # the packet walk traced the overflowed tiles
+    assert st["internal_visits"][0] > 0   # a walk traced the overflowed tiles (the binned pass visits no node)
     assert ost["hits"] > 100_000
 
 
