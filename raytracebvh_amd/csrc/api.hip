@@ -1105,6 +1105,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         if (!c->side) {   // high priority: its workgroups go first while the crossing nodes' fill the CUs
             int lo = 0, hi = 0;
             HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+            if (const char* e = getenv("RTBVH_SIDE_PRIORITY")) if (atoi(e) == 0) hi = lo;   // (A/B runs)
             HIPC(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi));
         }
         if (!c->ev_leaf) HIPC(c, hipEventCreateWithFlags(&c->ev_leaf, hipEventDisableTiming));
@@ -1143,6 +1144,17 @@ rtbvh_status rtbvh_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces)
     return rtbvh_synchronize(c);
 }
 
+// The binned primary pass of rtbvh_compute_bvh on a side stream beside the build's crossing nodes
+// (ev_leaf / ev_prim): opt-in (RTBVH_OVERLAP=1).  A/B at C5: the rocprof frame span 5.07 -> ~4.95
+// ms in a process with the context's own stream, but bench.py's context (a torch stream, the slot
+// streams of frames in flight) ran every build kernel of the frame up to 10x slower while the side
+// queue held its wait (6.28 ms per frame against 5.14 without; 5.81 at normal priority), and as a
+// hipGraph it was +-0 (4.98 / 4.99 / 5.00 ms).
+static bool side_overlap() {
+    const char* e = getenv("RTBVH_OVERLAP");
+    return e && atoi(e) != 0;
+}
+
 // RTBVH_FLAG_GRAPH: Graphics.cpp:56 rebuilds and traces every frame, ~20 launches and memsets
 // of little work each on the reference's own meshes; the frame is captured once into a
 // hipGraph and replayed.  A plain frame runs first so that every buffer exists before the
@@ -1153,7 +1165,7 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
                              (uint64_t)c->slots_used | (uint64_t)c->cfg.stack_limit << 1};
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
         drop_graph(c);
-        c->leaf_want = true;
+        c->leaf_want = side_overlap();
         rtbvh_status st = rtbvh_build_async(c);
         c->leaf_want = false;
         if (!st) st = rtbvh_trace_async(c, W, H, bounces);
@@ -1161,7 +1173,7 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
         if (st && st != RTBVH_ERR_STACK_OVERFLOW) return st;
         HIPC(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         c->capturing = true;
-        c->leaf_want = true;
+        c->leaf_want = side_overlap();
         st = rtbvh_build_async(c);
         c->leaf_want = false;
         if (!st) st = rtbvh_trace_async(c, W, H, bounces);
@@ -1206,7 +1218,7 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
 rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
     if (!c) return RTBVH_ERR_INVALID_ARG;
     if (c->cfg.flags & RTBVH_FLAG_GRAPH) return compute_graph(c, W, H, bounces);
-    c->leaf_want = true;
+    c->leaf_want = side_overlap();
     rtbvh_status st = rtbvh_build_async(c);
     c->leaf_want = false;
     if (st) return st;

@@ -1053,14 +1053,16 @@ def test_binned_band_traces_match_oracle(nranks, share):
     np.testing.assert_array_equal(frame, ofb)
 
 
+@pytest.mark.parametrize("overlap", ["0", "1"])
 @pytest.mark.parametrize("tris", [3000, 300_000])
-def test_rebuilt_frame_overlap_matches_build_then_trace(tris):
-    """rtbvh_compute_bvh with the binned primary pass: the pass starts on a side stream once the
-    build's leaves are written (ev_leaf, after k_refit + k_zrange) and runs beside the crossing
-    nodes (k_refit_top, k_qnodes_cross); the packet walk of overflowed tiles and the bounce wait for
-    it.  Frame, intensities, counts and tree equal build() then trace() on one stream -- plain,
-    timed, and as a replayed hipGraph -- over frames and a scene change (3000 triangles: also the
-    oracle's frame)."""
+def test_rebuilt_frame_overlap_matches_build_then_trace(tris, overlap, monkeypatch):
+    """rtbvh_compute_bvh with the binned primary pass, and with RTBVH_OVERLAP=1 the pass on a side
+    stream from the moment the build's leaves are written (ev_leaf, after k_refit + k_zrange),
+    beside the crossing nodes (k_refit_top, k_qnodes_cross); the walk of overflowed tiles and the
+    bounce wait for it.  Frame, intensities, counts and tree equal build() then trace() on one
+    stream -- plain, timed, and as a replayed hipGraph -- over frames and a scene change (3000
+    triangles: also the oracle's frame)."""
+    monkeypatch.setenv("RTBVH_OVERLAP", overlap)
     W, H = 640, 360
     wvp, wv = rt.camera_reference(W, H)
     f = BINNED_FAST | rt.FLAG_MULTI_KERNEL_BUILD | rt.FLAG_COUNT_VISITS
