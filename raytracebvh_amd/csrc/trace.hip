@@ -1167,8 +1167,14 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
 // written at base + its rank.  (One atomic per wave -- k_primary's wave_append -- is 130K claims on
 // one counter per C5 frame, ~1.2 ms at the ~100 claims per us one address takes.)  Tiles whose bins
 // overflowed return (k_primary traced them).
+// (a 1024-thread block, one pixel per thread: 256 threads with four pixels each held 86 VGPRs,
+// 5 waves per SIMD, for the shading's dependent gathers)
+#ifndef RTBVH_PB_SHADE_BLOCK
+#define RTBVH_PB_SHADE_BLOCK 1024
+#endif
+constexpr uint32_t PB_SHADE_BLOCK = RTBVH_PB_SHADE_BLOCK;
 template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void k_pb_shade(TraceArgs a, const uint32_t* __restrict__ off, uint32_t cap,
+__global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, const uint32_t* __restrict__ off, uint32_t cap,
                                                     uint32_t ntx, uint32_t rows,
                                                     const unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
                                                     uint32_t* __restrict__ qcount, int emit) {
@@ -1178,14 +1184,14 @@ __global__ __launch_bounds__(BLOCK) void k_pb_shade(TraceArgs a, const uint32_t*
     const uint32_t tile = blockIdx.y * ntx + blockIdx.x;
     if (off[(tile + 1) * PB_NZ] > cap) return;
     const uint32_t X0 = blockIdx.x * PB_TILE, C0 = blockIdx.y * PB_TILE;
-    constexpr uint32_t NST = (PB_TILE / 8) * (PB_TILE / 8) / (BLOCK / 64);   // sub-tiles per wave
+    constexpr uint32_t NST = (PB_TILE / 8) * (PB_TILE / 8) / (PB_SHADE_BLOCK / 64);   // sub-tiles per wave
     uint32_t x[NST], crow[NST];
     uint64_t key[NST];
     bool valid[NST];
     uint64_t livem[NST];
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++) {
-        const uint32_t st = w + i * (BLOCK / 64);
+        const uint32_t st = w + i * (PB_SHADE_BLOCK / 64);
         x[i] = X0 + (st % (PB_TILE / 8)) * 8 + (lane & 7u);
         crow[i] = C0 + (st / (PB_TILE / 8)) * 8 + (lane >> 3);
         valid[i] = x[i] < a.W && crow[i] < rows;
@@ -1201,7 +1207,7 @@ __global__ __launch_bounds__(BLOCK) void k_pb_shade(TraceArgs a, const uint32_t*
             live = 0 < a.mats[mi].shininess / 1000.f * 1;
         }
         livem[i] = __ballot(live);
-        if (lane == 0) s_cnt[w + i * (BLOCK / 64)] = (uint32_t)__popcll(livem[i]);
+        if (lane == 0) s_cnt[w + i * (PB_SHADE_BLOCK / 64)] = (uint32_t)__popcll(livem[i]);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1228,7 +1234,7 @@ __global__ __launch_bounds__(BLOCK) void k_pb_shade(TraceArgs a, const uint32_t*
             hits += h1;
             tex += t1;
             if (emit && live)
-                q[s_base + s_cnt[w + i * (BLOCK / 64)] + (uint32_t)__popcll(livem[i] & ((1ull << lane) - 1))] = e;
+                q[s_base + s_cnt[w + i * (PB_SHADE_BLOCK / 64)] + (uint32_t)__popcll(livem[i] & ((1ull << lane) - 1))] = e;
         }
     }
     if (COUNT) {
@@ -1913,10 +1919,10 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
         hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
                            pb.keys);
     if (count)
-        hipLaunchKernelGGL((k_pb_shade<true>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
+        hipLaunchKernelGGL((k_pb_shade<true>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
                            qcount, (int)emit);
     else
-        hipLaunchKernelGGL((k_pb_shade<false>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
+        hipLaunchKernelGGL((k_pb_shade<false>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
                            qcount, (int)emit);
 }
 
