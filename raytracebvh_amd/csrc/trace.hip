@@ -991,14 +991,18 @@ static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 4 x 4 bloc
 #else
 #define PB_T(i) do { } while (0)
 #endif
+#ifndef RTBVH_PB_RASTER_BLOCK
+#define RTBVH_PB_RASTER_BLOCK 256
+#endif
+constexpr uint32_t PB_RASTER_BLOCK = RTBVH_PB_RASTER_BLOCK;   // threads per tile of k_primary_binned
 template <bool COUNT>
-__global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
+__global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
                                                              const uint4* __restrict__ bins, uint32_t cap,
                                                              uint32_t ntx, uint32_t rows,
                                                              unsigned long long* __restrict__ keys) {
     __shared__ unsigned long long s_key[PB_TILE * PB_KS];
     __shared__ float s_bmax[(PB_TILE / 8) * (PB_TILE / 8)];
-    __shared__ uint32_t s_q[BLOCK / 64][PB_QCAP];
+    __shared__ uint32_t s_q[PB_RASTER_BLOCK / 64][PB_QCAP];
     __shared__ uint32_t s_next;
     const uint32_t* s_t = reinterpret_cast<const uint32_t*>(s_key);   // [2 slot + 1]: a pixel's bound (t bits)
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -1011,7 +1015,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
 #endif
     // keys of the pixels outside the frame (or the rank's rows) start at t = 0: no entry covers them,
     // and they never raise a block's largest bound
-    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_KS; i += BLOCK)
+    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_KS; i += PB_RASTER_BLOCK)
         s_key[i] = X0 + i % PB_KS < a.W && C0 + i / PB_KS < rows ? NO_HIT : 0ull;
     if (threadIdx.x < (PB_TILE / 8) * (PB_TILE / 8)) s_bmax[threadIdx.x] = INFINITY;
     if (threadIdx.x == 0) s_next = 0;
@@ -1148,7 +1152,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary_binned(TraceArgs a, const 
     }
     __syncthreads();
     // the tile's keys, row segments of 32 pixels
-    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += BLOCK) {
+    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += PB_RASTER_BLOCK) {
         const uint32_t px = i % PB_TILE, py = i / PB_TILE;
         if (X0 + px < a.W && C0 + py < rows) keys[(size_t)(C0 + py) * a.W + X0 + px] = s_key[py * PB_KS + px];
     }
@@ -1913,10 +1917,10 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
     hipLaunchKernelGGL((k_pb_bin<true>), lg, dim3(BLOCK), 0, s, a, pb.fp, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
     const dim3 grid(pb.ntx, pb.nty);
     if (count)
-        hipLaunchKernelGGL((k_primary_binned<true>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
+        hipLaunchKernelGGL((k_primary_binned<true>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
                            pb.keys);
     else
-        hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
+        hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
                            pb.keys);
     if (count)
         hipLaunchKernelGGL((k_pb_shade<true>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
