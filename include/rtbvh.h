@@ -146,7 +146,8 @@ enum {
                                              min.z does not exceed, nearest depth bucket first, the (t, leaf)
                                              keys in LDS: the lexicographic minimum of the 4-wide walks, with no
                                              dependent record fetches.  Frames up to 32768 pixels
-                                             a side (larger ones take the 4-wide packet walk) */
+                                             a side (larger ones take the 4-wide packet walk); a tile whose bins
+                                             overflow takes the per-lane nearest-first walk */
     RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
                                               build instead of the one-workgroup build (same output) */
     /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n

@@ -66,7 +66,7 @@ struct rtbvh_ctx {
     float* d_zpart = nullptr;
     // rtbvh_compute_bvh: the binned primary pass of the frame starts on `side` once the build's
     // leaves are written (ev_leaf, between k_zrange and k_refit_top) and joins the context stream
-    // (ev_prim) before the packet walk of its overflowed tiles, which reads the whole BVH
+    // (ev_prim) before the walk of its overflowed tiles, which reads the whole BVH
     hipStream_t side = nullptr;
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
     bool pseudo_ok = false;      // the built tree has its leaf pseudo-records (read by the packet walks only)

@@ -156,7 +156,7 @@ struct PrimBins {
 };
 inline uint32_t pb_tiles_x(uint32_t W) { return (W + PB_TILE - 1) / PB_TILE; }
 inline uint32_t pb_tiles_y(uint32_t rows) { return (rows + PB_TILE - 1) / PB_TILE; }
-// footprints, bins, the binned kernel, then k_primary (4-wide packets) behind it for any tile whose
+// footprints, bins, the binned kernel, then k_primary (the lane walk) behind it for any tile whose
 // bins overflowed `cap`; rows = the rank's compact rows
 void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
                            bool count, bool emit, bool zeroed, hipStream_t s);

@@ -790,7 +790,7 @@ __global__ __launch_bounds__(BLOCK) void k_zero(ZeroList z) {
 // a third of them past the 8 x 8-block bound test, 35M triangle tests, all independent, in place of
 // 17.9M dependent record fetches of 8x8-pixel packets.  k_pb_shade then writes k_primary's outputs
 // (shading, RayPresent records, the bounce queue).  A tile whose bins overflowed the buffer is
-// traced by k_primary (4-wide packets) behind these kernels (pb_gate).
+// traced by k_primary (the per-lane nearest-first walk) behind these kernels (pb_gate).
 
 // k of band b in this rank's deal (its compact rows k*8 .. k*8+7), or -1 when another rank has it
 __device__ __forceinline__ int pb_band_pos(const TraceArgs& a, uint32_t b) {
