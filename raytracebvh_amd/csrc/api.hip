@@ -99,7 +99,6 @@ struct rtbvh_ctx {
     // RTBVH_FLAG_BINNED_PRIMARY, per buffer set (chain / frames-in-flight slot): leaf footprints,
     // tile counts / offsets, fill cursors and the bins (trace.hip k_pb_bin)
     struct PbBufs {
-        uint4* fp = nullptr;
         uint32_t *off = nullptr, *cur = nullptr, *sums = nullptr;
         uint4* bins = nullptr;
         unsigned long long* keys = nullptr;
@@ -302,7 +301,7 @@ constexpr uint32_t BINS_PER_LEAF = 3;
 rtbvh_status ensure_pb_capacity(rtbvh_ctx* c, uint32_t b, uint32_t T, uint32_t tiles, size_t pixels) {
     rtbvh_ctx::PbBufs& p = c->pb[b];
     const uint32_t bins = BINS_PER_LEAF * T + 16 * tiles;
-    if (T <= p.cap_T && tiles <= p.cap_tiles && bins <= p.cap_bins && pixels <= p.cap_px && p.fp) return RTBVH_OK;
+    if (T <= p.cap_T && tiles <= p.cap_tiles && bins <= p.cap_bins && pixels <= p.cap_px && p.off) return RTBVH_OK;
     drop_graph(c);
     if (pixels > p.cap_px) {
         HIPC(c, dalloc(p.keys, pixels));
@@ -310,7 +309,6 @@ rtbvh_status ensure_pb_capacity(rtbvh_ctx* c, uint32_t b, uint32_t T, uint32_t t
     }
     const uint32_t nT = std::max(T, p.cap_T), nt = std::max(tiles, p.cap_tiles);
     const uint32_t nb = std::max(BINS_PER_LEAF * nT + 16 * nt, p.cap_bins);
-    HIPC(c, dalloc(p.fp, nT));
     HIPC(c, dalloc(p.off, (size_t)nt * PB_NZ + 1));
     HIPC(c, dalloc(p.cur, (size_t)nt * PB_NZ));
     HIPC(c, dalloc(p.sums, (size_t)nt * PB_NZ / 1024 + 1));
@@ -678,7 +676,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         const bool tg = timing && g == 0;   // stage events: chain 0's kernels
         if (pkind == PrimaryKind::BINNED) {
             const rtbvh_ctx::PbBufs& pbb = c->pb[b];
-            const PrimBins pb{pbb.fp, pbb.off, pbb.cur, pbb.bins, pbb.keys, pbb.sums, pbb.cap_bins, ntx, nty};
+            const PrimBins pb{pbb.off, pbb.cur, pbb.bins, pbb.keys, pbb.sums, pbb.cap_bins, ntx, nty};
             if (rows) {
                 launch_pb_pass(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, overlap ? sp : sg);
                 if (overlap) {
@@ -929,7 +927,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     }
     if (c->ev_leaf) (void)hipEventDestroy(c->ev_leaf);
     if (c->ev_prim) (void)hipEventDestroy(c->ev_prim);
-    for (auto& p : c->pb) { dfree(p.fp); dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
+    for (auto& p : c->pb) { dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_lfp);

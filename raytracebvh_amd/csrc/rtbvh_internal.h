@@ -145,7 +145,6 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 constexpr uint32_t PB_TILE = 32;
 constexpr uint32_t PB_NZ = 16;   // depth buckets per tile: a tile's bins are listed nearest bucket first
 struct PrimBins {
-    uint4* fp;        // [T] leaf footprints: {x0 | x1 << 16, row0 | row1 << 16, min.z, general}
     uint32_t* off;    // [tiles * PB_NZ + 1] leaves per (tile, depth bucket), then their offsets (exclusive
                       //   scan), [tiles * PB_NZ] the total
     uint32_t* cur;    // [tiles * PB_NZ] fill cursors
