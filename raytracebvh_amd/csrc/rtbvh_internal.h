@@ -19,7 +19,10 @@ struct Mat4 { float m[16]; };
 
 // ---- radix sort (sort.hip) --------------------------------------------------
 constexpr uint32_t SORT_BLOCK = 256;
-constexpr uint32_t SORT_ITEMS = 16;
+#ifndef RTBVH_SORT_ITEMS
+#define RTBVH_SORT_ITEMS 16
+#endif
+constexpr uint32_t SORT_ITEMS = RTBVH_SORT_ITEMS;   // keys per thread of a tile (A/B: 8 / 16 / 32)
 constexpr uint32_t SORT_TILE = SORT_BLOCK * SORT_ITEMS;   // 4096 keys per tile
 #ifndef RTBVH_RADIX_BITS
 #define RTBVH_RADIX_BITS 8
