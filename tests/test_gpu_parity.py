@@ -782,6 +782,38 @@ def test_frames_in_flight_match_one_at_a_time(nranks):
             c.trace_band_async(W, H, 1, r, nranks, bufs[0].data_ptr(), stream_ptr=torch.cuda.Stream().cuda_stream)
 
 
+def test_packet_frames_in_flight_after_a_binned_build():
+    """A binned context's build leaves out the leaf pseudo-records; switched to the packet walk,
+    its first frames go straight to caller streams (frames in flight): the pseudo-records are
+    written on the context stream first and every slot's trace waits for them -- each frame equals
+    the packet walk's frame on a tree built with them, and the binned frame is unchanged."""
+    import torch
+    s = rt.synthetic(200_000, seed=0x5EED0014, half_extent=(100, 100, 50))
+    W, H = 800, 400
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    packet = TRACE_MODES["nearest+packet+wide"]
+    with rt.Context(device=0, flags=packet) as ref:
+        ref.set_scene(s)
+        ref.set_camera(*rt.camera_reference(W, H))
+        ref.compute_bvh(W, H, 1)
+        want = torch.from_numpy(ref.read_framebuffer()).to("cuda:0")
+    with rt.Context(device=0, flags=BINNED_FAST) as c:
+        c.set_scene(s)
+        c.set_camera(*rt.camera_reference(W, H))
+        c.compute_bvh(W, H, 1)
+        binned = c.read_framebuffer()
+        c.set_flags(packet)
+        bufs = [torch.full((H, W, 4), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(3)]
+        torch.cuda.synchronize()
+        for i, b in enumerate(bufs):
+            c.trace_band_async(W, H, 1, 0, 1, b.data_ptr(), stream_ptr=streams[i].cuda_stream)
+        c.synchronize()
+        torch.cuda.synchronize()
+        for i, b in enumerate(bufs):
+            assert torch.equal(b, want), i
+        np.testing.assert_array_equal(binned, want.cpu().numpy())
+
+
 def test_compute_bvh_graph_replays_the_frame():
     """RTBVH_FLAG_GRAPH: compute_bvh captures build + trace into a hipGraph and replays it; the
     frames and trees equal a plain context's, across replays and the re-captures that a new
