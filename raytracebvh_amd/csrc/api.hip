@@ -70,6 +70,10 @@ struct rtbvh_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
     bool pseudo_ok = false;      // the built tree has its leaf pseudo-records (read by the packet walks only)
+    // rtbvh_compute_bvh: the build leaves its crossing nodes (launch_refit_tail) to the frame's binned
+    // pass, which runs them in its bin launches (launch_pb_bin_tail); any other first use of the tree
+    // runs them first (flush_tail)
+    bool tail_want = false, tail_pending = false;
     bool leaf_want = false;      // the next build records ev_leaf
     bool leaf_pending = false;   // ev_leaf recorded and nothing enqueued on the stream since
     SortResult sorted{nullptr, nullptr};
@@ -560,6 +564,18 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
                            float4* color, float* inten, hipStream_t s, uint32_t slot, uint32_t flags, bool timed) {
     const bool leaf_pending = c->leaf_pending;   // (this trace is the first after the build or none is)
     c->leaf_pending = false;
+    // the build's crossing nodes, if left to this trace: run in the binned pass's launches below, or
+    // before any walk (and on every early return) by the guard
+    struct TailGuard {
+        rtbvh_ctx* c;
+        bool pending;
+        void run() {
+            if (pending) launch_refit_tail(build_args(c), c->stream);
+            pending = false;
+        }
+        ~TailGuard() { run(); }
+    } tail{c, c->tail_pending};
+    c->tail_pending = false;
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
     if (W == 0 || H == 0 || nranks == 0 || rank >= nranks || bounces > 14)
         return fail(c, RTBVH_ERR_INVALID_ARG, "bad trace dimensions");
@@ -618,6 +634,8 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool binned = wk.primary == PrimaryKind::BINNED;
     const PrimaryKind pkind = binned && (W > 32768u || H > 32768u) ? PrimaryKind::PACKET_WIDE : wk.primary;
     if (sort || my_bands < nsplit || slot || c->slots_used || binned) nsplit = 1;
+    const bool fuse_tail = tail.pending && pkind == PrimaryKind::BINNED && s == c->stream && slot == 0 && rows > 0;
+    if (!fuse_tail) tail.run();   // before any walk reads the tree
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
@@ -678,7 +696,10 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             const rtbvh_ctx::PbBufs& pbb = c->pb[b];
             const PrimBins pb{pbb.off, pbb.cur, pbb.bins, pbb.keys, pbb.sums, pbb.cap_bins, ntx, nty};
             if (rows) {
-                launch_pb_pass(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, overlap ? sp : sg);
+                const BuildArgs ba = build_args(c);
+                launch_pb_pass(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, overlap ? sp : sg,
+                               fuse_tail ? &ba : nullptr);
+                if (fuse_tail) tail.pending = false;
                 if (overlap) {
                     HIPC(c, hipEventRecord(c->ev_prim, sp));
                     HIPC(c, hipStreamWaitEvent(sg, c->ev_prim, 0));
@@ -1074,6 +1095,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         launch_build_small(a, s);
         launch_qnodes(a, s);
         c->leaf_pending = false;
+        c->tail_pending = false;
         c->pseudo_ok = true;
         if (timing) for (int k = 1; k <= 5; k++) HIPC(c, hipEventRecord(ev[k], s));
         if (timing) c->n_builds++;
@@ -1111,7 +1133,8 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         HIPC(c, hipEventRecord(c->ev_leaf, s));
         c->leaf_pending = true;
     }
-    launch_refit_tail(a, s);
+    if (c->tail_want && !c->leaf_pending) c->tail_pending = true;   // (the trace runs it: launch_pb_bin_tail)
+    else launch_refit_tail(a, s);
     if (timing) HIPC(c, hipEventRecord(ev[5], s));
     if (timing) c->n_builds++;
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
@@ -1148,6 +1171,15 @@ rtbvh_status rtbvh_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces)
 // streams of frames in flight) ran every build kernel of the frame up to 10x slower while the side
 // queue held its wait (6.28 ms per frame against 5.14 without; 5.81 at normal priority), and as a
 // hipGraph it was +-0 (4.98 / 4.99 / 5.00 ms).
+// the crossing nodes a build left to the trace, when the trace did not run (an error on the way)
+static rtbvh_status flush_tail(rtbvh_ctx* c, rtbvh_status st) {
+    if (c->tail_pending) {
+        launch_refit_tail(build_args(c), c->stream);
+        c->tail_pending = false;
+    }
+    return st;
+}
+
 static bool side_overlap() {
     const char* e = getenv("RTBVH_OVERLAP");
     return e && atoi(e) != 0;
@@ -1164,17 +1196,21 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
         drop_graph(c);
         c->leaf_want = side_overlap();
+        c->tail_want = true;
         rtbvh_status st = rtbvh_build_async(c);
-        c->leaf_want = false;
+        c->leaf_want = c->tail_want = false;
         if (!st) st = rtbvh_trace_async(c, W, H, bounces);
+        st = flush_tail(c, st);
         if (!st) st = rtbvh_synchronize(c);
         if (st && st != RTBVH_ERR_STACK_OVERFLOW) return st;
         HIPC(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         c->capturing = true;
         c->leaf_want = side_overlap();
+        c->tail_want = true;
         st = rtbvh_build_async(c);
-        c->leaf_want = false;
+        c->leaf_want = c->tail_want = false;
         if (!st) st = rtbvh_trace_async(c, W, H, bounces);
+        st = flush_tail(c, st);
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(c->stream, &g);
         c->capturing = false;
@@ -1217,10 +1253,11 @@ rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
     if (!c) return RTBVH_ERR_INVALID_ARG;
     if (c->cfg.flags & RTBVH_FLAG_GRAPH) return compute_graph(c, W, H, bounces);
     c->leaf_want = side_overlap();
+    c->tail_want = true;
     rtbvh_status st = rtbvh_build_async(c);
-    c->leaf_want = false;
-    if (st) return st;
-    st = rtbvh_trace_async(c, W, H, bounces);
+    c->leaf_want = c->tail_want = false;
+    if (st) return flush_tail(c, st);
+    st = flush_tail(c, rtbvh_trace_async(c, W, H, bounces));
     if (st) return st;
     return rtbvh_synchronize(c);
 }

@@ -667,8 +667,8 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes(Inner* __restrict__ rec, const
 // refit workgroup walks them (a few dozen typically; up to RBLOCK for a degenerate tree).
 constexpr uint32_t XWAVES = BLOCK / 64;
 template <class F>
-__device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f) {
-    const uint32_t b = blockIdx.x * XWAVES + (threadIdx.x >> 6);
+__device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f, uint32_t bid = blockIdx.x) {
+    const uint32_t b = bid * XWAVES + (threadIdx.x >> 6);
     if (b * RBLOCK >= a.T) return;
     const uint32_t n = a.xcnt[b];
     for (uint32_t j = threadIdx.x & 63u; j < n; j += 64) f(a.xlist[b * RBLOCK + j]);
@@ -940,6 +940,22 @@ __global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
     for_crossing(a, [&](uint32_t k) { refit_top_node(a, k); });
 }
 
+// rtbvh_compute_bvh with the binned primary pass: the climb of the build's crossing nodes runs in
+// the launch of the pass's count pass, which reads only what k_refit wrote (leaf footprints, the depth
+// range): blocks [0, ntail) climb (k_refit_top's work), the rest count.  k_qnodes_cross follows as
+// its own launch (fused into the fill pass its 81 VGPRs held that pass to 5 waves per SIMD); the
+// gated walk and the bounce walk, which read the whole tree, come after both.
+#include "pb_bin.h"
+__global__ __launch_bounds__(BLOCK) void k_pb_count_top(BuildArgs b, TraceArgs a, uint32_t ntail,
+                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                                                        uint4* __restrict__ bins, uint32_t cap, uint32_t ntx) {
+    if (blockIdx.x < ntail) {
+        for_crossing(b, [&](uint32_t k) { refit_top_node(b, k); }, blockIdx.x);
+        return;
+    }
+    pb_bin_block<false>(a, blockIdx.x - ntail, off, cur, bins, cap, ntx);
+}
+
 __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= a.T) return;
@@ -1193,6 +1209,13 @@ void launch_refit_leaves(const BuildArgs& a, hipStream_t s) {
     if (a.pseudo) hipLaunchKernelGGL(k_refit<true>, dim3(nb), dim3(RBLOCK), 0, s, a);
     else hipLaunchKernelGGL(k_refit<false>, dim3(nb), dim3(RBLOCK), 0, s, a);
     hipLaunchKernelGGL(k_zrange, dim3(1), dim3(1024), 0, s, a.zpart, nb, a.rootbox);
+}
+void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, uint32_t* cur, uint4* bins, uint32_t cap,
+                         uint32_t ntx, uint32_t leaf_blocks, hipStream_t s) {
+    const uint32_t nb = refit_blocks(b.T);
+    const uint32_t ntail = b.T > RBLOCK ? (nb + XWAVES - 1) / XWAVES : 0u;
+    hipLaunchKernelGGL(k_pb_count_top, dim3(ntail + leaf_blocks), dim3(BLOCK), 0, s, b, a, ntail, off, cur, bins, cap, ntx);
+    if (ntail) hipLaunchKernelGGL(k_qnodes_cross, dim3(ntail), dim3(BLOCK), 0, s, b);
 }
 void launch_refit_tail(const BuildArgs& a, hipStream_t s) {
     const uint32_t nb = refit_blocks(a.T);

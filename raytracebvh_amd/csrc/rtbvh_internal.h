@@ -165,7 +165,11 @@ void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows
 // ... in two parts: the binned pass (reads what launch_refit_leaves writes) and the packet walk of
 // the overflowed tiles (the whole BVH)
 void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
-                    bool emit, bool zeroed, hipStream_t s);
+                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail = nullptr);
+// the count pass of launch_pb_pass with the climb of the build's crossing nodes in the same launch,
+// then their QNodes (build.hip: the build's launch_refit_tail, moved into the frame)
+void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, uint32_t* cur, uint4* bins, uint32_t cap,
+                         uint32_t ntx, uint32_t leaf_blocks, hipStream_t s);
 void launch_pb_gate(const TraceArgs& a, const PrimBins& pb, RayQ* q, uint32_t* qcount, bool count, bool emit,
                     hipStream_t s);
 // up to N arrays of 32-bit words zeroed by one launch (null / 0 words: unused)

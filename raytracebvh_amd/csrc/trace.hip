@@ -792,128 +792,18 @@ __global__ __launch_bounds__(BLOCK) void k_zero(ZeroList z) {
 // (shading, RayPresent records, the bounce queue).  A tile whose bins overflowed the buffer is
 // traced by k_primary (the per-lane nearest-first walk) behind these kernels (pb_gate).
 
-// k of band b in this rank's deal (its compact rows k*8 .. k*8+7), or -1 when another rank has it
-__device__ __forceinline__ int pb_band_pos(const TraceArgs& a, uint32_t b) {
-    if (a.band_slots) {
-        const uint32_t s = a.band_slots[b];
-        return (s >> 24) == a.rank ? (int)(s & 0xFFFFFFu) : -1;
-    }
-    return b % a.nranks == a.rank ? (int)(b / a.nranks) : -1;
-}
-// the rank's compact rows among image rows [y0, y1] (an order-preserving map, so a range [c0, c1])
-__device__ __forceinline__ void pb_rows(const TraceArgs& a, int y0, int y1, int& c0, int& c1) {
-    if (a.nranks == 1 || y0 > y1) { c0 = y0; c1 = y1; return; }
-    c0 = 1; c1 = 0;
-    const int b0 = y0 >> 3, b1 = y1 >> 3;
-    int b = b0;
-    for (; b <= b1; b++) {
-        const int k = pb_band_pos(a, (uint32_t)b);
-        if (k >= 0) { c0 = b == b0 ? k * 8 + (y0 & 7) : k * 8; break; }
-    }
-    if (b > b1) return;   // none of the bands is the rank's
-    for (b = b1; b >= b0; b--) {
-        const int k = pb_band_pos(a, (uint32_t)b);
-        if (k >= 0) { c1 = b == b1 ? k * 8 + (y1 & 7) : k * 8 + 7; break; }
-    }
-}
+#include "pb_bin.h"
 // image row of the rank's compact row
 __device__ __forceinline__ uint32_t pb_image_row(const TraceArgs& a, uint32_t crow) {
     const uint32_t k = crow >> 3;
     return (a.band_list ? a.band_list[k] : k * a.nranks + a.rank) * 8 + (crow & 7u);
 }
 
-// pass 1 (FILL false): leaf j's footprint -- its pixel columns and the rank's compact rows, min.z,
-// the general bit -- and its count in every (screen tile, depth bucket) bin it covers; pass 2 (FILL
-// true): the footprint with j into those bins at the scanned offsets (16-B entries: the binned pass
-// streams them with no dependent fetch).  A workgroup takes PB_LEAVES consecutive sorted leaves --
-// neighbours in space, sharing their bins -- and counts them per bin in an LDS table first, so the
-// global atomics are one per bin and workgroup instead of one per wave and bin; in pass 2 the
-// table's returned bases and LDS cursors place every entry.  A bin the full table cannot hold takes
-// a global atomic of its own (correct either way).
-constexpr uint32_t PB_LEAVES = 1024;      // leaves per workgroup (4 per thread)
-constexpr uint32_t PB_HASH = 1024;        // LDS table slots
-constexpr uint32_t PB_EMPTY = 0xFFFFFFFFu;
-__device__ __forceinline__ int pb_slot_of(uint32_t* h_key, uint32_t key, bool insert) {
-    uint32_t h = (key * 2654435761u) >> 22;   // 10 bits
-    for (int probe = 0; probe < 32; probe++) {
-        const uint32_t k = insert ? atomicCAS(&h_key[h], PB_EMPTY, key) : h_key[h];
-        if (k == key || (insert && k == PB_EMPTY)) return (int)h;
-        if (!insert && k == PB_EMPTY) return -1;
-        h = (h + 1) & (PB_HASH - 1);
-    }
-    return -1;
-}
-// (both passes derive the frame's footprint from the build's: storing it in the first pass for the
-// second was +-0, C5 A/B 0.952 / 0.952 ms, for 16 B per leaf of memory)
 template <bool FILL>
 __global__ __launch_bounds__(BLOCK) void k_pb_bin(TraceArgs a, uint32_t* __restrict__ off,
                                                   uint32_t* __restrict__ cur, uint4* __restrict__ bins, uint32_t cap,
                                                   uint32_t ntx) {
-    __shared__ uint32_t h_key[PB_HASH], h_cnt[PB_HASH], h_base[FILL ? PB_HASH : 1];
-    for (uint32_t i = threadIdx.x; i < PB_HASH; i += BLOCK) { h_key[i] = PB_EMPTY; h_cnt[i] = 0; }
-    __syncthreads();
-    constexpr uint32_t LPT = PB_LEAVES / BLOCK;
-    uint4 f[LPT];
-    uint32_t zb[LPT];
-    const float zlo = a.rootbox[6], zhi = a.rootbox[7];   // the leaves' depth range (= the root box's)
-#pragma unroll
-    for (uint32_t i = 0; i < LPT; i++) {
-        const uint32_t j = blockIdx.x * PB_LEAVES + i * BLOCK + threadIdx.x;
-        f[i] = make_uint4(1, 1, 0, 0);   // empty: x0 = 1 > x1 = 0
-        if (j < a.T) {
-            {   // the build's footprint (pixel offsets from the frame centre) on this frame and rank
-                const uint4 l = a.lfp[j];
-                const int hw = (int)(a.W >> 1), hh = (int)(a.H >> 1);
-                const int x0 = max((int)(int16_t)(l.x & 0xFFFFu) + hw, 0), x1 = min((int)(int16_t)(l.x >> 16) + hw, (int)a.W - 1);
-                const int y0 = max((int)(int16_t)(l.y & 0xFFFFu) + hh, 0), y1 = min((int)(int16_t)(l.y >> 16) + hh, (int)a.H - 1);
-                int c0 = 1, c1 = 0;
-                if (x0 <= x1) pb_rows(a, y0, y1, c0, c1);
-                if (x0 <= x1 && c0 <= c1)
-                    f[i] = make_uint4((uint32_t)x0 | (uint32_t)x1 << 16, (uint32_t)c0 | (uint32_t)c1 << 16, l.z, l.w);
-            }
-        }
-        // the depth bucket of min.z in the root box's depth range (general boxes first: they always test)
-        const float u = (__uint_as_float(f[i].z) - zlo) / (zhi - zlo) * (float)PB_NZ;
-        zb[i] = f[i].w ? 0u : (uint32_t)fminf(fmaxf(u, 0.f), (float)(PB_NZ - 1));   // NaN: 0
-    }
-    // the (leaf, bin) pairs of item i, visited by `body(key)`
-    const auto pairs = [&](uint32_t i, auto&& body) {
-        const uint32_t x0 = f[i].x & 0xFFFFu, x1 = f[i].x >> 16, c0 = f[i].y & 0xFFFFu, c1 = f[i].y >> 16;
-        if (x0 > x1 || c0 > c1) return;
-        for (uint32_t ty = c0 / PB_TILE; ty <= c1 / PB_TILE; ty++)
-            for (uint32_t tx = x0 / PB_TILE; tx <= x1 / PB_TILE; tx++) body((ty * ntx + tx) * PB_NZ + zb[i]);
-    };
-    // counts per bin in the table (or straight to the global count when the table is full)
-#pragma unroll
-    for (uint32_t i = 0; i < LPT; i++)
-        pairs(i, [&](uint32_t key) {
-            const int sl = pb_slot_of(h_key, key, true);
-            if (sl >= 0) atomicAdd(&h_cnt[sl], 1u);
-            else if (!FILL) atomicAdd(&off[key], 1u);
-        });
-    __syncthreads();
-    for (uint32_t sl = threadIdx.x; sl < PB_HASH; sl += BLOCK) {
-        const uint32_t key = h_key[sl];
-        if (key == PB_EMPTY) continue;
-        if (!FILL) {
-            atomicAdd(&off[key], h_cnt[sl]);
-        } else {
-            h_base[sl] = off[key] + atomicAdd(&cur[key], h_cnt[sl]);
-            h_cnt[sl] = 0;
-        }
-    }
-    if (!FILL) return;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t i = 0; i < LPT; i++) {
-        const uint32_t j = blockIdx.x * PB_LEAVES + i * BLOCK + threadIdx.x;
-        const uint4 entry = make_uint4(f[i].x, f[i].y, f[i].z, j | (f[i].w ? LEAF_BIT : 0u));
-        pairs(i, [&](uint32_t key) {
-            const int sl = pb_slot_of(h_key, key, false);
-            const uint32_t e = sl >= 0 ? h_base[sl] + atomicAdd(&h_cnt[sl], 1u) : off[key] + atomicAdd(&cur[key], 1u);
-            if (e < cap) bins[e] = entry;
-        });
-    }
+    pb_bin_block<FILL>(a, blockIdx.x, off, cur, bins, cap, ntx);
 }
 
 // exclusive scan of the n bin counts in place, off[n] = the total, the fill cursors zeroed: blocks of
@@ -1903,12 +1793,13 @@ void launch_zero(const ZeroList& z, hipStream_t s) {
 }
 
 void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
-                    bool emit, bool zeroed, hipStream_t s) {
+                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail) {
     if (rows == 0 || a.W == 0 || a.T == 0) return;
     const uint32_t keys = pb.ntx * pb.nty * PB_NZ;
     if (!zeroed) (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
     const dim3 lg((a.T + PB_LEAVES - 1) / PB_LEAVES);
-    hipLaunchKernelGGL((k_pb_bin<false>), lg, dim3(BLOCK), 0, s, a, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
+    if (tail) launch_pb_count_top(*tail, a, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx, lg.x, s);
+    else hipLaunchKernelGGL((k_pb_bin<false>), lg, dim3(BLOCK), 0, s, a, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
     const uint32_t sb = (keys + PB_SCAN - 1) / PB_SCAN;
     hipLaunchKernelGGL(k_pb_sums, dim3(sb), dim3(PB_SCAN), 0, s, pb.off, pb.sums, keys);
     hipLaunchKernelGGL(k_pb_scan, dim3(sb), dim3(PB_SCAN), 0, s, pb.off, pb.cur, pb.sums, keys);
