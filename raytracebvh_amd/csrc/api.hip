@@ -635,7 +635,13 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const PrimaryKind pkind = binned && (W > 32768u || H > 32768u) ? PrimaryKind::PACKET_WIDE : wk.primary;
     if (sort || my_bands < nsplit || slot || c->slots_used || binned) nsplit = 1;
     const bool fuse_tail = tail.pending && pkind == PrimaryKind::BINNED && s == c->stream && slot == 0 && rows > 0;
-    if (!fuse_tail) tail.run();   // before any walk reads the tree
+    if (!fuse_tail && tail.pending) {   // before any walk reads the tree
+        tail.run();
+        if (s != c->stream) {   // (a caller stream: ordered after it like after the build)
+            if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
+            HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+        }
+    }
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
