@@ -1245,7 +1245,14 @@ __device__ __forceinline__ float bf16_up(uint16_t h) { return __uint_as_float((u
 // rounded toward -inf (6 B each; the pop's prune test on the rounded-down distance keeps
 // every entry the exact test keeps), deeper entries as full pairs in scratch.
 constexpr int SB = 16;   // 16 x 4 B x 256 lanes = 16 KB per block
-constexpr int SW = 12;   // 12 x 6 B x 256 lanes = 18 KB per block (8 blocks per CU)
+// 13 x 6 B x 256 lanes = 19.5 KB per block: 8 blocks per CU in 160 KB.  A/B (C5 bounce stage):
+// 8 entries 2.75-2.77 ms (deeper entries go to scratch), 12 2.50-2.55, 13 2.47-2.52, 14 2.51-2.53
+// (7 blocks per CU)
+#ifndef RTBVH_SW
+#define RTBVH_SW 13
+#endif
+constexpr int SW = RTBVH_SW;
+static_assert(SW * 6 * 256 * 8 <= 160 * 1024, "the 4-wide bounce walk's LDS stack: 8 blocks per CU");
 
 // ---- the slack test of a quantized node --------------------------------------------------
 // The exact form (RTBVH_QBOX below) decodes each corner, org + q * scl, and runs the reference
@@ -1317,7 +1324,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     int sp = 0;
     float best = 0.f;
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
-    __shared__ uint32_t s_stk[WIDE ? 1 : SB][BLOCK];
+    __shared__ uint32_t s_stk[WIDE ? 1 : SB][WIDE ? 1 : BLOCK];   // (none for WIDE: its LDS is the 6-B stack)
     uint32_t stack[WIDE ? 1 : STACK_SIZE - SB];   // entries [SB, STACK_SIZE)
     __shared__ uint32_t s_wid[WIDE ? SW : 1][BLOCK];
     __shared__ uint16_t s_wt[WIDE ? SW : 1][BLOCK];
