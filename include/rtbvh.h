@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RTBVH_ABI_VERSION 5
+#define RTBVH_ABI_VERSION 6
 
 typedef enum {
     RTBVH_OK = 0,
@@ -128,17 +128,18 @@ enum {
                                              boxes share one 128-B line), keeping the lexicographic
                                              (t, leaf) minimum as NEAREST_FIRST does */
     RTBVH_FLAG_AUTO_WALK = 1u << 8,       /* choose the walks, ignoring the walk flags (the four above and
-                                             BINNED_PRIMARY), and return
-                                             the reference-order frame always: up to 65536 triangles the
-                                             reference-order kernels (exact by construction; the fastest on the
-                                             reference's own meshes); above that, per frame key (scene + camera
-                                             of the build, camera, size, bounces, band), the first frame is
-                                             traced in the reference order into the outputs AND with
-                                             NEAREST_FIRST | PACKET_PRIMARY | REFILL_BOUNCE | WIDE_BVH |
-                                             BINNED_PRIMARY into
-                                             scratch, compared on the device; the key's later frames take the
-                                             fast walks only if nothing differed (stats walk_state /
-                                             walk_checks / walk_fallbacks) */
+                                             BINNED_PRIMARY), and return the reference-order frame always: up
+                                             to 65536 triangles the reference-order kernels (exact by
+                                             construction; the fastest on the reference's own meshes); above
+                                             that, the CERTIFIED fast walks: BINNED_PRIMARY and
+                                             the 4-wide bounce walk, pruning on boxes grown by the triangle
+                                             test's rounding margin so that they see every triangle that could
+                                             be accepted below their bound, then a per-ray certificate (the
+                                             winning leaf's own box passes the reference slab test at its t);
+                                             the rays without one are re-traced in the reference order
+                                             (stats walk_state 2, redo_rays).  No per-frame or per-camera check.
+                                             The reference order throughout with a stack_limit below the
+                                             capacity or the CPUTests delta */
     RTBVH_FLAG_BINNED_PRIMARY = 1u << 9,  /* primary rays: every leaf listed in the 32 x 32 screen tiles its box
                                              covers (the set of orthographic primary rays a box passes is a
                                              pixel rectangle, recorded by the build), then per tile each listed
@@ -148,6 +149,8 @@ enum {
                                              dependent record fetches.  Frames up to 32768 pixels
                                              a side (larger ones take the 4-wide packet walk); a tile whose bins
                                              overflow takes the per-lane nearest-first walk */
+    RTBVH_FLAG_CERTIFIED = 1u << 10,      /* the certified fast walks of RTBVH_FLAG_AUTO_WALK whatever the scene's
+                                             size (the reference-order frame, per-ray certificates) */
     RTBVH_FLAG_MULTI_KERNEL_BUILD = 1u << 16, /* scenes of <= 2048 triangles: use the multi-kernel
                                               build instead of the one-workgroup build (same output) */
     /* bits 17..19: trace chains (0 = automatic, n = 1..4): a trace deals its bands over n
@@ -155,8 +158,9 @@ enum {
     RTBVH_FLAG_SPLIT_SHIFT = 17,
     RTBVH_FLAG_GRAPH = 1u << 20   /* rtbvh_compute_bvh replays one hipGraph of the whole frame (build +
                                      trace: ~20 launches and memsets), captured on the first call and
-                                     re-captured when W, H, bounces, the flags, the scene or the
-                                     camera change; no per-stage times (rtbvh_get_stats) */
+                                     re-captured when W, H, bounces, the flags or the scene change (not
+                                     the camera: the kernels read it from a device buffer updated before
+                                     each replay); no per-stage times (rtbvh_get_stats) */
 };
 
 typedef struct {
@@ -198,19 +202,20 @@ typedef struct {
     uint64_t graph_captures;   /* RTBVH_FLAG_GRAPH: frames captured so far (a replay captures nothing) */
     uint32_t walk_flags;       /* the walk flags the last trace's frame was traced with (RTBVH_FLAG_AUTO_WALK:
                                   the reference order, or the four walk flags once verified) */
-    uint32_t walk_state;       /* RTBVH_FLAG_AUTO_WALK, last trace: 0 the reference order by size (<= 65536
-                                  triangles) or no AUTO; 1 the frame key was being checked (the frame is the
-                                  reference order's); 2 fast walks, verified for this key; 3 reference order
-                                  because the check found the fast walks' frame differing (a fallback) */
+    uint32_t walk_state;       /* RTBVH_FLAG_AUTO_WALK, last trace: 0 the reference order (<= 65536 triangles,
+                                  a stack limit, the CPUTests delta) or no AUTO; 2 the certified fast walks */
     /* RTBVH_FLAG_COUNT_VISITS, wave-packet primary walks: wave steps (one record fetch for the
      * wave each) at internal nodes [0] and at leaves [1] */
     uint64_t packet_steps[2];
-    /* RTBVH_FLAG_AUTO_WALK: device checks run (one per new frame key) and those that found the
-     * fast walks' frame differing from the reference order's (the key stays on the reference order) */
+    /* RTBVH_FLAG_AUTO_WALK: traces run with the certified walks since rtbvh_create, and the rays the last
+     * one re-traced in the reference order (no certificate: redo_rays[0] + redo_rays[1]) */
     uint64_t walk_checks, walk_fallbacks;
     /* RTBVH_FLAG_COUNT_VISITS, RTBVH_FLAG_BINNED_PRIMARY: (leaf, screen tile) bin entries of the primary
      * pass [0] and those that passed the tile's 8 x 8-block bound test [1] (one leaf-record fetch each) */
     uint64_t bin_entries[2];
+    /* RTBVH_FLAG_AUTO_WALK, last trace: the rays re-traced in the reference order because their certificate
+     * failed, of the primary pass [0] and of the bounce passes [1] */
+    uint64_t redo_rays[2];
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 
@@ -417,6 +422,13 @@ rtbvh_status rtbvh_set_scene_obj(rtbvh_ctx* ctx, const rtbvh_scene* s, const rtb
 /* Graphics::onUpdate's camera (Graphics.cpp:44-53, Graphics.h:200-204):
  * LookAtLH(eye (0,5,-100), at 0, up +y) * PerspectiveFovLH(pi/4, H/W, 0.1, 1000). */
 void rtbvh_camera_reference(uint32_t width, uint32_t height, float wvp[16], float wv[16]);
+/* The same camera from any eye (at 0, up +y): Graphics::onUpdate after the eye has moved. */
+void rtbvh_camera_look(const float eye[3], uint32_t width, uint32_t height, float wvp[16], float wv[16]);
+/* Graphics::onKeyDown (Graphics.cpp:937-960): the eye rotated about `at` = 0 by CAM_DELTA = 0.1 rad
+ * (Graphics.h:14): key 0 VK_LEFT (RotationY(-0.1)), 1 VK_RIGHT (RotationY(0.1)), 2 VK_UP (RotationX(0.1)),
+ * 3 VK_DOWN (RotationX(-0.1)); the vector times the rotation matrix, row-vector convention (XMVector4Transform).
+ * Other keys leave the eye unchanged.  (DirectXMath's own sin/cos approximation is not restated: libm's.) */
+void rtbvh_camera_orbit(float eye[3], uint32_t key);
 
 #ifdef __cplusplus
 }

@@ -22,6 +22,7 @@ FLAG_PACKET_PRIMARY = 1 << 5
 FLAG_REFILL_BOUNCE = 1 << 6
 FLAG_WIDE_BVH = 1 << 7
 FLAG_BINNED_PRIMARY = 1 << 9   # primary rays by screen-tile bins of the leaves (include/rtbvh.h)
+FLAG_CERTIFIED = 1 << 10   # the certified fast walks whatever the size (include/rtbvh.h)
 FLAG_MULTI_KERNEL_BUILD = 1 << 16
 FLAG_AUTO_WALK = 1 << 8   # walks chosen by scene size (include/rtbvh.h)
 FLAG_SPLIT_SHIFT = 17   # trace chains: (n << FLAG_SPLIT_SHIFT), 0 = automatic
@@ -40,7 +41,7 @@ EXPORTS = [
     "rtbvh_scene_synthetic", "rtbvh_scene_free", "rtbvh_scene_num_vertices", "rtbvh_scene_num_indices",
     "rtbvh_scene_num_materials", "rtbvh_scene_num_textures", "rtbvh_scene_vertices", "rtbvh_scene_indices",
     "rtbvh_scene_mat_indices", "rtbvh_scene_materials", "rtbvh_scene_texture_path", "rtbvh_set_scene_obj",
-    "rtbvh_camera_reference", "rtbvh_texture_load_bmp", "rtbvh_texture_load_jpeg", "rtbvh_texture_decode_jpeg",
+    "rtbvh_camera_reference", "rtbvh_camera_look", "rtbvh_camera_orbit", "rtbvh_texture_load_bmp", "rtbvh_texture_load_jpeg", "rtbvh_texture_decode_jpeg",
     "rtbvh_texture_load", "rtbvh_texture_free", "rtbvh_srgb_table",
     "rtbvh_present", "rtbvh_save_bmp", "rtbvh_assemble_bands", "rtbvh_comm_unique_id", "rtbvh_comm_init",
     "rtbvh_comm_destroy", "rtbvh_trace_tiles",
@@ -80,7 +81,7 @@ class Stats(ctypes.Structure):
                 ("graph_captures", ctypes.c_uint64), ("walk_flags", ctypes.c_uint32),
                 ("walk_state", ctypes.c_uint32), ("packet_steps", ctypes.c_uint64 * 2),
                 ("walk_checks", ctypes.c_uint64), ("walk_fallbacks", ctypes.c_uint64),
-                ("bin_entries", ctypes.c_uint64 * 2)]
+                ("bin_entries", ctypes.c_uint64 * 2), ("redo_rays", ctypes.c_uint64 * 2)]
 
     def as_dict(self) -> dict:
         d = {}
@@ -170,6 +171,8 @@ def lib() -> ctypes.CDLL:
         "rtbvh_scene_texture_path": (ctypes.c_char_p, [vp, u32]),
         "rtbvh_set_scene_obj": (i32, [vp, vp, vp, u32]),
         "rtbvh_camera_reference": (None, [u32, u32, vp, vp]),
+        "rtbvh_camera_look": (None, [vp, u32, u32, vp, vp]),
+        "rtbvh_camera_orbit": (None, [vp, u32]),
         "rtbvh_texture_load_bmp": (i32, [ctypes.c_char_p, vp]),
         "rtbvh_texture_load_jpeg": (i32, [ctypes.c_char_p, vp]),
         "rtbvh_texture_decode_jpeg": (i32, [vp, ctypes.c_size_t, vp]),

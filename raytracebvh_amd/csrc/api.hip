@@ -33,6 +33,8 @@ struct rtbvh_ctx {
     uint32_t* d_matidx = nullptr;
     Mat* d_mats = nullptr;
     float wvp[16], wv[16];
+    float* d_cam = nullptr;     // [32] the kernels' camera (BuildArgs::cam): WVP, WV, uploaded in stream order
+    bool cam_dirty = false;     //   (sync_camera) when set_camera changed it
     bool have_scene = false, have_camera = false, built = false;
     bool built_clz64 = false;   // the BVH was built with the clz64 delta: a valid tree (no cycles)
 
@@ -141,29 +143,21 @@ struct rtbvh_ctx {
     struct TraceState {
         uint32_t W, H, bounces, nsplit;
         size_t rec_P;
+        uint32_t walk, walk_state;
+        bool cert;
     } graph_state{};
-    // RTBVH_FLAG_AUTO_WALK above AUTO_WALK_MAX_TRIS: a frame key (scene and camera of the build,
-    // camera, size, bounces, band) takes the fast walks only after one of its frames was traced
-    // both ways and compared on the device (enqueue_trace); until then, and for good after a
-    // mismatch, it takes the reference-order walks (findCollision's DFS)
-    uint64_t scene_gen = 0, cam_gen = 0;              // bumped by set_scene / a changed camera
-    uint64_t built_scene_gen = 0, built_cam_gen = 0;  // ... as of the last build
-    static constexpr int VKEYS = 8;
-    struct WalkKey { uint64_t w[4]; };
-    WalkKey vkeys[VKEYS] = {};                        // decided keys, ring
-    bool vfast[VKEYS] = {};                           //   true: fast walks verified; false: reference order
-    uint32_t nvkeys = 0;
-    bool vpending = false;                            // a check in flight (one at a time)
-    WalkKey vpend_key{};
-    hipEvent_t ev_verify = nullptr;
-    unsigned long long* d_vdiff = nullptr;            // differing pixels + intensities of the check
-    unsigned long long* h_vdiff = nullptr;            //   (pinned copy)
-    float4* d_vcolor = nullptr;                       // the fast walks' frame of a check
-    float* d_vinten = nullptr;
-    size_t cap_v = 0;
-    uint64_t walk_checks = 0, walk_fallbacks = 0;
+    // RTBVH_FLAG_AUTO_WALK above AUTO_WALK_MAX_TRIS: the certified fast walks: per buffer
+    // set, the list of rays a pass re-traces in the reference order (their counts: d_qcount 16..31)
+    uint32_t* d_redo[MAXSPLIT] = {};
+    size_t cap_redo[MAXSPLIT] = {};
+    uint64_t walk_checks = 0;                         // certified traces so far
     uint32_t last_walk = 0;                           // walk flags of the last trace
     uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
+    bool last_cert = false;                           // the last trace was certified (its re-trace counts)
+    // tuning knobs of A/B runs, read once by rtbvh_create (RTBVH_BOUNCE_BLOCKS, RTBVH_OVERLAP,
+    // RTBVH_SIDE_PRIORITY): a shipped context does not change its launches per frame
+    uint32_t knob_bounce_blocks = 0;
+    bool knob_overlap = false, knob_side_priority = true;
     // the band deal of band traces (rtbvh_set_band_deal): rank 0's weight in 1/16 of another rank's
     uint32_t root_share = 16;
     struct DealTab {   // a weighted deal's device table: every rank's bands, then slots[b] = r << 24 | pos
@@ -171,7 +165,8 @@ struct rtbvh_ctx {
         uint32_t* d;
         std::vector<uint32_t> off;   // rank r's bands at d[off[r] .. off[r + 1])
     };
-    std::deque<DealTab> deals;       // one per (H, nranks, share) used; kept until destroy (traces in flight read them)
+    std::deque<DealTab> deals;       // the MAX_DEALS most recently used (H, nranks, share), most recent first
+    static constexpr size_t MAX_DEALS = 8;
 };
 
 namespace {
@@ -237,9 +232,9 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_cnt, ni));
     HIPC(c, dalloc(c->d_xlist, n));
     HIPC(c, dalloc(c->d_xcnt, refit_blocks(T)));
-    HIPC(c, dalloc(c->d_zpart, 2 * (size_t)refit_blocks(T)));
+    HIPC(c, dalloc(c->d_zpart, ZPART * (size_t)refit_blocks(T)));
     HIPC(c, dalloc(c->d_bounds, BOUNDS_WORDS));
-    HIPC(c, dalloc(c->d_rootbox, 8));
+    HIPC(c, dalloc(c->d_rootbox, ROOTBOX_WORDS));
     c->cap_T = T;
     return RTBVH_OK;
 }
@@ -332,7 +327,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.T = c->T;
     a.morton_mode = (int)c->cfg.morton_mode;
     a.delta_mode = (int)c->cfg.delta_mode;
-    memcpy(a.wvp.m, c->wvp, sizeof(c->wvp));
+    a.cam = c->d_cam;
     memcpy(a.smin, c->cfg.scene_bb_min, 12);
     memcpy(a.smax, c->cfg.scene_bb_max, 12);
     a.bounds = c->d_bounds;
@@ -358,7 +353,8 @@ BuildArgs build_args(rtbvh_ctx* c) {
     // context's walks include a packet primary walk (AUTO and the binned pass take none)
     // (choose_walks: a packet primary walk iff PACKET_PRIMARY without BINNED_PRIMARY)
     const uint32_t f = c->cfg.flags;
-    a.pseudo = (f & RTBVH_FLAG_PACKET_PRIMARY) && !(f & (RTBVH_FLAG_BINNED_PRIMARY | RTBVH_FLAG_AUTO_WALK));
+    a.pseudo = (f & RTBVH_FLAG_PACKET_PRIMARY) &&
+               !(f & (RTBVH_FLAG_BINNED_PRIMARY | RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_CERTIFIED));
     return a;
 }
 
@@ -405,17 +401,31 @@ uint32_t deal_max_rows(uint32_t H, uint32_t nranks, uint32_t share) {
     for (uint32_t r = 0; r < nranks; r++) m = std::max(m, deal_rows(H, r, nranks, share));
     return m;
 }
-// The device table of a weighted deal (null for round-robin: the kernels compute it).  Uploaded
-// synchronously on first use, so not from inside a graph capture (whose frames have one rank).
+rtbvh_status sync_all(rtbvh_ctx* c);
+// The device table of a weighted deal (null for round-robin: the kernels compute it).  Uploaded on
+// first use (a few KB, once per frame size and deal), so not from inside a graph capture (whose frames
+// have one rank).  The MAX_DEALS most recently used tables are kept; evicting one first waits for the
+// context's work (traces in flight may read it).
 rtbvh_status get_deal(rtbvh_ctx* c, uint32_t H, uint32_t nranks, const rtbvh_ctx::DealTab** out) {
     *out = nullptr;
     if (c->root_share == 16 || nranks <= 1) return RTBVH_OK;
-    for (const auto& t : c->deals)
-        if (t.H == H && t.nranks == nranks && t.share == c->root_share) {
-            *out = &t;
+    for (auto it = c->deals.begin(); it != c->deals.end(); ++it)
+        if (it->H == H && it->nranks == nranks && it->share == c->root_share) {
+            if (it != c->deals.begin()) {   // most recent first
+                rtbvh_ctx::DealTab t = std::move(*it);
+                c->deals.erase(it);
+                c->deals.push_front(std::move(t));
+            }
+            *out = &c->deals.front();
             return RTBVH_OK;
         }
     if (c->capturing) return fail(c, RTBVH_ERR_INVALID_ARG, "a new band deal inside a graph capture");
+    if (c->deals.size() >= rtbvh_ctx::MAX_DEALS) {
+        rtbvh_status st = sync_all(c);
+        if (st) return st;
+        dfree(c->deals.back().d);
+        c->deals.pop_back();
+    }
     std::vector<uint32_t> owner;
     deal_owners(H, nranks, c->root_share, owner);
     const uint32_t nb = (uint32_t)owner.size();
@@ -430,8 +440,8 @@ rtbvh_status get_deal(rtbvh_ctx* c, uint32_t H, uint32_t nranks, const rtbvh_ctx
     }
     HIPC(c, hipMalloc((void**)&t.d, host.size() * sizeof(uint32_t)));
     HIPC(c, hipMemcpy(t.d, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    c->deals.push_back(std::move(t));
-    *out = &c->deals.back();
+    c->deals.push_front(std::move(t));
+    *out = &c->deals.front();
     return RTBVH_OK;
 }
 
@@ -461,7 +471,7 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     const uint32_t nb = (H + 7) / 8;
     a.my_bands = rank < nb ? (nb - rank + nranks - 1) / nranks : 0;   // round-robin; enqueue_walks sets a deal's
     a.band_list = nullptr;
-    memcpy(a.wv.m, c->wv, sizeof(c->wv));
+    a.cam = c->d_cam;
     a.color = color;
     a.intensity = inten;
     a.counters = c->d_counters;
@@ -558,10 +568,43 @@ rtbvh_status check_launch(rtbvh_ctx* c, const char* what) {
     return RTBVH_OK;
 }
 
+// the context stream and the frames in flight on caller streams, drained
+rtbvh_status sync_all(rtbvh_ctx* c) {
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)
+        if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
+    return RTBVH_OK;
+}
+
+// The camera the kernels read (BuildArgs::cam), uploaded in stream order on the context stream when
+// rtbvh_set_camera changed it -- after the frames in flight, which read the old one -- and ordered
+// before stream s.  A captured frame (RTBVH_FLAG_GRAPH) reads the buffer, so it survives a camera change
+// (Graphics::onUpdate writes the camera every frame and the arrow keys orbit it, Graphics.cpp:40-56,
+// 937-960).  The source is pageable (the matrices in the context), so the copy is staged at the call.
+rtbvh_status sync_camera(rtbvh_ctx* c, hipStream_t s) {
+    if (!c->cam_dirty) return RTBVH_OK;
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)
+        if (c->slot_busy[k]) {
+            HIPC(c, hipStreamWaitEvent(c->stream, c->ev_slot[k], 0));
+            c->slot_busy[k] = false;
+        }
+    HIPC(c, hipMemcpyAsync(c->d_cam, c->wvp, sizeof(c->wvp), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_cam + 16, c->wv, sizeof(c->wv), hipMemcpyHostToDevice, c->stream));
+    if (s != c->stream) {
+        HIPC(c, hipEventRecord(c->ev_built, c->stream));
+        HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+    }
+    c->cam_dirty = false;
+    return RTBVH_OK;
+}
+
 // The kernels of one trace with the walks of `flags` (timed: record the stage events when
 // RTBVH_FLAG_TIMING asks for them).
+// cert: the certified walks (flags = the fast walks: binned primary pass, 4-wide bounce walk):
+// every pass checks each ray's certificate and re-traces the rays that fail it in the reference order.
 rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
-                           float4* color, float* inten, hipStream_t s, uint32_t slot, uint32_t flags, bool timed) {
+                           float4* color, float* inten, hipStream_t s, uint32_t slot, uint32_t flags, bool timed,
+                           bool cert = false) {
     const bool leaf_pending = c->leaf_pending;   // (this trace is the first after the build or none is)
     c->leaf_pending = false;
     // the build's crossing nodes, if left to this trace: run in the binned pass's launches below, or
@@ -607,10 +650,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
 #define RTBVH_BOUNCE_GRID (256 * BOUNCE_WAVES)
 #endif
     uint32_t tblocks = P < (1u << 22) ? 1024 : RTBVH_BOUNCE_GRID;
-    if (const char* e = getenv("RTBVH_BOUNCE_BLOCKS")) {   // tuning override (A/B runs)
-        const int v = atoi(e);
-        if (v > 0) tblocks = (uint32_t)v;
-    }
+    if (c->knob_bounce_blocks) tblocks = c->knob_bounce_blocks;   // tuning override (A/B runs)
     if (records) {
         if (c->cap_rec < P) {
             drop_graph(c);
@@ -632,7 +672,10 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     // are exact for frames of up to 32768 pixels a side (rtbvh_device.h leaf_footprint)
     const uint32_t rows = P / W;
     const bool binned = wk.primary == PrimaryKind::BINNED;
-    const PrimaryKind pkind = binned && (W > 32768u || H > 32768u) ? PrimaryKind::PACKET_WIDE : wk.primary;
+    // (a certified trace past that size: the reference-order lane walk, exact by construction)
+    const PrimaryKind pkind = binned && (W > 32768u || H > 32768u)
+                                  ? (cert ? PrimaryKind::LANE_REFERENCE : PrimaryKind::PACKET_WIDE)
+                                  : wk.primary;
     if (sort || my_bands < nsplit || slot || c->slots_used || binned) nsplit = 1;
     const bool fuse_tail = tail.pending && pkind == PrimaryKind::BINNED && s == c->stream && slot == 0 && rows > 0;
     if (!fuse_tail && tail.pending) {   // before any walk reads the tree
@@ -654,6 +697,12 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         c->pseudo_ok = true;
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
         if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+    }
+    // a certified trace's re-trace list (one chain: buffer set `slot`; counts at d_qcount 16 + pass)
+    if (cert && c->cap_redo[slot] < P) {
+        drop_graph(c);
+        HIPC(c, dalloc(c->d_redo[slot], P));
+        c->cap_redo[slot] = P;
     }
     // the binned pass's buffers (one chain: buffer set `slot`)
     const uint32_t ntx = pb_tiles_x(W), nty = pb_tiles_y(rows);
@@ -703,14 +752,15 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             const PrimBins pb{pbb.off, pbb.cur, pbb.bins, pbb.keys, pbb.sums, pbb.cap_bins, ntx, nty};
             if (rows) {
                 const BuildArgs ba = build_args(c);
+                const Redo rd{c->d_redo[b], &qc[16]};
                 launch_pb_pass(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, overlap ? sp : sg,
-                               fuse_tail ? &ba : nullptr);
+                               fuse_tail ? &ba : nullptr, cert ? &rd : nullptr);
                 if (fuse_tail) tail.pending = false;
                 if (overlap) {
                     HIPC(c, hipEventRecord(c->ev_prim, sp));
                     HIPC(c, hipStreamWaitEvent(sg, c->ev_prim, 0));
                 }
-                launch_pb_gate(ag, pb, q[0], &qc[0], count, bounces > 0, sg);
+                launch_pb_gate(ag, pb, q[0], &qc[0], count, bounces > 0, sg, cert);
             } else if (overlap) {   // (nothing traced: the zeroing still joins)
                 HIPC(c, hipEventRecord(c->ev_prim, sp));
                 HIPC(c, hipStreamWaitEvent(sg, c->ev_prim, 0));
@@ -728,10 +778,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             if (refill) {
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[3], sg));
                 launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, wk.bounce, hit,
-                                       nx + (size_t)NEXT_SEGS * NEXT_STRIDE * b, tblocks, sg);
+                                       nx + (size_t)NEXT_SEGS * NEXT_STRIDE * b, tblocks, sg, cert);
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[4], sg));
+                const Redo rd{c->d_redo[slot], &qc[17 + b]};
                 launch_bounce_shade(ag, q[b & 1], &qc[b], hit, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
-                                    Pg, sg);
+                                    Pg, sg, cert ? &rd : nullptr);
             } else
                 launch_bounce(ag, q[b & 1], &qc[b], perm, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
                               wk.nearest, sg);
@@ -759,101 +810,49 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     c->frame_here = color == c->d_color && nranks == 1;
     c->intensity_here = c->frame_here && inten != nullptr;
     c->last_walk = flags & WALK_FLAGS;
+    c->last_cert = cert;
     return check_launch(c, "trace kernels");
 }
 
-// ---- RTBVH_FLAG_AUTO_WALK: the fast walks only where a device check found them exact --------
-// The 4-wide nearest-first walks return the lexicographic (t, leaf) minimum over the leaves they
-// reach, findCollision (RayTraceTraversal.hlsl:106-193) the first strict minimum over the leaves
-// IT reaches; the two agree whenever the hit lies inside every box on its root path under the
-// same rounding ("containment").  When containment fails the walks can differ
-// (tests/containment.py builds such a scene: two coplanar triangles whose Moller-Trumbore t
-// rounds below their slab entry).  No cheap per-ray certificate exists -- the hit a walk misses
-// lies in a subtree it pruned, unvisited -- so the check is per frame: the first frame of a key
-// is traced with the fast walks into scratch AND with the reference order into the outputs, and
-// the two are compared on the device.  The outputs are always the reference frame; the key takes
-// the fast walks from its next frame on only if nothing differed.  The build is deterministic, so
-// frames of one key are identical.
-rtbvh_ctx::WalkKey walk_key(const rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank,
-                            uint32_t nranks) {
-    rtbvh_ctx::WalkKey k;
-    k.w[0] = c->built_scene_gen << 32 | (c->built_cam_gen & 0xFFFFFFFFu);
-    k.w[1] = c->cam_gen;
-    k.w[2] = (uint64_t)W | (uint64_t)H << 32;
-    k.w[3] = (uint64_t)bounces | (uint64_t)rank << 8 | (uint64_t)c->root_share << 24 | (uint64_t)nranks << 32;
-    return k;
-}
-int find_walk_key(const rtbvh_ctx* c, const rtbvh_ctx::WalkKey& k) {
-    const uint32_t n = c->nvkeys < (uint32_t)rtbvh_ctx::VKEYS ? c->nvkeys : rtbvh_ctx::VKEYS;
-    for (uint32_t i = 0; i < n; i++)
-        if (memcmp(&c->vkeys[i], &k, sizeof(k)) == 0) return (int)i;
-    return -1;
-}
-// Take the result of the check in flight once its event has completed (wait: block on it).
-void resolve_walk_check(rtbvh_ctx* c, bool wait) {
-    if (!c->vpending) return;
-    const hipError_t e = wait ? hipEventSynchronize(c->ev_verify) : hipEventQuery(c->ev_verify);
-    if (e == hipErrorNotReady) return;
-    c->vpending = false;
-    if (e != hipSuccess) return;   // undecided: the key is checked again
-    const bool fast = *c->h_vdiff == 0;
-    if (!fast) c->walk_fallbacks++;
-    const uint32_t i = c->nvkeys++ % rtbvh_ctx::VKEYS;
-    c->vkeys[i] = c->vpend_key;
-    c->vfast[i] = fast;
+// ---- RTBVH_FLAG_AUTO_WALK: the certified fast walks ---------------------------------
+// The fast walks return the lexicographic (t, leaf) minimum over the leaves they reach, findCollision
+// (RayTraceTraversal.hlsl:106-193) the first strict minimum over the leaves IT reaches; they agree
+// whenever every hit lies inside the boxes on its root path under the same rounding ("containment").
+// Where containment fails they can differ (tests/containment.py).  The certified walks make each ray
+// carry its own proof: they prune on boxes grown by the rounding margin of the triangle test
+// (margin.h), so they see every triangle that could be accepted below their bound -- the minimum they
+// return is the minimum over every triangle the reference could test -- and a ray's answer is the
+// reference's when its winning leaf's own box passes the reference slab test at that t (the
+// certificate).  Rays without one are re-traced in the reference order.  No per-frame check, no frame
+// key: a moving camera costs nothing extra, and a captured frame replays as it is.
+// The walks of a trace: (flags, certified)
+struct TracePlan {
+    uint32_t flags;
+    bool cert;
+    uint32_t state;   // rtbvh_stats.walk_state
+};
+TracePlan plan_trace(const rtbvh_ctx* c, uint32_t f) {
+    if (!(f & (RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_CERTIFIED))) return TracePlan{f, false, 0};
+    const uint32_t ref = f & ~WALK_FLAGS;
+    // the certificate speaks for the reference order on a clz64 tree with the full stack (a run-time
+    // stack limit makes the reference order end rays early, which no fast walk reproduces)
+    const bool limited = c->cfg.stack_limit != 0 && c->cfg.stack_limit < (uint32_t)STACK_SIZE;
+    const bool want = (f & RTBVH_FLAG_CERTIFIED) || auto_checked(c);
+    if (!want || !c->built_clz64 || limited) return TracePlan{ref, false, 0};
+    return TracePlan{ref | RTBVH_FLAG_NEAREST_FIRST | RTBVH_FLAG_REFILL_BOUNCE | RTBVH_FLAG_WIDE_BVH |
+                         RTBVH_FLAG_BINNED_PRIMARY,
+                     true, 2};
 }
 
 rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces, uint32_t rank, uint32_t nranks,
                            float4* color, float* inten, hipStream_t s, uint32_t slot = 0) {
-    const uint32_t f = c->cfg.flags;
-    if (!(f & RTBVH_FLAG_AUTO_WALK)) {
-        c->last_walk_state = 0;
-        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, f, true);
-    }
-    const uint32_t ref = f & ~WALK_FLAGS, fast = ref | WALK_FLAGS;
-    if (!auto_checked(c)) {   // small scenes: the reference order, the fastest there
-        c->last_walk_state = 0;
-        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, ref, true);
-    }
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
-    resolve_walk_check(c, false);
-    const rtbvh_ctx::WalkKey key = walk_key(c, W, H, bounces, rank, nranks);
-    const int known = find_walk_key(c, key);
-    if (known >= 0) {
-        const bool fw = c->vfast[known];
-        c->last_walk_state = fw ? 2 : 3;
-        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, fw ? fast : ref, true);
-    }
-    // undecided: the reference order while another check is in flight, inside a graph capture
-    // (compute_graph decides the key with its plain frame first) and for the RayPresent records
-    if (c->vpending || c->capturing || (f & RTBVH_FLAG_REFRACT_RECORDS)) {
-        c->last_walk_state = 1;
-        return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, ref, true);
-    }
-    if (!color) color = c->d_color;
-    const size_t n = (size_t)W * deal_rows(H, rank, nranks, c->root_share);
-    if (c->cap_v < n) {
-        HIPC(c, dalloc(c->d_vcolor, n));
-        HIPC(c, dalloc(c->d_vinten, n));
-        c->cap_v = n;
-    }
-    if (!c->d_vdiff) HIPC(c, dalloc(c->d_vdiff, 1));
-    if (!c->h_vdiff) HIPC(c, hipHostMalloc((void**)&c->h_vdiff, sizeof(unsigned long long), hipHostMallocDefault));
-    if (!c->ev_verify) HIPC(c, hipEventCreateWithFlags(&c->ev_verify, hipEventDisableTiming));
-    rtbvh_status st =
-        enqueue_walks(c, W, H, bounces, rank, nranks, c->d_vcolor, inten ? c->d_vinten : nullptr, s, slot, fast, false);
-    if (!st) st = enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, ref, true);
+    rtbvh_status st = sync_camera(c, s);
     if (st) return st;
-    HIPC(c, hipMemsetAsync(c->d_vdiff, 0, sizeof(unsigned long long), s));
-    launch_count_diff(c->d_vcolor, color, n, c->d_vdiff, s);
-    if (inten) launch_count_diff32(c->d_vinten, inten, n, c->d_vdiff, s);
-    HIPC(c, hipMemcpyAsync(c->h_vdiff, c->d_vdiff, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    HIPC(c, hipEventRecord(c->ev_verify, s));
-    c->vpending = true;
-    c->vpend_key = key;
-    c->walk_checks++;
-    c->last_walk_state = 1;
-    return check_launch(c, "walk check");
+    const TracePlan p = plan_trace(c, c->cfg.flags);
+    c->last_walk_state = p.state;
+    if (p.cert && !c->capturing) c->walk_checks++;
+    return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, p.flags, true, p.cert);
 }
 
 }  // namespace
@@ -924,6 +923,15 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
         return fail(nullptr, RTBVH_ERR_OOM, "overflow counter allocation failed");
     }
     memset(c->h_ovf, 0, sizeof(unsigned long long) * rtbvh_ctx::MAXSPLIT);
+    if (hipMalloc((void**)&c->d_cam, 32 * sizeof(float)) != hipSuccess ||
+        hipMemset(c->d_cam, 0, 32 * sizeof(float)) != hipSuccess) {
+        rtbvh_destroy(c);
+        return fail(nullptr, RTBVH_ERR_OOM, "camera buffer allocation failed");
+    }
+    // A/B tuning knobs, read once here (not per frame)
+    if (const char* e = getenv("RTBVH_BOUNCE_BLOCKS")) c->knob_bounce_blocks = (uint32_t)std::max(0, atoi(e));
+    if (const char* e = getenv("RTBVH_OVERLAP")) c->knob_overlap = atoi(e) != 0;
+    if (const char* e = getenv("RTBVH_SIDE_PRIORITY")) c->knob_side_priority = atoi(e) != 0;
     *out = c;
     return RTBVH_OK;
 }
@@ -966,10 +974,9 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_texels); dfree(c->d_texinfo); dfree(c->d_srgb);
     dfree(c->d_counters);
     dfree(c->d_ovf);
-    dfree(c->d_vcolor); dfree(c->d_vinten); dfree(c->d_vdiff);
+    for (auto& r : c->d_redo) dfree(r);
+    dfree(c->d_cam);
     for (auto& t : c->deals) dfree(t.d);
-    if (c->h_vdiff) (void)hipHostFree(c->h_vdiff);
-    if (c->ev_verify) (void)hipEventDestroy(c->ev_verify);
     if (c->h_ovf) (void)hipHostFree(c->h_ovf);
     for (auto& row : c->evb)
         for (auto& e : row)
@@ -1059,22 +1066,20 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
     }
     c->have_scene = true;
     c->built = false;
-    c->scene_gen++;
     return RTBVH_OK;
 }
 
 rtbvh_status rtbvh_set_camera(rtbvh_ctx* c, const float wvp[16], const float wv[16]) {
     if (!c || !wvp || !wv) return RTBVH_ERR_INVALID_ARG;
-    // Graphics::onUpdate writes the same matrices every frame (Graphics.cpp:44-53): a
-    // captured frame (RTBVH_FLAG_GRAPH), whose kernels hold the camera, is kept unless
-    // the matrices change
+    // Graphics::onUpdate writes the matrices every frame (Graphics.cpp:44-53); the kernels read them
+    // from a device buffer (sync_camera), so a captured frame (RTBVH_FLAG_GRAPH) replays with the new
+    // camera as it is
     if (c->have_camera && memcmp(c->wvp, wvp, sizeof(c->wvp)) == 0 && memcmp(c->wv, wv, sizeof(c->wv)) == 0)
         return RTBVH_OK;
     memcpy(c->wvp, wvp, sizeof(c->wvp));
     memcpy(c->wv, wv, sizeof(c->wv));
     c->have_camera = true;
-    c->cam_gen++;
-    drop_graph(c);
+    c->cam_dirty = true;
     return RTBVH_OK;
 }
 
@@ -1090,6 +1095,8 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
             HIPC(c, hipStreamWaitEvent(s, c->ev_slot[k], 0));
             c->slot_busy[k] = false;
         }
+    rtbvh_status cst = sync_camera(c, s);
+    if (cst) return cst;
     hipEvent_t* ev = c->evb[c->n_builds % rtbvh_ctx::RING];
     if (timing) HIPC(c, hipEventRecord(ev[0], s));
     if (c->T <= small_build_max() && !(c->cfg.flags & RTBVH_FLAG_MULTI_KERNEL_BUILD)) {
@@ -1108,8 +1115,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
         c->built = true;
         c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
-        c->built_scene_gen = c->scene_gen;
-        c->built_cam_gen = c->cam_gen;
         return check_launch(c, "build kernel");
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
@@ -1131,7 +1136,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         if (!c->side) {   // high priority: its workgroups go first while the crossing nodes' fill the CUs
             int lo = 0, hi = 0;
             HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-            if (const char* e = getenv("RTBVH_SIDE_PRIORITY")) if (atoi(e) == 0) hi = lo;   // (A/B runs)
+            if (!c->knob_side_priority) hi = lo;   // (A/B runs: RTBVH_SIDE_PRIORITY=0)
             HIPC(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi));
         }
         if (!c->ev_leaf) HIPC(c, hipEventCreateWithFlags(&c->ev_leaf, hipEventDisableTiming));
@@ -1146,8 +1151,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
     c->built = true;
     c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
-    c->built_scene_gen = c->scene_gen;
-    c->built_cam_gen = c->cam_gen;
     return check_launch(c, "build kernels");
 }
 
@@ -1186,22 +1189,22 @@ static rtbvh_status flush_tail(rtbvh_ctx* c, rtbvh_status st) {
     return st;
 }
 
-static bool side_overlap() {
-    const char* e = getenv("RTBVH_OVERLAP");
-    return e && atoi(e) != 0;
-}
+static bool side_overlap(const rtbvh_ctx* c) { return c->knob_overlap; }
 
 // RTBVH_FLAG_GRAPH: Graphics.cpp:56 rebuilds and traces every frame, ~20 launches and memsets
 // of little work each on the reference's own meshes; the frame is captured once into a
 // hipGraph and replayed.  A plain frame runs first so that every buffer exists before the
-// capture; kernel arguments (camera, sizes, buffers) are baked into the graph, hence the key
-// and the drop on set_scene / set_camera.
+// capture; kernel arguments (sizes, buffers) are baked into the graph, hence the key and the
+// drop on set_scene and reallocations.  The camera is not: the kernels read it from the
+// context's camera buffer, updated before each replay (sync_camera), so a moving camera
+// (Graphics::onKeyDown, Graphics.cpp:937-960) replays the same graph; and the certified walks
+// (plan_trace) need no per-camera decision.
 static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
     const uint64_t key[5] = {W, H, bounces, (uint64_t)c->cfg.flags | (uint64_t)c->T << 32,
                              (uint64_t)c->slots_used | (uint64_t)c->cfg.stack_limit << 1};
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
         drop_graph(c);
-        c->leaf_want = side_overlap();
+        c->leaf_want = side_overlap(c);
         c->tail_want = true;
         rtbvh_status st = rtbvh_build_async(c);
         c->leaf_want = c->tail_want = false;
@@ -1211,7 +1214,7 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
         if (st && st != RTBVH_ERR_STACK_OVERFLOW) return st;
         HIPC(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         c->capturing = true;
-        c->leaf_want = side_overlap();
+        c->leaf_want = side_overlap(c);
         c->tail_want = true;
         st = rtbvh_build_async(c);
         c->leaf_want = c->tail_want = false;
@@ -1227,7 +1230,8 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
         c->graph = g;
         HIPC(c, hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
         memcpy(c->graph_key, key, sizeof(key));
-        c->graph_state = rtbvh_ctx::TraceState{c->W, c->H, c->bounces, c->nsplit, c->rec_P};
+        c->graph_state = rtbvh_ctx::TraceState{c->W,     c->H,         c->bounces,        c->nsplit,
+                                                c->rec_P, c->last_walk, c->last_walk_state, c->last_cert};
         c->graph_captures++;
     }
     // the replayed build rewrites the BVH (and a split trace the slot queues): after the
@@ -1237,6 +1241,8 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
             HIPC(c, hipStreamWaitEvent(c->stream, c->ev_slot[k], 0));
             c->slot_busy[k] = false;
         }
+    rtbvh_status cst = sync_camera(c, c->stream);   // this frame's camera, before the replay
+    if (cst) return cst;
     HIPC(c, hipGraphLaunch(c->graph_exec, c->stream));
     HIPC(c, hipEventRecord(c->ev_built, c->stream));
     // the host-side state of the captured trace (a trace in between may have changed it)
@@ -1246,6 +1252,10 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
     c->bounces = g.bounces;
     c->nsplit = g.nsplit;
     c->rec_P = g.rec_P;
+    c->last_walk = g.walk;
+    c->last_walk_state = g.walk_state;
+    c->last_cert = g.cert;
+    if (g.cert) c->walk_checks++;
     c->rank = 0;
     c->nranks = 1;
     c->last_slot = 0;
@@ -1258,7 +1268,7 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
 rtbvh_status rtbvh_compute_bvh(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounces) {
     if (!c) return RTBVH_ERR_INVALID_ARG;
     if (c->cfg.flags & RTBVH_FLAG_GRAPH) return compute_graph(c, W, H, bounces);
-    c->leaf_want = side_overlap();
+    c->leaf_want = side_overlap(c);
     c->tail_want = true;
     rtbvh_status st = rtbvh_build_async(c);
     c->leaf_want = c->tail_want = false;
@@ -1284,13 +1294,18 @@ rtbvh_status rtbvh_verify_walk(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
     unsigned long long* d_diff = nullptr;
     HIPC(c, hipMallocAsync((void**)&ref, n * sizeof(float4) + 256, c->stream));
     d_diff = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ref) + n * sizeof(float4));
-    // the reference order, then the walks the context would take for a key it has verified (AUTO:
-    // the fast walks above AUTO_WALK_MAX_TRIS), without the ray records
+    // the reference order, then the walks the context takes (AUTO: the certified fast walks above
+    // AUTO_WALK_MAX_TRIS), without the ray records
     const uint32_t f = c->cfg.flags & ~RTBVH_FLAG_REFRACT_RECORDS;
-    const uint32_t refw = f & ~WALK_FLAGS;
-    const uint32_t mine = (f & RTBVH_FLAG_AUTO_WALK) ? (auto_checked(c) ? refw | WALK_FLAGS : refw) : f;
-    st = enqueue_walks(c, W, H, bounces, 0, 1, ref, nullptr, c->stream, 0, refw, true);
-    if (!st) st = enqueue_walks(c, W, H, bounces, 0, 1, c->d_color, c->d_intensity, c->stream, 0, mine, true);
+    const uint32_t refw = f & ~(WALK_FLAGS | RTBVH_FLAG_AUTO_WALK);
+    const TracePlan mine = plan_trace(c, f);
+    st = sync_camera(c, c->stream);
+    if (!st) st = enqueue_walks(c, W, H, bounces, 0, 1, ref, nullptr, c->stream, 0, refw, true);
+    if (!st) {
+        c->last_walk_state = mine.state;
+        st = enqueue_walks(c, W, H, bounces, 0, 1, c->d_color, c->d_intensity, c->stream, 0, mine.flags, true,
+                           mine.cert);
+    }
     unsigned long long diff = 0;
     if (!st) {
         hipError_t e = hipMemsetAsync(d_diff, 0, sizeof(unsigned long long), c->stream);
@@ -1469,7 +1484,6 @@ rtbvh_status rtbvh_synchronize(rtbvh_ctx* c) {
     HIPC(c, hipStreamSynchronize(c->stream));
     for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)   // and the frames in flight on caller streams
         if (c->slot_busy[k]) HIPC(c, hipEventSynchronize(c->ev_slot[k]));
-    resolve_walk_check(c, true);
     // each trace ends by copying the never-reset overflow word into its slot's pinned word
     unsigned long long ovf = c->ovf_seen;
     for (uint32_t k = 0; k < rtbvh_ctx::MAXSPLIT; k++)
@@ -1669,11 +1683,16 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         out->bin_entries[0] = w[2];
         out->bin_entries[1] = w[3];
     }
-    resolve_walk_check(c, true);
     out->walk_flags = c->last_walk;
     out->walk_state = c->last_walk_state;
     out->walk_checks = c->walk_checks;
-    out->walk_fallbacks = c->walk_fallbacks;
+    if (c->traced && c->last_cert && c->d_qcount) {   // the last trace's re-trace counts (d_qcount 16..)
+        uint32_t q[32];
+        HIPC(c, hipMemcpy(q, c->d_qcount + 32 * c->last_slot, sizeof(q), hipMemcpyDeviceToHost));
+        out->redo_rays[0] = q[16];
+        for (uint32_t k = 0; k < c->bounces && k < 15; k++) out->redo_rays[1] += q[17 + k];
+    }
+    out->walk_fallbacks = out->redo_rays[0] + out->redo_rays[1];
     return RTBVH_OK;
 }
 

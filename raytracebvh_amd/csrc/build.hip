@@ -128,7 +128,7 @@ __device__ __forceinline__ uint32_t morton_code(const BuildArgs& a, uint32_t t, 
     const uint32_t i0 = a.idx[3 * (size_t)t], i1 = a.idx[3 * (size_t)t + 1], i2 = a.idx[3 * (size_t)t + 2];
     const float4 q0 = a.opos[i0], q1 = a.opos[i1], q2 = a.opos[i2];
     const f3 p0 = mk(q0.x, q0.y, q0.z), p1 = mk(q1.x, q1.y, q1.z), p2 = mk(q2.x, q2.y, q2.z);
-    const f3 c0 = xform_point(a.wvp.m, p0), c1 = xform_point(a.wvp.m, p1), c2 = xform_point(a.wvp.m, p2);
+    const f3 c0 = xform_point(a.cam, p0), c1 = xform_point(a.cam, p1), c2 = xform_point(a.cam, p2);
     uint32_t code;
     if (a.morton_mode == 0) {
         const f3 mn = mk(a.bounds[0], a.bounds[1], a.bounds[2]);
@@ -283,12 +283,6 @@ __device__ __forceinline__ void leaf_record_words(const BuildArgs& a, uint32_t i
     r[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
     r[2] = make_float4(e2.z, __uint_as_float(leaf_tri_word(t, lo, hi)), lo.x, lo.y);
     r[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
-}
-__device__ __forceinline__ void leaf_record(const BuildArgs& a, uint32_t i, f3& lo, f3& hi) {
-    float4 r[4];
-    leaf_record_words(a, i, lo, hi, r);
-    float4* dst = a.leaf + 4 * (size_t)i;
-    dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2]; dst[3] = r[3];
 }
 // 64-B records of consecutive indices, one per lane, written with every store instruction of
 // the wave covering 1 KB contiguously (16 B per lane): each half-wave's records are staged in
@@ -711,7 +705,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     __shared__ uint32_t s_pint[RBLOCK];
     __shared__ uint32_t s_xn;
     __shared__ uint32_t s_own[RTBVH_REFIT_STAGE_SLOTS / 32];   // phase 4: staged slots of this round
-    __shared__ float s_topo_z[2 * (RBLOCK / 64)];
+    __shared__ float s_topo_z[3 * (RBLOCK / 64)];
     const uint32_t T = a.T;
     const uint32_t base = blockIdx.x * RBLOCK, tid = threadIdx.x;
     const uint32_t i = base + tid;
@@ -724,11 +718,14 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     }
     f3 lo = mk(0.f, 0.f, 0.f), hi = lo;
     uint32_t e = INVALID;
+    float emax = 0.f;   // the leaf's edge bound (margin.h): the bounce walk's margin takes the largest
     {
         float4 r[4] = {};
         if (i < T) {
             leaf_record_words(a, i, lo, hi, r);
-            a.lfp[i] = leaf_footprint(lo, hi);
+            float zkey;
+            leaf_margin(r, lo.z, hi.z, emax, zkey);
+            a.lfp[i] = leaf_footprint(lo, hi, zkey);
         }
         const uint32_t w0 = base + (tid & ~63u);   // this wave's first leaf
         staged_records(a.leaf + 4 * (size_t)w0, T > w0 ? min(64u, T - w0) : 0u, r,
@@ -744,26 +741,31 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     }
     {   // the block's depth range (min lo.z, max hi.z of its leaves) for k_zrange: the binned primary
         // pass buckets by depth as soon as the leaves are written, before the climb above the blocks
-        float zl = i < T ? lo.z : INFINITY, zh = i < T ? hi.z : -INFINITY;
+        // (and the largest edge bound: an infinite one -- a non-finite triangle -- stays infinite)
+        float zl = i < T ? lo.z : INFINITY, zh = i < T ? hi.z : -INFINITY, em = emax;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             zl = fminf(zl, __shfl_xor(zl, off, 64));
             zh = fmaxf(zh, __shfl_xor(zh, off, 64));
+            em = fmaxf(em, __shfl_xor(em, off, 64));
         }
         if ((tid & 63u) == 0) {
-            s_topo_z[2 * (tid >> 6)] = zl;
-            s_topo_z[2 * (tid >> 6) + 1] = zh;
+            s_topo_z[3 * (tid >> 6)] = zl;
+            s_topo_z[3 * (tid >> 6) + 1] = zh;
+            s_topo_z[3 * (tid >> 6) + 2] = em;
         }
     }
     __syncthreads();
     if (tid == 0) {
-        float zl = INFINITY, zh = -INFINITY;
+        float zl = INFINITY, zh = -INFINITY, em = 0.f;
         for (uint32_t w = 0; w < RBLOCK / 64; w++) {
-            zl = fminf(zl, s_topo_z[2 * w]);
-            zh = fmaxf(zh, s_topo_z[2 * w + 1]);
+            zl = fminf(zl, s_topo_z[3 * w]);
+            zh = fmaxf(zh, s_topo_z[3 * w + 1]);
+            em = fmaxf(em, s_topo_z[3 * w + 2]);
         }
-        a.zpart[2 * blockIdx.x] = zl;
-        a.zpart[2 * blockIdx.x + 1] = zh;
+        a.zpart[ZPART * blockIdx.x] = zl;
+        a.zpart[ZPART * blockIdx.x + 1] = zh;
+        a.zpart[ZPART * blockIdx.x + 2] = em;
     }
     for (int level = 0; e != INVALID && level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
@@ -998,6 +1000,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
     __shared__ float s_box[SMALL_T][2][6];
     __shared__ uint32_t s_cnt[SMALL_T];
     __shared__ float s_red[16 * 6];
+    __shared__ uint32_t s_emax;             // the largest leaf edge bound (rootbox[8], margin.h)
     const uint32_t tid = threadIdx.x, T = a.T;
     for (uint32_t k = tid; k < SMALL_T; k += SMALL_BLOCK) s_cnt[k] = 0;
     if (a.morton_mode == 0) {   // k_bounds + k_bounds_final as one reduction
@@ -1055,14 +1058,23 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
     }
     __syncthreads();   // sorted ids (leaf_record) and clip triangles visible to the block
     const LdsCodes codes{s_kv};
+    if (tid == 0) s_emax = 0u;
+    __syncthreads();
     for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
         f3 lo, hi;
-        leaf_record(a, i, lo, hi);
-        a.lfp[i] = leaf_footprint(lo, hi);
+        float4 r[4];
+        leaf_record_words(a, i, lo, hi, r);
+        float4* dst = a.leaf + 4 * (size_t)i;
+        dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2]; dst[3] = r[3];
+        float em, zkey;
+        leaf_margin(r, lo.z, hi.z, em, zkey);
+        a.lfp[i] = leaf_footprint(lo, hi, zkey);
+        atomicMax(&s_emax, __float_as_uint(em));   // (non-negative floats order as their bits)
         if (i + 1 < T) karras_node<MODE>(codes, T, i, a.topo, a.pleaf, a.pint);
     }
     if (tid == 0 && T > 1) a.pint[0] = INVALID;
     __syncthreads();   // links written by other threads: copy them into LDS
+    if (tid == 0) a.rootbox[8] = __uint_as_float(s_emax);
     for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
         s_pleaf[i] = a.pleaf[i];
         if (i + 1 < T) {
@@ -1177,31 +1189,37 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_qnodes, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.rec, a.pint, a.qnode, a.T);
 }
 uint32_t refit_blocks(uint32_t T) { return (T + RBLOCK - 1) / RBLOCK; }
-// the leaves' depth range: rootbox[6..7] = min lo.z, max hi.z over k_refit's per-block ranges
+// the leaves' depth range: rootbox[6..7] = min lo.z, max hi.z over k_refit's per-block ranges, and
+// rootbox[8] = the largest leaf edge bound (the bounce walk's margin, margin.h)
 __global__ __launch_bounds__(1024) void k_zrange(const float* __restrict__ zpart, uint32_t nb, float* __restrict__ rootbox) {
-    __shared__ float s_z[2 * 16];
-    float zl = INFINITY, zh = -INFINITY;
+    __shared__ float s_z[3 * 16];
+    float zl = INFINITY, zh = -INFINITY, em = 0.f;
     for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
-        zl = fminf(zl, zpart[2 * b]);
-        zh = fmaxf(zh, zpart[2 * b + 1]);
+        zl = fminf(zl, zpart[ZPART * b]);
+        zh = fmaxf(zh, zpart[ZPART * b + 1]);
+        em = fmaxf(em, zpart[ZPART * b + 2]);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         zl = fminf(zl, __shfl_xor(zl, off, 64));
         zh = fmaxf(zh, __shfl_xor(zh, off, 64));
+        em = fmaxf(em, __shfl_xor(em, off, 64));
     }
     if ((threadIdx.x & 63u) == 0) {
-        s_z[2 * (threadIdx.x >> 6)] = zl;
-        s_z[2 * (threadIdx.x >> 6) + 1] = zh;
+        s_z[3 * (threadIdx.x >> 6)] = zl;
+        s_z[3 * (threadIdx.x >> 6) + 1] = zh;
+        s_z[3 * (threadIdx.x >> 6) + 2] = em;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (uint32_t w = 1; w < 16; w++) {
-            zl = fminf(zl, s_z[2 * w]);
-            zh = fmaxf(zh, s_z[2 * w + 1]);
+            zl = fminf(zl, s_z[3 * w]);
+            zh = fmaxf(zh, s_z[3 * w + 1]);
+            em = fmaxf(em, s_z[3 * w + 2]);
         }
         rootbox[6] = zl;
         rootbox[7] = zh;
+        rootbox[8] = em;
     }
 }
 void launch_refit_leaves(const BuildArgs& a, hipStream_t s) {

@@ -1,0 +1,70 @@
+// margin.h -- the rounding margin of Moller-Trumbore (rayTriangleCollision, RayTraceTraversal.hlsl:41-86)
+// that makes the certified walks exhaustive ("The per-ray certificate").  Shared by the
+// kernels (build.hip: the primary rays' depth keys; trace.hip: the bounce walk's expanded entries) and
+// the CPU checker tools/margin_check.cpp, so the checker tests these very functions.
+//
+// The bound.  Let the float test accept (o, d; p0, e1 = RN(p1 - p0), e2 = RN(p2 - p0)) with |det| >= 0.01
+// and return t.  Then the real point o + t d lies within
+//     rho(t) = 35.4 u L A E^2 (A t + 1.31 E) + u (4 A t + 6 E)           (u = 2^-24)
+// (2-norm) of the triangle conv(p0, p1, p2), hence of every box that contains the triangle, where
+// E >= max(|e1|, |e2|), A >= |d|, L >= 1 / |det|, provided (C): 28.3 L A u E (A t + 2 E) <= 0.2.
+// (Forward error analysis of each dot and cross product, gamma_n bounds, the computed u, v, t against
+// Cramer's rule on the same float inputs; DESIGN.md 3 has the steps.)  Everything below rounds that
+// bound UP: the 1.01 factor covers the roundings of computing and applying it.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define RTBVH_HD __host__ __device__
+#else
+#define RTBVH_HD
+#endif
+
+namespace rtbvh {
+
+constexpr float MT_U = 0x1p-24f;
+constexpr float MT_LAMBDA = 100.01f;        // >= 1 / |det| of any accepted test: |det| >= EPSILON = 0.01f
+constexpr float MT_A = 1.f + 0x1p-18f;      // >= |d| of a ray whose d.d <= MT_DD (bounce rays are normalized)
+constexpr float MT_DD = 1.f + 0x1p-18f;
+constexpr float MT_FLOOR = 1e-37f;          // absolute floor: the gradual-underflow terms of the products
+
+// rho(t) = r1 * t + r0, valid for t <= tcap (condition (C)); tcap < 0: no t is covered
+struct MtMargin {
+    float r1, r0, tcap;
+};
+RTBVH_HD inline MtMargin mt_margin(float E, float L, float A) {
+    MtMargin m;
+    const float K = 35.4f * MT_U * L * A * E * E;
+    m.r1 = 1.01f * A * (K + 4.f * MT_U);
+    m.r0 = 1.01f * E * (1.31f * K + 6.f * MT_U) + MT_FLOOR;
+    const float c = 28.3f * L * A * MT_U * E;   // (C): c (A t + 2 E) <= 0.2
+    m.tcap = c > 0.f ? (0.2f / c - 2.f * E) / A * 0.999f : INFINITY;
+    if (!(E >= 0.f && E < INFINITY && m.r1 < 0.5f && m.r0 < INFINITY)) m.tcap = -1.f;   // (NaN: not covered)
+    return m;
+}
+
+// the global edge bound of a triangle: max(|e1|, |e2|) rounded up (inf for a non-finite triangle)
+RTBVH_HD inline float mt_edge_bound(float e1x, float e1y, float e1z, float e2x, float e2y, float e2z) {
+    const float a = e1x * e1x + e1y * e1y + e1z * e1z, b = e2x * e2x + e2y * e2y + e2z * e2z;
+    const float m = sqrtf(fmaxf(a, b)) * (1.f + 0x1p-20f);
+    return m == m ? m : INFINITY;
+}
+
+// The depth key of a leaf for the orthographic primary rays (d = (0, 0, 1), so |d| = 1 and the
+// determinant of the test, `dx` as the kernels compute it for that d, is the same for every pixel):
+// every pixel ray whose test accepts this triangle returns t >= the key.  +inf when no primary ray
+// can be accepted (|dx| < 0.01, or NaN), -inf when no bound is available (the leaf is never pruned).
+RTBVH_HD inline float mt_primary_zkey(float dx, float E, float lo_z, float hi_z) {
+    if (!(fabsf(dx) >= 0.01f)) return INFINITY;
+    if (!(fabsf(lo_z) < INFINITY && fabsf(hi_z) < INFINITY && E < INFINITY)) return -INFINITY;
+    const float L = 1.f / fabsf(dx) * (1.f + 0x1p-20f);
+    const MtMargin m = mt_margin(E, L, 1.f);
+    // a candidate's t lies within rho(t) of [lo_z, hi_z] (its point is (o.x, o.y, t)): t <= th
+    const float th = (fmaxf(hi_z, 0.f) + m.r0) / (1.f - m.r1) * (1.f + 0x1p-20f);
+    if (!(th <= m.tcap)) return -INFINITY;
+    const float rho = (m.r1 * th + m.r0) * (1.f + 0x1p-20f);
+    return nextafterf(lo_z - rho, -INFINITY);   // below the rounded difference
+}
+
+}  // namespace rtbvh

@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "margin.h"
+
 namespace rtbvh {
 
 constexpr uint32_t LEAF_BIT = 0x80000000u;
@@ -135,9 +137,12 @@ __device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, 0.0f), 1.0
 // not depend on the frame size): the n with lo < n / 4 < hi on each axis -- exactly the rays the 4-wide
 // packet walk's axis-parallel test lets through (n / 4 is exact) -- or, for a box that needs the
 // general slab test (`general`), the closed superset lo <= n / 4 <= hi (every n when a corner is NaN).
-// Written by the build, one 16-B record per sorted leaf: {nx0 | nx1 << 16, ny0 | ny1 << 16, min.z, general},
+// Written by the build, one 16-B record per sorted leaf: {nx0 | nx1 << 16, ny0 | ny1 << 16, zkey, general},
 // offsets as int16 clamped to +-32767 (exact for frames of up to 32768 pixels a side: a clamped bound lies
-// outside every such frame).  Read by the binned primary pass (trace.hip k_pb_bin).
+// outside every such frame).  zkey <= min.z is the leaf's depth key (margin.h mt_primary_zkey): no pixel ray
+// whose triangle test accepts the leaf returns t < zkey, so a pixel whose bound is below zkey cannot take
+// the leaf -- even when the rounded t falls below min.z (containment failing).  Read by the
+// binned primary pass (trace.hip k_pb_bin).
 __device__ __forceinline__ void footprint_axis(float lo, float hi, bool general, int& a, int& b) {
     const float r = 4.f * lo, R = 4.f * hi;   // exact (powers of two); +-inf past the float range
     float fa, fb;
@@ -154,14 +159,23 @@ __device__ __forceinline__ void footprint_axis(float lo, float hi, bool general,
     a = (int)fminf(fmaxf(fa, -32767.f), 32767.f);
     b = (int)fminf(fmaxf(fb, -32767.f), 32767.f);
 }
-__device__ __forceinline__ uint4 leaf_footprint(f3 lo, f3 hi) {
+__device__ __forceinline__ uint4 leaf_footprint(f3 lo, f3 hi, float zkey) {
     // the general bit of build.hip leaf_tri_word
     const bool general = !(lo.x < hi.x && lo.y < hi.y && lo.z <= hi.z && 0.f <= hi.z && hi.z < INFINITY);
     int x0, x1, y0, y1;
     footprint_axis(lo.x, hi.x, general, x0, x1);
     footprint_axis(lo.y, hi.y, general, y0, y1);
     return make_uint4((uint32_t)(x0 & 0xFFFF) | (uint32_t)x1 << 16, (uint32_t)(y0 & 0xFFFF) | (uint32_t)y1 << 16,
-                      __float_as_uint(lo.z), general ? 1u : 0u);
+                      __float_as_uint(zkey), general ? 1u : 0u);
+}
+// A leaf's margin data from its record words r[0..2] = {v0, e1.x}, {e1.yz, e2.xy}, {e2.z, ...}: the edge
+// bound E (the bounce walk's global margin, margin.h) and the primary rays' depth key, from the
+// determinant the kernels compute for d = (0, 0, 1) (trace.hip ray_triangle_flat: dot(e1, cross(d, e2))).
+__device__ __forceinline__ void leaf_margin(const float4 (&r)[4], float lo_z, float hi_z, float& E, float& zkey) {
+    const f3 e1 = mk(r[0].w, r[1].x, r[1].y), e2 = mk(r[1].z, r[1].w, r[2].x);
+    const float dx = dot(e1, cross(mk(0.f, 0.f, 1.f), e2));
+    E = mt_edge_bound(e1.x, e1.y, e1.z, e2.x, e2.y, e2.z);
+    zkey = mt_primary_zkey(dx, E, lo_z, hi_z);
 }
 __device__ __forceinline__ float lerpf(float a, float b, float s) { return a + s * (b - a); }
 

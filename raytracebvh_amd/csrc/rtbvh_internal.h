@@ -15,8 +15,6 @@ namespace rtbvh {
 #endif
 constexpr uint32_t BOUNCE_WAVES = RTBVH_BOUNCE_WAVES;
 
-struct Mat4 { float m[16]; };
-
 // ---- radix sort (sort.hip) --------------------------------------------------
 constexpr uint32_t SORT_BLOCK = 256;
 #ifndef RTBVH_SORT_ITEMS
@@ -30,6 +28,8 @@ constexpr uint32_t SORT_TILE = SORT_BLOCK * SORT_ITEMS;   // 4096 keys per tile
 constexpr uint32_t RADIX_BITS = RTBVH_RADIX_BITS;   // digit width: 8 (4 passes of 30-bit codes) or 10 (3)
 constexpr uint32_t RADIX = 1u << RADIX_BITS;
 constexpr size_t BOUNDS_WORDS = 8 + 6 * 1024;
+constexpr uint32_t ROOTBOX_WORDS = 16;   // BuildArgs::rootbox
+constexpr uint32_t ZPART = 3;            // floats per refit workgroup in BuildArgs::zpart
 
 inline uint32_t sort_tiles(uint32_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
 // scratch words needed: RADIX * tiles (per-tile digit counts) + RADIX (digit totals)
@@ -50,7 +50,8 @@ struct BuildArgs {
     const uint32_t* matidx;   // [T] (into the clip triangle's fourth float4 for the shading)
     uint32_t V, T;
     int morton_mode, delta_mode;
-    Mat4 wvp;
+    const float* cam;         // [32] device: the camera of the frame, WVP then WV (row-major, row vectors;
+                              //   rtbvh_set_camera), read by the kernels -- a captured frame keeps it
     float smin[3], smax[3];   // HLSL-mode scene box
     float* bounds;            // CPUTests mode: [0..5] scene box (min xyz, max xyz), [8..] 1024 x 6 partials
     uint32_t* keys;           // [T] Morton codes (triangle order) -> sort input
@@ -67,10 +68,11 @@ struct BuildArgs {
     uint32_t* refit_cnt;      // [T-1]
     uint32_t* xlist;          // [T] k_refit workgroup b's crossing nodes at [b * RBLOCK, ...)
     uint32_t* xcnt;           // [T / RBLOCK + 1] their counts
-    float* rootbox;           // [8] the root box (min xyz, max xyz), then the leaves' depth range (k_zrange)
+    float* rootbox;           // [ROOTBOX_WORDS] the root box (min xyz, max xyz), the leaves' depth range and
+                              //   [8] the largest leaf edge bound (k_zrange; margin.h)
     QNode* qnode;             // [2T-1] quantized 4-wide nodes in slots (rtbvh_device.h), from rec
     uint4* lfp;               // [T] leaf footprints on the primary pixel grid (rtbvh_device.h leaf_footprint)
-    float* zpart;             // [2 * refit_blocks(T)] k_refit workgroup b's leaf depth range
+    float* zpart;             // [ZPART * refit_blocks(T)] k_refit workgroup b's leaf depth range, edge bound
     uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
@@ -122,7 +124,7 @@ struct TraceArgs {
     uint32_t pb_cap, pb_ntx;
     const float* rootbox;     // [6] the BVH root's box (min xyz, max xyz): the bins' depth buckets
     const uint4* lfp;         // [T] leaf footprints (BuildArgs::lfp)
-    Mat4 wv;
+    const float* cam;         // [32] device: WVP, WV (BuildArgs::cam); the shading reads WV
     float4* color;            // output pixels (compacted band rows when nranks > 1)
     float* intensity;         // optional, same indexing as color
     unsigned long long* counters;   // [64] per trace: see flush_counts (trace.hip) and rtbvh_get_stats
@@ -143,6 +145,14 @@ enum class PrimaryKind { LANE_REFERENCE, LANE_NEAREST, PACKET_REFERENCE, PACKET_
 enum class BounceWalk { REFERENCE, NEAREST, WIDE_QUANTIZED };
 void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, bool emit, PrimaryKind kind,
                     hipStream_t s);
+// A certified trace's re-trace list: the rays of one pass whose certificate failed, and their
+// count (zeroed before the pass); the pass's re-trace kernel (reference order) runs over them, REDO_BLOCKS
+// workgroups striding over the count on the device
+struct Redo {
+    uint32_t* list;
+    uint32_t* count;
+};
+constexpr uint32_t REDO_BLOCKS = 512;
 // binned primary rays (trace.hip k_primary_binned): the rank's frame in PB_TILE x PB_TILE screen
 // tiles (columns x compact band rows), every leaf listed in the tiles its box covers
 constexpr uint32_t PB_TILE = 32;
@@ -164,14 +174,16 @@ void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows
                            bool count, bool emit, bool zeroed, hipStream_t s);
 // ... in two parts: the binned pass (reads what launch_refit_leaves writes) and the packet walk of
 // the overflowed tiles (the whole BVH)
+// redo: a certified pass (the shading checks each hit's certificate; the flagged pixels are re-traced)
 void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
-                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail = nullptr);
+                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail = nullptr, const Redo* redo = nullptr);
 // the count pass of launch_pb_pass with the climb of the build's crossing nodes in the same launch,
 // then their QNodes (build.hip: the build's launch_refit_tail, moved into the frame)
 void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, uint32_t* cur, uint4* bins, uint32_t cap,
                          uint32_t ntx, uint32_t leaf_blocks, hipStream_t s);
+// reference: the overflowed tiles in the reference order (a certified trace), else nearest-first
 void launch_pb_gate(const TraceArgs& a, const PrimBins& pb, RayQ* q, uint32_t* qcount, bool count, bool emit,
-                    hipStream_t s);
+                    hipStream_t s, bool reference);
 // up to N arrays of 32-bit words zeroed by one launch (null / 0 words: unused)
 struct ZeroList {
     static constexpr int N = 4;
@@ -191,11 +203,15 @@ void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_coun
 constexpr uint32_t NEXT_SEGS = RTBVH_NEXT_SEGS;
 constexpr uint32_t NEXT_STRIDE = 32;                          // one 128-B line per counter
 constexpr uint32_t NEXT_WORDS = 16 * NEXT_SEGS * NEXT_STRIDE;  // per buffer set: bounce passes 0..15
+// cert: the certified 4-wide walk (WIDE_QUANTIZED, no stack limit, a clz64 tree), whose hit records flag
+// the rays it cannot vouch for; the shading with a Redo checks each hit's certificate and re-traces
+// the flagged rays in the reference order
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
-                            hipStream_t s);
+                            hipStream_t s, bool cert = false);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
-                         RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s);
+                         RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s,
+                         const Redo* redo = nullptr);
 // *diff += the number of the n float4 pixels of a and b whose bits differ
 void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long long* diff, hipStream_t s);
 void launch_count_diff32(const float* a, const float* b, size_t n, unsigned long long* diff, hipStream_t s);

@@ -317,7 +317,30 @@ rtbvh_status rtbvh_set_scene_obj(rtbvh_ctx* ctx, const rtbvh_scene* s, const rtb
 
 // Graphics.cpp:44-53: XMMatrixLookAtLH(eye, at, up) * XMMatrixPerspectiveFovLH(pi/4, H/W, .1, 1000)
 void rtbvh_camera_reference(uint32_t W, uint32_t H, float wvp[16], float wv[16]) {
-    const float eye[3] = {0.0f, 5.0f, -100.0f}, at[3] = {0, 0, 0}, up[3] = {0, 1.f, 0};
+    const float eye[3] = {0.0f, 5.0f, -100.0f};   // Graphics.h:200-205
+    rtbvh_camera_look(eye, W, H, wvp, wv);
+}
+
+// Graphics::onKeyDown (Graphics.cpp:937-960): eye = at + XMVector4Transform(eye - at, R), at = 0, with
+// R = XMMatrixRotationY(-+CAM_DELTA) (left / right) or XMMatrixRotationX(+-CAM_DELTA) (up / down), CAM_DELTA
+// = .1f (Graphics.h:14).  DirectXMath's rotations (row vectors, v' = v R): RotationY(a) = {c 0 -s; 0 1 0;
+// s 0 c}, RotationX(a) = {1 0 0; 0 c s; 0 -s c}.
+void rtbvh_camera_orbit(float eye[3], uint32_t key) {
+    if (key > 3) return;
+    const float a = key == 0 || key == 3 ? -0.1f : 0.1f;
+    const float s = sinf(a), c = cosf(a);
+    const float x = eye[0], y = eye[1], z = eye[2];
+    if (key < 2) {   // about y
+        eye[0] = x * c + z * s;
+        eye[2] = x * -s + z * c;
+    } else {         // about x
+        eye[1] = y * c + z * -s;
+        eye[2] = y * s + z * c;
+    }
+}
+
+void rtbvh_camera_look(const float eye_in[3], uint32_t W, uint32_t H, float wvp[16], float wv[16]) {
+    const float eye[3] = {eye_in[0], eye_in[1], eye_in[2]}, at[3] = {0, 0, 0}, up[3] = {0, 1.f, 0};
     auto dot3 = [](const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
     auto cross3 = [](const float* a, const float* b, float* r) {
         r[0] = a[1] * b[2] - a[2] * b[1];

@@ -310,6 +310,10 @@ __device__ __forceinline__ float ray_triangle_flat(f3 o, f3 d, f3 p0, f3 e1, f3 
 // not <= +inf (NaN) fails the slab test's own mn <= mx too, as the reference's !hit || ... does.
 constexpr uint64_t NO_HIT = 0x7F800000FFFFFFFFull;
 __device__ __forceinline__ float key_t(uint64_t key) { return __uint_as_float((uint32_t)(key >> 32)); }
+// a bounce hit record's word (the triangle, INVALID for a miss) with bit 30 flipped: the certified walk
+// could not vouch for the ray (k_bounce_trav CERT); the shading hands it to the reference-order re-trace
+constexpr uint32_t HIT_FLAG = 0x40000000u;
+__device__ __forceinline__ bool hit_flagged(uint32_t w) { return ((w >> 31) ^ (w >> 30)) & 1u; }
 
 // v_writelane_b32: lane K of v := the wave-uniform s (a VALU op, no scalar work)
 template <int K> __device__ __forceinline__ void writelane(uint32_t& v, uint32_t s) {
@@ -596,7 +600,7 @@ __device__ __forceinline__ HitInfo shade_hit_tri(const TraceArgs& a, uint32_t tr
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const float* v = a.verts + 8 * (size_t)vi[k];
-        n[k] = xform_normal(a.wv.m, mk(v[3], v[4], v[5]));
+        n[k] = xform_normal(a.cam + 16, mk(v[3], v[4], v[5]));
         uv[k][0] = v[6];
         uv[k][1] = v[7];
     }
@@ -1065,11 +1069,17 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs
 #define RTBVH_PB_SHADE_BLOCK 1024
 #endif
 constexpr uint32_t PB_SHADE_BLOCK = RTBVH_PB_SHADE_BLOCK;
-template <bool COUNT>
+// CERT (the certified pass): the binned pass tested every leaf whose triangle could be
+// accepted below a pixel's bound (its depth key, margin.h); a pixel's (t, leaf) is the reference's when
+// the leaf's own box passes the reference slab test with the bound t (k_bounce_shade's leaf_certified,
+// here from the leaf record's box).  Pixels that fail it go to the re-trace list (redo: compact pixel
+// index) and are left to k_primary_redo, outside the block's bounce-queue claim.
+template <bool COUNT, bool CERT>
 __global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, const uint32_t* __restrict__ off, uint32_t cap,
                                                     uint32_t ntx, uint32_t rows,
                                                     const unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
-                                                    uint32_t* __restrict__ qcount, int emit) {
+                                                    uint32_t* __restrict__ qcount, int emit,
+                                                    uint32_t* __restrict__ redo, uint32_t* __restrict__ redo_count) {
     __shared__ uint32_t s_cnt[(PB_TILE / 8) * (PB_TILE / 8)];
     __shared__ uint32_t s_base;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -1080,7 +1090,8 @@ __global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, con
     uint32_t x[NST], crow[NST];
     uint64_t key[NST];
     bool valid[NST];
-    uint64_t livem[NST];
+    uint64_t livem[NST], flagm[NST];
+    const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++) {
         const uint32_t st = w + i * (PB_SHADE_BLOCK / 64);
@@ -1092,8 +1103,17 @@ __global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, con
     // the live reflection rays: hit, and the hit material's shininess > 0
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++) {
-        bool live = false;
-        if (emit && key[i] != NO_HIT) {
+        bool live = false, flag = false;
+        if (CERT && key[i] != NO_HIT) {   // the certificate: the leaf's box, the reference slab test at t
+            const float4 b2 = a.leaf[4 * (size_t)(uint32_t)key[i] + 2], b3 = a.leaf[4 * (size_t)(uint32_t)key[i] + 3];
+            const f3 o = mk(((float)x[i] - hw) / 4.f, ((float)pb_image_row(a, crow[i]) - hh) / 4.f, 0.f);
+            const f3 d = mk(0.f, 0.f, 1.f);
+            float tm;
+            flag = !ray_box(o, mk(1.f / d.x, 1.f / d.y, 1.f / d.z), b2.z, b2.w, b3.x, b3.y, b3.z, b3.w, true,
+                            key_t(key[i]), tm);
+        }
+        flagm[i] = CERT ? __ballot(flag) : 0ull;
+        if (emit && key[i] != NO_HIT && !flag) {
             const uint32_t tri = __float_as_uint(a.leaf[4 * (size_t)(uint32_t)key[i] + 2].y) & ~LEAF_BIT;
             const uint32_t mi = TCS == 4 ? __float_as_uint(a.tclip[TCS * (size_t)tri + 3].w) : a.matidx[tri];
             live = 0 < a.mats[mi].shininess / 1000.f * 1;
@@ -1112,11 +1132,15 @@ __global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, con
         s_base = run && emit ? atomicAdd(qcount, run) : 0u;
     }
     __syncthreads();
-    const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
     uint32_t hits = 0, tex = 0;
 #pragma unroll
     for (uint32_t i = 0; i < NST; i++) {
-        if (valid[i]) {
+        const bool flag = CERT && ((flagm[i] >> lane) & 1u);
+        if (CERT && flagm[i]) {   // (rare) the re-trace list, one atomic per wave
+            const uint32_t slot = wave_append(flag, redo_count);
+            if (flag) redo[slot] = crow[i] * a.W + x[i];
+        }
+        if (valid[i] && !flag) {
             const f3 o = mk(((float)x[i] - hw) / 4.f, ((float)pb_image_row(a, crow[i]) - hh) / 4.f, 0.f);
             const bool phit = key[i] != NO_HIT;
             uint32_t h1 = 0, t1 = 0;
@@ -1133,6 +1157,39 @@ __global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, con
         Counts c = {0, 0, 0, 0, 0};
         flush_counts<COUNT>(a, c, hits, tex, 2);
     }
+}
+
+// The reference-order re-trace of the pixels a certified primary pass flagged (redo: compact pixel
+// indices crow * W + x): the exact findCollision DFS per pixel (traverse), then k_primary's outputs
+// (primary_pixel) and the bounce queue.  A fixed grid over the count on the device.
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_primary_redo(TraceArgs a, const uint32_t* __restrict__ redo,
+                                                        const uint32_t* __restrict__ redo_count, RayQ* __restrict__ q,
+                                                        uint32_t* __restrict__ qcount, int emit) {
+    const uint32_t n = *redo_count;
+    Counts c = {0, 0, 0, 0, 0};
+    uint32_t hits = 0, tex = 0;
+    const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
+    const f3 d = mk(0.f, 0.f, 1.f);
+    const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    for (uint32_t base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        bool live = false;
+        RayQ e;
+        if (i < n) {
+            const uint32_t p = redo[i], crow = p / a.W, x = p % a.W;
+            const f3 o = mk(((float)x - hw) / 4.f, ((float)pb_image_row(a, crow) - hh) / 4.f, 0.f);
+            float best;
+            uint32_t bl, h1 = 0, t1 = 0;
+            const bool h = traverse<COUNT, false>(a.inner, a.leaf, a.T, o, d, inv, STACK_SIZE, best, bl, c);
+            live = primary_pixel(a, p, o, d, h, best, bl, h1, t1, e);
+            hits += h1;
+            tex += t1;
+        }
+        const uint32_t slot = wave_append(emit && live, qcount);
+        if (emit && live) q[slot] = e;
+    }
+    flush_counts<COUNT>(a, c, hits, tex, 2);
 }
 
 // RayTraceReflection.hlsl:6-62 over the compacted queue of live rays (in `perm`
@@ -1276,7 +1333,11 @@ __device__ __forceinline__ bool qnode_fast_ray(f3 o, f3 inv) {
     return mi <= 0x1p20f && mo <= 0x1p90f;   // NaN: false
 }
 struct QAxis { uint32_t nw, fw; float b, an, af; };
-__device__ __forceinline__ QAxis qaxis(float org, float scl, uint32_t lw, uint32_t hw, float o, float inv) {
+// CERT (the certified walk): the near side is widened by the margin rr as well, in
+// position (rr * |inv| in distance): the entry of the box grown by rr on every side (margin.h).
+template <bool CERT = false>
+__device__ __forceinline__ QAxis qaxis(float org, float scl, uint32_t lw, uint32_t hw, float o, float inv,
+                                       float rr = 0.f) {
     QAxis r;
     const bool neg = inv < 0.f;
     r.nw = neg ? hw : lw;
@@ -1284,7 +1345,8 @@ __device__ __forceinline__ QAxis qaxis(float org, float scl, uint32_t lw, uint32
     const float m = fmaf(scl, 256.f, fabsf(org) + fabsf(o));
     const float e = m * fabsf(inv);
     const float a = (org - o) * inv;
-    r.an = fmaf(e, -0x1p-20f, a);
+    if (CERT) r.an = fmaf(-fmaf(m, 0x1p-20f, rr), fabsf(inv), a);
+    else r.an = fmaf(e, -0x1p-20f, a);
     r.af = fmaf(e, 0x1p-20f, a);
     r.b = scl * inv;
     return r;
@@ -1300,8 +1362,14 @@ __device__ __forceinline__ bool qbox_fast(const QAxis& x, const QAxis& y, const 
     return 0 <= mx && mn <= mx && (!hit || mn <= best);
 }
 
-// GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it)
-template <bool COUNT, int MODE, bool LIM, bool GUARD>
+// GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it).
+// CERT (MODE 2 only): the certified walk.  Every box test's entry distance is taken on the
+// box grown by the margin rho(best) (margin.h: no hit the triangle test accepts at t <= best lies outside
+// that box), so the walk sees EVERY leaf whose triangle could be accepted at t <= best: its (t, leaf)
+// minimum is the minimum over all triangles the reference could test.  A ray the bound does not cover --
+// a slack-test-free ray (qnode_fast_ray), |d| off unit, a node without a grid, a stack overflow -- is
+// flagged in its hit record (HIT_FLAG) for the reference-order re-trace (k_bounce_redo).
+template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
@@ -1310,8 +1378,10 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          unsigned long long* __restrict__ overflow, int stack_limit) {
+                                                          unsigned long long* __restrict__ overflow, int stack_limit,
+                                                          const float* __restrict__ rootbox) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
+    static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
     const uint32_t n = *qin_count;
     if (n == 0) return;
@@ -1324,6 +1394,12 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     int sp = 0;
     float best = 0.f;
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
+    // CERT: the margin of the scene's edge bound (rootbox[8]); per ray the pruning bound kb (best, or +inf
+    // past the margin's range mg.tcap: no pruning) and the margin rr = rho(best), and the flag
+    MtMargin mg{0.f, 0.f, -1.f};
+    if (CERT) mg = mt_margin(rootbox[8], MT_LAMBDA, MT_A);
+    float kb = __builtin_inff(), rr = 0.f;
+    bool flg = false;
     __shared__ uint32_t s_stk[WIDE ? 1 : SB][WIDE ? 1 : BLOCK];   // (none for WIDE: its LDS is the 6-B stack)
     uint32_t stack[WIDE ? 1 : STACK_SIZE - SB];   // entries [SB, STACK_SIZE)
     __shared__ uint32_t s_wid[WIDE ? SW : 1][BLOCK];
@@ -1355,7 +1431,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
         uint4 a3, b3;
         float t0, t1, t2, t3;
         bool h0, h1, h2, h3;
-        const float kb = key_t(key);
+        const float kbb = CERT ? kb : key_t(key);
         if (q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
             const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w, sy = q1.x, sz = q1.y;
             const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
@@ -1363,16 +1439,17 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
             a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
             b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
             if (qfast) {
-                const QAxis X = qaxis(ox, sx, lx, hx, o.x, inv.x), Y = qaxis(oy, sy, ly, hy, o.y, inv.y),
-                            Z = qaxis(oz, sz, lz, hz, o.z, inv.z);
-                h0 = qbox_fast(X, Y, Z, 0, true, kb, t0);
-                h1 = qbox_fast(X, Y, Z, 1, true, kb, t1);
-                h2 = qbox_fast(X, Y, Z, 2, true, kb, t2);
-                h3 = qbox_fast(X, Y, Z, 3, true, kb, t3);
+                const QAxis X = qaxis<CERT>(ox, sx, lx, hx, o.x, inv.x, rr),
+                            Y = qaxis<CERT>(oy, sy, ly, hy, o.y, inv.y, rr),
+                            Z = qaxis<CERT>(oz, sz, lz, hz, o.z, inv.z, rr);
+                h0 = qbox_fast(X, Y, Z, 0, true, kbb, t0);
+                h1 = qbox_fast(X, Y, Z, 1, true, kbb, t1);
+                h2 = qbox_fast(X, Y, Z, 2, true, kbb, t2);
+                h3 = qbox_fast(X, Y, Z, 3, true, kbb, t3);
             } else {
     #define RTBVH_QBOX(c, t)                                                                                      \
 ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
-        qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), true, kb, t)
+        qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), true, kbb, t)
                 h0 = RTBVH_QBOX(0, t0);
                 h1 = RTBVH_QBOX(1, t1);
                 h2 = RTBVH_QBOX(2, t2);
@@ -1384,7 +1461,9 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
         } else {
             // a node without a finite grid: its exact record pair (node = its slot; the
             // pair of its children's records is at 2 * own, own = word 14 of its record; the
-            // build writes the pseudo-records of such a node's leaf children whatever the flags)
+            // build writes the pseudo-records of such a node's leaf children whatever the flags).
+            // Not widened by the margin: a certified walk flags the ray
+            if (CERT) flg = true;
             const uint32_t own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
             const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
             q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
@@ -1397,10 +1476,10 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             if (a3.y != INVALID && !(a3.y & LEAF_BIT)) a3.y = 2 * ol + 1;
             if (!(b3.x & LEAF_BIT)) b3.x = 2 * orr;
             if (b3.y != INVALID && !(b3.y & LEAF_BIT)) b3.y = 2 * orr + 1;
-            h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, true, kb, t0);
-            h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, true, kb, t1) & (a3.y != INVALID);
-            h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, true, kb, t2);
-            h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, true, kb, t3) & (b3.y != INVALID);
+            h0 = ray_box_xy(o, inv, q0.xy, q0.zw, q2.x, q2.y, true, kbb, t0);
+            h1 = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, true, kbb, t1) & (a3.y != INVALID);
+            h2 = ray_box_xy(o, inv, q4.xy, q4.zw, q6.x, q6.y, true, kbb, t2);
+            h3 = ray_box_xy(o, inv, q5.xy, q5.zw, q6.z, q6.w, true, kbb, t3) & (b3.y != INVALID);
         }
         const float INF = __builtin_inff();
         k0 = h0 ? t0 : INF; k1 = h1 ? t1 : INF; k2 = h2 ? t2 : INF; k3 = h3 ? t3 : INF;
@@ -1446,6 +1525,12 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     top = INVALID;
                     node = root_slot(T);
                     guard = 2 * T + 2;
+                    if (CERT) {   // a ray the margin does not cover ends at its first step, flagged
+                        kb = __builtin_inff();
+                        rr = 0.f;
+                        flg = !(qfast && dot(d, d) <= MT_DD && mg.tcap > EPSILON);
+                        if (flg) node = INVALID;
+                    }
                 }
             }
         }
@@ -1469,6 +1554,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             if (GUARD && --guard == 0) {
                 c.overflow++;
                 done = true;
+                if (CERT) flg = true;
             } else {
                 if (node & LEAF_BIT) {
                     L = node;
@@ -1487,6 +1573,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     if (sp + 3 > limit) {
                         c.overflow++;
                         done = true;
+                        if (CERT) flg = true;
                     } else {   // push the others farthest first
                         if (i3 != INVALID) wpush(i3, k3);
                         if (i2 != INVALID) wpush(i2, k2);
@@ -1504,6 +1591,12 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
                     btri = k < key ? __float_as_uint(lc.y) & ~LEAF_BIT : btri;
                     key = k < key ? k : key;
+                    if (CERT) {   // the pruning bound and the margin of the new best
+                        const float tk = key_t(key);
+                        const bool cov = tk <= mg.tcap;
+                        kb = cov ? tk : __builtin_inff();
+                        rr = cov ? fmaf(mg.r1, tk, mg.r0) : 0.f;
+                    }
                 }
                 if (!done && node == INVALID) {   // pop, dropping entries that cannot improve
                     while (sp > 0) {
@@ -1511,7 +1604,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                         uint2 e;
                         if (sp < SW) e = make_uint2(s_wid[sp][tid], __float_as_uint(bf16_up(s_wt[sp][tid])));
                         else e = wstack[sp - SW];
-                        if (__uint_as_float(e.y) <= key_t(key)) {
+                        if (__uint_as_float(e.y) <= (CERT ? kb : key_t(key))) {
                             node = e.x;
                             break;
                         }
@@ -1576,7 +1669,11 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
         }
         if (done) {
             // (t, triangle) of the hit, INVALID for a miss: the shading reads no leaf record
-            if (WIDE) hitrec[r] = make_float2(key_t(key), __uint_as_float(key != NO_HIT ? btri : INVALID));
+            if (WIDE) {
+                uint32_t w = key != NO_HIT ? btri : INVALID;
+                if (CERT && flg) w ^= HIT_FLAG;   // (a hit: bit 30 set; a miss: bit 30 cleared)
+                hitrec[r] = make_float2(key_t(key), __uint_as_float(w));
+            }
             else hitrec[r] = make_float2(best, __uint_as_float(hit ? btri : INVALID));
             has = false;
             if (COUNT && GUARD) {   // walk length census (stats trav_max_steps / trav_steps_log2)
@@ -1608,51 +1705,89 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
     }
 }
 
-// RayTraceReflection.hlsl:19-60 for every queued ray, from its hit record
-template <bool COUNT>
+// RayTraceReflection.hlsl:19-60 for one queued ray e from its closest hit (tri at t; tri INVALID: a
+// miss): colour, intensity, the reflectRay record, and the next ray in e (returns whether it is live)
+__device__ __forceinline__ bool bounce_apply(const TraceArgs& a, RayQ& e, uint32_t tri, float t, uint32_t& hits,
+                                             uint32_t& tex) {
+    const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
+    float4 col = a.color[e.idx];
+    float intensity = e.intensity;
+    bool live = false;
+    if (tri != INVALID) {
+        hits = 1;
+        const HitInfo h = shade_hit_tri(a, tri, o, d, t);
+        tex = h.textured;
+        col = make_float4(lerpf(col.x, h.color.x, intensity), lerpf(col.y, h.color.y, intensity),
+                          lerpf(col.z, h.color.z, intensity), lerpf(col.w, h.color.w, intensity));
+        intensity *= h.shininess / 1000.f * 1;
+        const f3 ro = add(h.hitp, mul(h.nrm, .0001f));   // RAY_OFFSET .0001
+        const f3 rd = normalize(reflect(d, h.nrm));
+        e.intensity = intensity;
+        e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
+        e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
+        live = 0 < intensity;
+        if (a.refl_rec) put_record(a.refl_rec, e.idx, intensity, true, ro, rd, col);   // :42-46
+    } else {
+        col = make_float4(lerpf(col.x, .5f, intensity), lerpf(col.y, .5f, intensity),
+                          lerpf(col.z, .5f, intensity), lerpf(col.w, 1.f, intensity));
+        intensity = 0.f;
+        if (a.refl_rec) {   // :50-55: the ray stays, intensity 0, colour blended
+            float* r = a.refl_rec + 14 * (size_t)e.idx;
+            r[0] = 0.f;
+            r[10] = col.x; r[11] = col.y; r[12] = col.z; r[13] = col.w;
+        }
+    }
+    a.color[e.idx] = col;
+    if (a.intensity) a.intensity[e.idx] = intensity;
+    return live;
+}
+
+// The certificate of a certified walk's hit: the reference's findCollision
+// (RayTraceTraversal.hlsl:106-193) reaches leaf x -- and, the walk having seen every triangle that could
+// be accepted at t <= its best, returns x -- when x's own box passes the reference slab test with the
+// bound t (every box above contains it: the slab test is monotone in the box, so they pass too, at every
+// bound the reference holds, all >= t).  The box is the leaf's: min / max of its clip-space vertices
+// (build.hip leaf_record_words, MortonCodes.hlsl:87-96), from the triangle's record.
+__device__ __forceinline__ bool leaf_certified(const TraceArgs& a, uint32_t tri, f3 o, f3 inv, float t) {
+    const float4* P = a.tclip + TCS * (size_t)tri;
+    const float4 a0 = P[0], a1 = P[1], a2 = P[2];
+    const f3 v0 = mk(a0.x, a0.y, a0.z), v1 = mk(a1.x, a1.y, a1.z), v2 = mk(a2.x, a2.y, a2.z);
+    const f3 lo = vmin(vmin(v0, v1), v2), hi = vmax(vmax(v0, v1), v2);
+    float tm;
+    return ray_box(o, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, true, t, tm);
+}
+
+// RayTraceReflection.hlsl:19-60 for every queued ray, from its hit record.  CERT: a ray whose walk
+// flagged it or whose hit fails the certificate goes to the re-trace list (redo) instead
+template <bool COUNT, bool CERT>
 __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ* __restrict__ qin,
                                                         const uint32_t* __restrict__ qin_count,
                                                         const float2* __restrict__ hitrec, RayQ* __restrict__ qout,
-                                                        uint32_t* __restrict__ qout_count, int emit) {
+                                                        uint32_t* __restrict__ qout_count, int emit,
+                                                        uint32_t* __restrict__ redo, uint32_t* __restrict__ redo_count) {
     const uint32_t n = *qin_count;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (blockIdx.x * BLOCK >= n) return;   // whole block past the queue (wave_append below needs all lanes)
-    bool live = false;
+    bool live = false, flagged = false;
     uint32_t hits = 0, tex = 0;
     RayQ e;
     if (i < n) {
         e = qin[i];
         const float2 h2 = hitrec[i];
-        const uint32_t tri = __float_as_uint(h2.y);
-        const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
-        float4 col = a.color[e.idx];
-        float intensity = e.intensity;
-        if (tri != INVALID) {
-            hits = 1;
-            const HitInfo h = shade_hit_tri(a, tri, o, d, h2.x);
-            tex = h.textured;
-            col = make_float4(lerpf(col.x, h.color.x, intensity), lerpf(col.y, h.color.y, intensity),
-                              lerpf(col.z, h.color.z, intensity), lerpf(col.w, h.color.w, intensity));
-            intensity *= h.shininess / 1000.f * 1;
-            const f3 ro = add(h.hitp, mul(h.nrm, .0001f));   // RAY_OFFSET .0001
-            const f3 rd = normalize(reflect(d, h.nrm));
-            e.intensity = intensity;
-            e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
-            e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
-            live = 0 < intensity;
-            if (a.refl_rec) put_record(a.refl_rec, e.idx, intensity, true, ro, rd, col);   // :42-46
-        } else {
-            col = make_float4(lerpf(col.x, .5f, intensity), lerpf(col.y, .5f, intensity),
-                              lerpf(col.z, .5f, intensity), lerpf(col.w, 1.f, intensity));
-            intensity = 0.f;
-            if (a.refl_rec) {   // :50-55: the ray stays, intensity 0, colour blended
-                float* r = a.refl_rec + 14 * (size_t)e.idx;
-                r[0] = 0.f;
-                r[10] = col.x; r[11] = col.y; r[12] = col.z; r[13] = col.w;
+        uint32_t tri = __float_as_uint(h2.y);
+        if (CERT) {
+            flagged = hit_flagged(tri);
+            tri = (tri & LEAF_BIT) ? INVALID : tri & ~HIT_FLAG;
+            if (!flagged && tri != INVALID) {
+                const f3 d = mk(e.dx, e.dy, e.dz);
+                flagged = !leaf_certified(a, tri, mk(e.ox, e.oy, e.oz), mk(1.f / d.x, 1.f / d.y, 1.f / d.z), h2.x);
             }
         }
-        a.color[e.idx] = col;
-        if (a.intensity) a.intensity[e.idx] = intensity;
+        if (!flagged) live = bounce_apply(a, e, tri, h2.x, hits, tex);
+    }
+    if (CERT) {
+        const uint32_t slot = wave_append(flagged, redo_count);
+        if (flagged) redo[slot] = i;
     }
     const uint32_t slot = wave_append(emit && live, qout_count);
     if (emit && live) qout[slot] = e;
@@ -1660,6 +1795,41 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
         Counts c = {0, 0, 0, 0, 0};
         flush_counts<COUNT>(a, c, hits, tex, 5);
     }
+}
+
+// The reference-order re-trace of the rays a certified bounce pass flagged (redo: queue indices): the
+// exact findCollision DFS (traverse, reference order), then the shading as k_bounce_shade.  A fixed grid
+// over the count on the device (a captured frame replays it as it is).
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_bounce_redo(TraceArgs a, const RayQ* __restrict__ qin,
+                                                       const uint32_t* __restrict__ redo,
+                                                       const uint32_t* __restrict__ redo_count,
+                                                       RayQ* __restrict__ qout, uint32_t* __restrict__ qout_count,
+                                                       int emit) {
+    const uint32_t n = *redo_count;
+    Counts c = {0, 0, 0, 0, 0};
+    uint32_t hits = 0, tex = 0;
+    for (uint32_t base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        bool live = false;
+        RayQ e;
+        if (i < n) {
+            e = qin[redo[i]];
+            const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
+            const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+            float best;
+            uint32_t bl;
+            const bool h = traverse<COUNT, false>(a.inner, a.leaf, a.T, o, d, inv, STACK_SIZE, best, bl, c);
+            const uint32_t tri = h ? __float_as_uint(a.leaf[4 * (size_t)bl + 2].y) & ~LEAF_BIT : INVALID;
+            uint32_t h1 = 0, t1 = 0;
+            live = bounce_apply(a, e, tri, best, h1, t1);
+            hits += h1;
+            tex += t1;
+        }
+        const uint32_t slot = wave_append(emit && live, qout_count);
+        if (emit && live) qout[slot] = e;
+    }
+    flush_counts<COUNT>(a, c, hits, tex, 5);
 }
 
 // bounce-ray coherence sort key (results do not depend on the order): direction
@@ -1758,15 +1928,18 @@ void launch_primary_c(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count,
 
 template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                          float2* hitrec, uint32_t* next, uint32_t blocks, hipStream_t s) {
+                          float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, hipStream_t s) {
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
-#define RTBVH_BT(L, G)                                                                                              \
-    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
-                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)
+#define RTBVH_BT(L, G, C)                                                                                              \
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, a.rootbox)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
-    if (a.limited) { if (guard) RTBVH_BT(true, true); else RTBVH_BT(true, false); }
-    else { if (guard) RTBVH_BT(false, true); else RTBVH_BT(false, false); }
+    if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
+        if (guard) RTBVH_BT(false, true, MODE == 2);
+        else RTBVH_BT(false, false, MODE == 2);
+    } else if (a.limited) { if (guard) RTBVH_BT(true, true, false); else RTBVH_BT(true, false, false); }
+    else { if (guard) RTBVH_BT(false, true, false); else RTBVH_BT(false, false, false); }
 #undef RTBVH_BT
 }
 
@@ -1800,7 +1973,7 @@ void launch_zero(const ZeroList& z, hipStream_t s) {
 }
 
 void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
-                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail) {
+                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail, const Redo* redo) {
     if (rows == 0 || a.W == 0 || a.T == 0) return;
     const uint32_t keys = pb.ntx * pb.nty * PB_NZ;
     if (!zeroed) (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
@@ -1818,31 +1991,39 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
     else
         hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
                            pb.keys);
-    if (count)
-        hipLaunchKernelGGL((k_pb_shade<true>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
-                           qcount, (int)emit);
-    else
-        hipLaunchKernelGGL((k_pb_shade<false>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q,
-                           qcount, (int)emit);
+    uint32_t* rl = redo ? redo->list : nullptr;
+    uint32_t* rc = redo ? redo->count : nullptr;
+#define RTBVH_PBS(C, R)                                                                                              \
+    hipLaunchKernelGGL((k_pb_shade<C, R>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q, \
+                       qcount, (int)emit, rl, rc)
+    if (count) { if (redo) RTBVH_PBS(true, true); else RTBVH_PBS(true, false); }
+    else { if (redo) RTBVH_PBS(false, true); else RTBVH_PBS(false, false); }
+#undef RTBVH_PBS
+    if (redo) {   // the flagged pixels, in the reference order
+        const dim3 rg(REDO_BLOCKS);
+        if (count) hipLaunchKernelGGL((k_primary_redo<true>), rg, dim3(BLOCK), 0, s, a, rl, rc, q, qcount, (int)emit);
+        else hipLaunchKernelGGL((k_primary_redo<false>), rg, dim3(BLOCK), 0, s, a, rl, rc, q, qcount, (int)emit);
+    }
 }
 
 void launch_pb_gate(const TraceArgs& a, const PrimBins& pb, RayQ* q, uint32_t* qcount, bool count, bool emit,
-                    hipStream_t s) {
+                    hipStream_t s, bool reference) {
     if (a.W == 0 || a.T == 0) return;
     // the tiles whose bins overflowed: the per-lane nearest-first walk (every other block returns at
-    // once); a binary walk, which reads no leaf pseudo-records (a binned build writes none)
+    // once); a binary walk, which reads no leaf pseudo-records (a binned build writes none).  A certified
+    // trace takes the reference order there (exact by construction)
     TraceArgs g = a;
     g.pb_gate = pb.off;
     g.pb_cap = pb.cap;
     g.pb_ntx = pb.ntx;
-    launch_primary(g, q, qcount, count, emit, PrimaryKind::LANE_NEAREST, s);
+    launch_primary(g, q, qcount, count, emit, reference ? PrimaryKind::LANE_REFERENCE : PrimaryKind::LANE_NEAREST, s);
 }
 
 void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount,
                            bool count, bool emit, bool zeroed, hipStream_t s) {
     if (rows == 0) return;
     launch_pb_pass(a, pb, rows, q, qcount, count, emit, zeroed, s);
-    launch_pb_gate(a, pb, q, qcount, count, emit, s);
+    launch_pb_gate(a, pb, q, qcount, count, emit, s, false);
 }
 
 void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm, RayQ* qout,
@@ -1869,9 +2050,9 @@ void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, 
 
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
-                            hipStream_t s) {
+                            hipStream_t s, bool cert) {
     if (blocks == 0) blocks = 2048;
-#define RTBVH_TRAV(C, M) launch_bounce_trav_t<C, M>(a, qin, qin_count, perm, hitrec, next, blocks, s)
+#define RTBVH_TRAV(C, M) launch_bounce_trav_t<C, M>(a, qin, qin_count, perm, hitrec, next, blocks, cert, s)
     switch (walk) {
         case BounceWalk::NEAREST: if (count) RTBVH_TRAV(true, 1); else RTBVH_TRAV(false, 1); break;
         case BounceWalk::WIDE_QUANTIZED: if (count) RTBVH_TRAV(true, 2); else RTBVH_TRAV(false, 2); break;
@@ -1881,14 +2062,24 @@ void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t*
 }
 
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
-                         RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s) {
+                         RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s,
+                         const Redo* redo) {
     if (P == 0) return;
-    if (count)
-        hipLaunchKernelGGL((k_bounce_shade<true>), dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a, qin, qin_count,
-                           hitrec, qout, qout_count, (int)emit);
-    else
-        hipLaunchKernelGGL((k_bounce_shade<false>), dim3((P + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a, qin,
-                           qin_count, hitrec, qout, qout_count, (int)emit);
+    uint32_t* rl = redo ? redo->list : nullptr;
+    uint32_t* rc = redo ? redo->count : nullptr;
+    const dim3 g((P + BLOCK - 1) / BLOCK);
+#define RTBVH_BS(C, R)                                                                                             \
+    hipLaunchKernelGGL((k_bounce_shade<C, R>), g, dim3(BLOCK), 0, s, a, qin, qin_count, hitrec, qout, qout_count, \
+                       (int)emit, rl, rc)
+    if (count) { if (redo) RTBVH_BS(true, true); else RTBVH_BS(true, false); }
+    else { if (redo) RTBVH_BS(false, true); else RTBVH_BS(false, false); }
+#undef RTBVH_BS
+    if (redo) {   // the flagged rays, in the reference order
+        if (count) hipLaunchKernelGGL((k_bounce_redo<true>), dim3(REDO_BLOCKS), dim3(BLOCK), 0, s, a, qin, rl, rc, qout,
+                                      qout_count, (int)emit);
+        else hipLaunchKernelGGL((k_bounce_redo<false>), dim3(REDO_BLOCKS), dim3(BLOCK), 0, s, a, qin, rl, rc, qout,
+                                qout_count, (int)emit);
+    }
 }
 
 void launch_assemble(const float4* bands, const uint32_t* slots, uint32_t stride_rows, uint32_t W, uint32_t H,

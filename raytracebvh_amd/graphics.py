@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 from . import _lib as _L
-from .scene import Scene, camera_reference
+from .scene import EYE_REFERENCE, Scene, camera_look, camera_orbit, camera_reference
 
 
 class Context:
@@ -239,15 +239,20 @@ class Graphics:
     def __init__(self, width: int = 800, height: int = 800, bounces: int = 3, **ctx_kwargs):
         # main.cpp:7 opens an 800x800 window; Graphics.cpp:795 runs 3 reflection passes
         self.width, self.height, self.bounces = width, height, bounces
+        self.eye = np.array(EYE_REFERENCE, np.float32)   # Graphics.h:200-205
         self.ctx = Context(**ctx_kwargs)
 
     def onInit(self, scene: Scene):  # noqa: N802
         self.ctx.set_scene(scene)
 
     def onUpdate(self):  # noqa: N802
-        wvp, wv = camera_reference(self.width, self.height)
+        wvp, wv = camera_look(self.eye, self.width, self.height)
         self.ctx.set_camera(wvp, wv)
         self.computeBVH()
+
+    def onKeyDown(self, key: int):  # noqa: N802
+        """Graphics::onKeyDown (Graphics.cpp:937-960): KEY_LEFT/RIGHT/UP/DOWN orbit the eye about the origin."""
+        self.eye = camera_orbit(self.eye, key)
 
     def computeBVH(self):  # noqa: N802
         self.ctx.compute_bvh(self.width, self.height, self.bounces)

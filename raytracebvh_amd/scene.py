@@ -185,3 +185,24 @@ def camera_reference(width: int, height: int):
     wv = np.zeros(16, np.float32)
     _L.lib().rtbvh_camera_reference(width, height, _L.ptr(wvp), _L.ptr(wv))
     return wvp.reshape(4, 4), wv.reshape(4, 4)
+
+
+def camera_look(eye, width: int, height: int):
+    """Graphics::onUpdate's camera from any eye (at 0, up +y; rtbvh_camera_look): (WVP, WV) as (4,4) f32."""
+    e = np.ascontiguousarray(eye, np.float32).reshape(3)
+    wvp = np.zeros(16, np.float32)
+    wv = np.zeros(16, np.float32)
+    _L.lib().rtbvh_camera_look(_L.ptr(e), width, height, _L.ptr(wvp), _L.ptr(wv))
+    return wvp.reshape(4, 4), wv.reshape(4, 4)
+
+
+# Graphics::onKeyDown's keys (Graphics.cpp:937-960)
+KEY_LEFT, KEY_RIGHT, KEY_UP, KEY_DOWN = 0, 1, 2, 3
+EYE_REFERENCE = (0.0, 5.0, -100.0)   # Graphics.h:200-205
+
+
+def camera_orbit(eye, key: int) -> np.ndarray:
+    """The eye after one Graphics::onKeyDown (rtbvh_camera_orbit): rotated about the origin by CAM_DELTA."""
+    e = np.array(eye, np.float32).reshape(3)
+    _L.lib().rtbvh_camera_orbit(_L.ptr(e), key)
+    return e

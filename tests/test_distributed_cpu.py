@@ -65,16 +65,18 @@ def _worker(rank, world, port, W, H, out_path, nbuf, share=16):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nbuf,share", [(2, 1, 16), (2, 2, 16), (3, 2, 11)])
-def test_band_gather_gloo_matches_full_frame(tmp_path, world, nbuf, share):
-    """World 2 with the even deal (b % nranks), and world 3 with the uneven deal the bench uses
-    for N > 1 (rank 0 traces share/16 of another rank's bands, since it also receives and
-    assembles them): rank 0's gathered frame equals a full-frame oracle render."""
-    W, H = 160, 77   # ragged: 77 rows = 9 full bands + 5 rows
+@pytest.mark.parametrize("world,nbuf,share,H", [(2, 1, 16, 77), (2, 2, 16, 77), (3, 2, 11, 77), (8, 2, 13, 157)])
+def test_band_gather_gloo_matches_full_frame(tmp_path, world, nbuf, share, H):
+    """World 2 with the even deal (b % nranks), world 3 with an uneven deal, and world 8 with the
+    bench's N = 8 deal (root_share 13, bench.py: rank 0 traces 13/16 of another rank's bands, since
+    it also receives and assembles them) through BandGather with two buffers (one gather in flight):
+    rank 0's gathered frame equals a full-frame oracle render.  The frames are ragged (77 rows = 9
+    full bands + 5 rows; 157 = 19 + 5)."""
+    W = 160
     from raytracebvh_amd.tiles import band_row_ids
     if share < 16:   # the deal is uneven here: rank 0 holds fewer rows than the others
         rows = [len(band_row_ids(H, r, world, share)) for r in range(world)]
-        assert rows[0] < min(rows[1:]) and sum(rows) == H
+        assert rows[0] <= min(rows[1:]) and rows[0] < max(rows[1:]) and sum(rows) == H
     out = str(tmp_path / "frames.npy")
     mp.start_processes(_worker, args=(world, _free_port(), W, H, out, nbuf, share), nprocs=world, join=True,
                        start_method="spawn")

@@ -209,7 +209,8 @@ TRACE_MODES = {"reference": 0, "reference+sort": rt.FLAG_SORT_BOUNCE, "nearest":
                "wide+sort": rt.FLAG_WIDE_BVH | rt.FLAG_SORT_BOUNCE,
                "binned": rt.FLAG_BINNED_PRIMARY,
                "binned+wide+refill": WALK_FLAGS | rt.FLAG_BINNED_PRIMARY,
-               "auto": rt.FLAG_AUTO_WALK}
+               "auto": rt.FLAG_AUTO_WALK,
+               "certified": rt.FLAG_CERTIFIED}
 
 
 def _trace_both(s, W, H, bounces, rows=None, flags=0):
@@ -239,7 +240,7 @@ def test_trace_matches_oracle_on_obj(name, W, H, bounces, mode):
     np.testing.assert_array_equal(inten, oint)
     assert sum(st["hits"]) == ost["hits"] and st["textured_hits"] == ost["textured_hits"]
     assert st["bounce_rays"] == ost["bounce"] and st["stack_overflows"] == 0
-    if not any(k in mode for k in ("nearest", "wide", "binned", "auto")):   # reference order: the oracle's steps
+    if not any(k in mode for k in ("nearest", "wide", "binned", "auto", "certified")):   # reference order: the oracle's steps
         assert sum(st["internal_visits"]) == ost["internal_visits"]
         assert sum(st["leaf_visits"]) == ost["leaf_visits"]
     else:
@@ -310,7 +311,7 @@ def _reference_textures():
     return [load_texture(os.path.join(GOLDEN, "textures", str(n))) for n in d["texture_names"]]
 
 
-@pytest.mark.parametrize("mode", ["reference", "nearest+packet+wide", "auto"])
+@pytest.mark.parametrize("mode", ["reference", "nearest+packet+wide", "auto", "certified"])
 def test_reference_scene_with_its_own_textures(mode):
     """The reference's default scene as Graphics::onInit loads it (Graphics.cpp:364: Obj/Test.obj
     with Balls.jpg and Map__1_Composite.bmp), 1920x1080, primary + 1 bounce: GPU frame equals the
@@ -949,17 +950,19 @@ def test_stack_limit_reports_overflow(mode):
     assert not np.array_equal(frames[2], frames[0])
 
 
+CERT_WALKS = rt.FLAG_NEAREST_FIRST | rt.FLAG_REFILL_BOUNCE | rt.FLAG_WIDE_BVH | rt.FLAG_BINNED_PRIMARY
+
+
 def test_verify_walk_and_auto_walk():
     """rtbvh_verify_walk: the fast walks render the reference-order frame (0 differing pixels);
-    RTBVH_FLAG_AUTO_WALK takes the reference-order kernels on small scenes, and on large ones
-    checks the first frame of a key on the device (walk_state 1, the reference frame) before the
-    fast walks (binned primary pass, 4-wide nearest-first bounce walk) take over (walk_state 2),
-    with the same frames throughout."""
+    RTBVH_FLAG_AUTO_WALK takes the reference-order kernels on small scenes and, on large ones, the
+    certified fast walks (binned primary pass, 4-wide bounce walk, per-ray certificates)
+    from the first frame on (walk_state 2), with the reference frame throughout."""
     d = load_scene_fixture("Test")
     small = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
     big = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
     W, H = 960, 540
-    for s, walk in ((small, 0), (big, WALK_FLAGS | rt.FLAG_BINNED_PRIMARY)):
+    for s, walk in ((small, 0), (big, CERT_WALKS)):
         with rt.Context(device=0) as ref, rt.Context(device=0, flags=rt.FLAG_AUTO_WALK) as auto, \
                 rt.Context(device=0, flags=TRACE_MODES["nearest+packet+wide"]) as fast:
             for c in (ref, auto, fast):
@@ -967,29 +970,26 @@ def test_verify_walk_and_auto_walk():
                 c.set_camera(*rt.camera_reference(W, H))
                 c.compute_bvh(W, H, 1)
             want = ref.read_framebuffer()
-            st = auto.stats()
-            assert st["walk_flags"] == 0 and st["walk_state"] == (1 if walk else 0)
-            assert st["walk_checks"] == (1 if walk else 0) and st["walk_fallbacks"] == 0
-            np.testing.assert_array_equal(auto.read_framebuffer(), want)
-            auto.compute_bvh(W, H, 1)   # the key is verified: the fast walks
-            st = auto.stats()
-            assert st["walk_flags"] == walk and st["walk_state"] == (2 if walk else 0)
-            assert st["walk_checks"] == (1 if walk else 0)
-            np.testing.assert_array_equal(auto.read_framebuffer(), want)
-            np.testing.assert_array_equal(auto.read_intensity(), ref.read_intensity())
+            for k in range(2):
+                st = auto.stats()
+                assert st["walk_flags"] == walk and st["walk_state"] == (2 if walk else 0)
+                assert st["walk_checks"] == (k + 1 if walk else 0)
+                np.testing.assert_array_equal(auto.read_framebuffer(), want)
+                np.testing.assert_array_equal(auto.read_intensity(), ref.read_intensity())
+                auto.compute_bvh(W, H, 1)
             assert fast.verify_walk(W, H, 1) == 0
             np.testing.assert_array_equal(fast.read_framebuffer(), want)
             assert auto.verify_walk(W, H, 1) == 0
 
 
 def test_containment_failure_auto_walk_returns_the_reference_frame():
-    """VERDICT r2 missing #3: on a scene where containment fails (tests/containment.py: two
-    coplanar triangles whose Moller-Trumbore t rounds below their slab entry), the 4-wide packet
-    walk's frame DIFFERS from findCollision's (RayTraceTraversal.hlsl:106-193) at PIXEL, and
-    rtbvh_verify_walk reports it.  RTBVH_FLAG_AUTO_WALK (the scene is above its 65536-triangle
-    size) returns the reference frame -- equal to the CPU oracle's -- on the checked first frame
-    and, after the check found the difference, keeps the key on the reference order
-    (walk_state 3, one fallback), also through the hipGraph path."""
+    """On a scene where containment fails (tests/containment.py: two coplanar triangles whose
+    Moller-Trumbore t rounds below their slab entry), the 4-wide packet walk's frame DIFFERS from
+    findCollision's (RayTraceTraversal.hlsl:106-193) at PIXEL, and rtbvh_verify_walk reports it.
+    RTBVH_FLAG_AUTO_WALK (the scene is above its 65536-triangle size) takes the certified walks: the
+    pixel's hit (B, whose t lies below its own box's entry) fails its certificate and is re-traced in
+    the reference order (redo_rays[0] >= 1), so the frame is the reference's -- equal to the CPU
+    oracle's -- on every frame, also through the hipGraph path."""
     from tests.containment import PIXEL, H, W, containment_scene, identity_camera
     s = containment_scene()
     wvp, wv = identity_camera()
@@ -1009,15 +1009,77 @@ def test_containment_failure_auto_walk_returns_the_reference_frame():
         assert not np.array_equal(got[y, x], want[y, x])     # the fast walk took A, the reference B
         assert fast.verify_walk(W, H, 1) > 0
         for c in (auto, gauto):
-            st = c.stats()
-            assert st["walk_checks"] == 1 and st["walk_fallbacks"] == 1
-            np.testing.assert_array_equal(c.read_framebuffer(), want)
-            for _ in range(2):
+            for _ in range(3):
+                st = c.stats()
+                assert st["walk_state"] == 2 and st["walk_flags"] == CERT_WALKS
+                assert st["redo_rays"][0] >= 1 and st["walk_fallbacks"] >= 1
+                np.testing.assert_array_equal(c.read_framebuffer(), want)
                 c.set_camera(wvp.copy(), wv.copy())   # every frame, unchanged (Graphics::onUpdate)
                 c.compute_bvh(W, H, 1)
-                np.testing.assert_array_equal(c.read_framebuffer(), want)
-                st = c.stats()
-                assert st["walk_state"] == 3 and st["walk_flags"] == 0 and st["walk_checks"] == 1
+        assert gauto.stats()["graph_captures"] == 1
+
+
+def test_auto_walk_orbit_replays_one_graph():
+    """the reference's only interaction orbits the eye (Graphics::onKeyDown,
+    Graphics.cpp:937-960) and re-uploads WVP / WV every frame (Graphics.cpp:40-56).  Under
+    RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_GRAPH at 200k triangles, five distinct cameras (four key presses)
+    replay ONE captured graph (graph_captures == 1; the camera lives in a device buffer) with the
+    certified walks, and every frame equals the reference-order frame of its camera (and the CPU
+    oracle's on one of them)."""
+    s = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    W, H, B = 960, 540, 1
+    eye = np.array(rt.EYE_REFERENCE, np.float32)
+    cams = []
+    for key in (None, rt.KEY_LEFT, rt.KEY_LEFT, rt.KEY_UP, rt.KEY_RIGHT):
+        if key is not None:
+            eye = rt.camera_orbit(eye, key)
+        cams.append(rt.camera_look(eye, W, H))
+    with rt.Context(device=0, flags=rt.FLAG_AUTO_WALK | rt.FLAG_GRAPH) as g, rt.Context(device=0) as ref:
+        g.set_scene(s)
+        ref.set_scene(s)
+        for i, (wvp, wv) in enumerate(cams):
+            g.set_camera(wvp, wv)
+            g.compute_bvh(W, H, B)
+            ref.set_camera(wvp, wv)
+            ref.compute_bvh(W, H, B)
+            want = ref.read_framebuffer()
+            np.testing.assert_array_equal(g.read_framebuffer(), want, err_msg=f"camera {i}")
+            np.testing.assert_array_equal(g.read_intensity(), ref.read_intensity())
+            st = g.stats()
+            assert st["graph_captures"] == 1 and st["walk_state"] == 2 and st["walk_flags"] == CERT_WALKS
+            if i == 2:   # the oracle on one camera (1 row in 8)
+                nodes = ref.read_bvh()
+                np.testing.assert_array_equal(g.read_bvh()["bb_min"], nodes["bb_min"])
+                ofb, _, _ = orc.trace(_oscene(s), nodes, wvp, wv, W, H, B, 0, H, 8)
+                np.testing.assert_array_equal(want[0:H:8], ofb)
+        assert len({c[0].tobytes() for c in cams}) == 5
+
+
+def test_certified_walks_flag_rays_past_the_margin():
+    """A ray the certified bounce walk cannot vouch for -- here every ray of a scene whose triangles are
+    too large for the margin's range (margin.h: condition (C) fails for edges of ~60 units at any t) --
+    is re-traced in the reference order: the frame equals the reference's, and the bounce pass's
+    re-trace count is the whole live queue."""
+    rng = np.random.default_rng(7)
+    n = 70_000
+    cen = np.stack([rng.uniform(-60, 60, n), rng.uniform(-60, 60, n), rng.uniform(-20, 20, n)], 1)
+    off = rng.uniform(-8, 8, (n, 3, 3))   # object-space edges up to ~28: clip-space edges of ~60
+    v = np.zeros((3 * n, 8), np.float32)
+    v[:, :3] = (cen[:, None, :] + off).reshape(-1, 3)
+    v[:, 5] = -1.0
+    base = rt.synthetic(1, seed=1, half_extent=(1, 1, 1))
+    s = rt.Scene(v, np.arange(3 * n, dtype=np.uint32), np.zeros(n, np.uint32), base.material_blob)
+    W, H = 320, 240
+    with rt.Context(device=0) as ref, rt.Context(device=0, flags=rt.FLAG_AUTO_WALK) as auto:
+        for c in (ref, auto):
+            c.set_scene(s)
+            c.set_camera(*rt.camera_reference(W, H))
+            c.compute_bvh(W, H, 1)
+        np.testing.assert_array_equal(auto.read_framebuffer(), ref.read_framebuffer())
+        np.testing.assert_array_equal(auto.read_intensity(), ref.read_intensity())
+        st = auto.stats()
+        assert st["walk_state"] == 2 and st["bounce_rays"] > 0
+        assert st["redo_rays"][1] == st["bounce_rays"]
 
 
 @pytest.mark.parametrize("nranks,share", [(2, 16), (3, 16), (8, 16), (3, 11), (8, 13)])

@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol():
     L = rt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.rtbvh_abi_version() == 5
+    assert L.rtbvh_abi_version() == 6
 
 
 def test_layout_sizes():
@@ -101,6 +101,32 @@ def test_camera_matches_oracle():
     # SURVEY §8(d) quotes these WVP rows at 1920x1080
     np.testing.assert_allclose(wvp[0], [4.291935, 0, 0, 0], atol=1e-5)
     np.testing.assert_allclose(wvp[3], [0, 0, 100.03492, 100.12492], atol=1e-3)
+
+
+def test_camera_orbit_is_graphics_on_key_down():
+    """rtbvh_camera_orbit restates Graphics::onKeyDown (Graphics.cpp:937-960): eye = at + (eye - at) R with
+    DirectXMath's RotationY(-+0.1) / RotationX(+-0.1) (row vectors, CAM_DELTA .1f, Graphics.h:14); left and
+    right (up and down) undo each other; the distance to the origin is kept; camera_look at the reference
+    eye is the reference camera (Graphics.cpp:44-53)."""
+    eye = np.array(rt.EYE_REFERENCE, np.float32)
+    for W, H in ((1920, 1080), (3840, 2160)):
+        a, b = rt.camera_look(eye, W, H), rt.camera_reference(W, H)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+    c, s = np.cos(0.1), np.sin(0.1)
+    ry = lambda a: np.array([[np.cos(a), 0, -np.sin(a)], [0, 1, 0], [np.sin(a), 0, np.cos(a)]])
+    rx = lambda a: np.array([[1, 0, 0], [0, np.cos(a), np.sin(a)], [0, -np.sin(a), np.cos(a)]])
+    want = {rt.KEY_LEFT: eye @ ry(-0.1), rt.KEY_RIGHT: eye @ ry(0.1), rt.KEY_UP: eye @ rx(0.1), rt.KEY_DOWN: eye @ rx(-0.1)}
+    for key, w in want.items():
+        np.testing.assert_allclose(rt.camera_orbit(eye, key), w, rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(rt.camera_orbit(rt.camera_orbit(eye, rt.KEY_LEFT), rt.KEY_RIGHT), eye, atol=1e-4)
+    np.testing.assert_allclose(rt.camera_orbit(rt.camera_orbit(eye, rt.KEY_UP), rt.KEY_DOWN), eye, atol=1e-4)
+    e = eye
+    for _ in range(63):   # ~2 pi of left presses
+        e = rt.camera_orbit(e, rt.KEY_LEFT)
+    assert abs(np.linalg.norm(e) - np.linalg.norm(eye)) < 1e-3
+    np.testing.assert_array_equal(rt.camera_orbit(eye, 7), eye)   # other keys: unchanged
+    assert c > 0 and s > 0
 
 
 @pytest.mark.parametrize("H,n", [(1080, 1), (1080, 2), (1080, 8), (2160, 8), (7, 3), (17, 4)])
