@@ -375,16 +375,22 @@ def main():
         t0 = time.perf_counter()
         last = run(args.steps, inflight)
         torch.cuda.synchronize()
+        t_own = time.perf_counter() - t0   # this rank's own time, before waiting for the others
         barrier()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        own = torch.tensor([t_own / args.steps * 1e3], dtype=torch.float64, device=dev)
+        rank_ms = [float(own.item())]
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            allown = [torch.zeros_like(own) for _ in range(world)]
+            dist.all_gather(allown, own)
+            rank_ms = [round(float(x.item()), 4) for x in allown]
         ms = float(el.item()) / args.steps * 1e3
         rays = float(tot[0].item())
         # the output: the frame assembled on rank 0 (one rank: its band buffer is the frame)
         frame = g.frames[(args.steps - 1) % g.nbuf].clone() if rank == 0 else None
         return dict(ms_step=ms, rays=rays, value=rays / (ms * 1e-3) / 1e6, stats=ctx.stats(),
-                    band=last.clone(), frame=frame)
+                    band=last.clone(), frame=frame, rank_ms=rank_ms)
 
     # reference order (the exact findCollision DFS), nearest-first, and nearest-first on the
     # 4-wide view; a nearest-first number is the headline only if its frame is bit-identical
@@ -424,6 +430,9 @@ def main():
         use_name = pref
     use = res[use_name]
     traversal["mode"] = use_name
+    # each rank's own ms per step before the closing barrier (rank 0 also receives and assembles the
+    # frame): the data the band deal's root_share is fitted to
+    traversal["rank_ms_per_step"] = use["rank_ms"]
     mode_flags = modes[use_name]
     rays_per_step, ms_step, value = use["rays"], use["ms_step"], use["value"]
     # one frame at a time (one context, one stream): the per-frame latency, and the kernels'

@@ -887,6 +887,9 @@ static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 4 x 4 bloc
 #define RTBVH_PB_RASTER_BLOCK 256
 #endif
 constexpr uint32_t PB_RASTER_BLOCK = RTBVH_PB_RASTER_BLOCK;   // threads per tile of k_primary_binned
+#ifndef RTBVH_PB_ROWMAJOR
+#define RTBVH_PB_ROWMAJOR 0   // the fine phase's lanes: 0 = 8x8 / 16x4 / 32x2 pixel blocks, 1 = row-major (A/B)
+#endif
 template <bool COUNT>
 __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
                                                              const uint4* __restrict__ bins, uint32_t cap,
@@ -1006,12 +1009,23 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs
             const int sy0 = __builtin_amdgcn_readlane(ry0, k), sy1 = __builtin_amdgcn_readlane(ry1, k);
             const float sz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(zmin), k));
             const int lw = sx1 - sx0 + 1;
+#if RTBVH_PB_ROWMAJOR
+            // the rectangle's pixels row-major, 64 a pass: lane p of pass b is pixel b * 64 + p at
+            // (q % lw, q / lw); q / lw by a multiply-shift (q < 1024, lw <= 32: exact with the
+            // rounded-up 2^16 / lw).  A C5 leaf's ~9 x 5 pixels take one pass, not two of 16 x 4
+            const uint32_t npx = (uint32_t)(lw * (sy1 - sy0 + 1)), mg = (65536u + (uint32_t)lw - 1u) / (uint32_t)lw;
+            for (uint32_t q0 = 0; q0 < npx; q0 += 64) {
+                const uint32_t q = q0 + lane, qy = (q * mg) >> 16, qx = q - qy * (uint32_t)lw;
+                const bool ok = q < npx;
+                const uint32_t pi = (uint32_t)(((int)qy + sy0) * (int)PB_TILE + sx0 + (int)qx);
+#else
             const int cs = lw <= 8 ? 3 : lw <= 16 ? 4 : 5;   // lanes as 8x8, 16x4 or 32x2 pixels
             const int col = (int)(lane & ((1u << cs) - 1)), px = sx0 + col;
             for (int y0 = sy0; y0 <= sy1; y0 += 64 >> cs) {
                 const int y = y0 + (int)(lane >> cs);
                 const bool ok = col < lw && y <= sy1;
                 const uint32_t pi = (uint32_t)(y * (int)PB_TILE + px);
+#endif
                 const bool need = ok && (sg || sz <= __uint_as_float(s_t[2 * pb_slot(pi) + 1]));
                 const uint64_t nm = __ballot(need);
                 if (qn + (uint32_t)__popcll(nm) > PB_QCAP) flush();

@@ -47,6 +47,11 @@ def main():
     if os.environ.get("AB_SET") == "binnedbase":   # the binned mode only (A/B of two builds via RTBVH_LIB)
         variants = [("binned", rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
                      | rt.FLAG_BINNED_PRIMARY)]
+    if os.environ.get("AB_SET") == "certified":   # the certified walks (AUTO) against the same walks unchecked
+        variants = [("binned", rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
+                     | rt.FLAG_BINNED_PRIMARY), ("certified", rt.FLAG_CERTIFIED)]
+    if os.environ.get("AB_SET") == "certbase":   # the certified mode only (A/B of two builds via RTBVH_LIB)
+        variants = [("certified", rt.FLAG_CERTIFIED)]
     if os.environ.get("AB_SET") == "binned":   # primary pass: 4-wide packets vs screen-tile bins
         base = rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH
         variants = [("nearest-first-wide", base), ("binned", base | rt.FLAG_BINNED_PRIMARY)]
@@ -81,7 +86,8 @@ def main():
             st = ctx.stats()
             print(json.dumps({"variant": v, "packet_steps": list(st["packet_steps"]),
                               "internal_visits": list(st["internal_visits"]), "leaf_visits": list(st["leaf_visits"]),
-                              "trav_wave_steps": st["trav_wave_steps"], "bin_entries": list(st["bin_entries"])}))
+                              "trav_wave_steps": st["trav_wave_steps"], "bin_entries": list(st["bin_entries"]),
+                              "redo_rays": list(st["redo_rays"])}))
     for (v, srt), xs in res.items():
         a = np.array(xs)
         print(json.dumps({"variant": v, "primary_ms_med": float(np.median(a[:, 0])),

@@ -11,7 +11,8 @@ import raytracebvh_amd as rt  # noqa: E402
 mode = os.environ.get("PROF_MODE", "nearest")
 names = {"reference": 0, "nearest": rt.FLAG_NEAREST_FIRST, "sort": rt.FLAG_SORT_BOUNCE,
          "packet": rt.FLAG_PACKET_PRIMARY, "count": rt.FLAG_COUNT_VISITS, "refill": rt.FLAG_REFILL_BOUNCE,
-         "wide": rt.FLAG_WIDE_BVH, "binned": rt.FLAG_BINNED_PRIMARY}
+         "wide": rt.FLAG_WIDE_BVH, "binned": rt.FLAG_BINNED_PRIMARY, "certified": rt.FLAG_CERTIFIED,
+         "auto": rt.FLAG_AUTO_WALK}
 flags = 0
 for m in mode.split("+"):
     flags |= names[m]
