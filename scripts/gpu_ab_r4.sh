@@ -12,3 +12,9 @@ if [ -n "${AB_LIBS:-}" ]; then
   AB_SET=${LIB_SET:-certbase} ROUNDS=${ROUNDS:-2} timeout -k 10 900 bash scripts/ab_libs.sh $AB_LIBS > gpurun_out/${T}_libs.log 2>&1 || { echo "LIB AB FAILED"; tail -20 gpurun_out/${T}_libs.log; exit 1; }
   cat gpurun_out/${T}_libs.log
 fi
+if [ "${PB_PHASES:-0}" = 1 ]; then   # k_primary_binned's phase split (RTBVH_PB_PROF builds)
+  for lib in raytracebvh_amd/librtbvh_prof.so raytracebvh_amd/librtbvh_rmprof.so; do
+    RTBVH_LIB=$(realpath $lib) timeout -k 10 300 python -u scripts/pb_phases.py > gpurun_out/${T}_phases_$(basename $lib .so).log 2>&1 || { echo "PHASES FAILED"; tail -10 gpurun_out/${T}_phases_$(basename $lib .so).log; exit 1; }
+    echo "$lib: $(cat gpurun_out/${T}_phases_$(basename $lib .so).log)"
+  done
+fi

@@ -12,6 +12,6 @@ timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/${T}_bench.jso
 cat gpurun_out/${T}_bench.json
 if [ "${PROF:-0}" = 1 ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o prof -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-extras --steps 10 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.err || { echo "PROF FAILED"; tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.err; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o prof -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-extras --steps 10 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.err || { echo "PROF FAILED"; tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.err; exit 1; }
   echo prof ok
 fi
