@@ -23,7 +23,8 @@ the BVH and traces every frame, behind a fence -- is measured beside it at N = 1
 ("c5_frame_rebuild", its ms and Mrays/s also at the line's top level), and so is the reference's only
 interaction, the eye orbiting by Graphics::onKeyDown every frame ("c5_orbit": rebuild + trace of a new
 camera per frame under RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_GRAPH, frames checked against the reference
-order).  value = all rays of the frame (W*H primary + every live bounce ray, summed over ranks) /
+order; beside it the same cameras' frames with the eye standing still, and the C5 camera under the
+same flags).  value = all rays of the frame (W*H primary + every live bounce ray, summed over ranks) /
 max-over-ranks time per step.  The reported traversal is the certified walk of RTBVH_FLAG_AUTO_WALK
 (the reference-order frame by construction, per-ray certificates) unless another mode
 whose frame is identical in this run is clearly faster.
@@ -635,11 +636,35 @@ def main():
                     co.compute_bvh(W, H, bounces)
                 dto = (time.perf_counter() - t0) / nfr
                 qo = co.stats()
+                caps = int(qo["graph_captures"])
                 orb.update({"ms_per_frame": round(dto * 1e3, 4), "frames": nfr,
                             "mrays_s": round((qo["primary_rays"] + qo["bounce_rays"]) / dto / 1e6, 1),
-                            "graph_captures": int(qo["graph_captures"]), "walk_state": int(qo["walk_state"]),
+                            "graph_captures": caps, "walk_state": int(qo["walk_state"]),
                             "redo_rays_last_frame": list(qo["redo_rays"]),
                             "vs_c5_frame_rebuild": round(dto * 1e3 / reb["ms_per_frame_graph"], 4)})
+                # the same frames with the camera standing still: each timed camera set (and its first
+                # frame run) outside the clock, then one frame of it timed -- what a moving camera costs
+                # over the frames it renders (the views differ: a rotated eye sees other rays than C5's)
+                st_t = 0.0
+                for i in range(2, nfr + 2):
+                    co.set_camera(*cams[i])
+                    co.compute_bvh(W, H, bounces)
+                    t0 = time.perf_counter()
+                    co.compute_bvh(W, H, bounces)
+                    st_t += time.perf_counter() - t0
+                dts = st_t / nfr
+                # and the reference camera under the same flags (the c5_frame_rebuild frame, certified walks)
+                co.set_camera(wvp, wv)
+                co.compute_bvh(W, H, bounces)
+                t0 = time.perf_counter()
+                for _ in range(nfr):
+                    co.compute_bvh(W, H, bounces)
+                dtr = (time.perf_counter() - t0) / nfr
+                orb.update({"same_cameras_static_ms_per_frame": round(dts * 1e3, 4),
+                            "vs_same_cameras_static": round(dto / dts, 4),
+                            "c5_camera_same_flags_ms_per_frame": round(dtr * 1e3, 4),
+                            "vs_c5_camera_same_flags": round(dto / dtr, 4),
+                            "graph_captures_after_static": int(co.stats()["graph_captures"]) - caps})
                 # frames: the last timed camera and an earlier one, re-rendered (deterministic) against the
                 # reference-order frame of the same camera
                 checks = []
@@ -763,6 +788,7 @@ def main():
             "c5_frame_rebuild_mrays_s": reb.get("mrays_s_graph"),
             "c5_orbit_ms": orb.get("ms_per_frame"),
             "c5_orbit_mrays_s": orb.get("mrays_s"),
+            "c5_orbit_vs_same_cameras_static": orb.get("vs_same_cameras_static"),
             "roofline": roofline,
             "build_roofline": build_roofline,
             "parity": parity,

@@ -580,7 +580,10 @@ rtbvh_status sync_all(rtbvh_ctx* c) {
 // rtbvh_set_camera changed it -- after the frames in flight, which read the old one -- and ordered
 // before stream s.  A captured frame (RTBVH_FLAG_GRAPH) reads the buffer, so it survives a camera change
 // (Graphics::onUpdate writes the camera every frame and the arrow keys orbit it, Graphics.cpp:40-56,
-// 937-960).  The source is pageable (the matrices in the context), so the copy is staged at the call.
+// 937-960).  The matrices travel as a kernel argument (launch_set_camera): captured at the call, one
+// dispatch, no pageable host copy (staged through the driver at the call).  Never inside a capture:
+// compute_graph's plain frame before it has cleared cam_dirty, and the captured frame must not bake a
+// camera in.
 rtbvh_status sync_camera(rtbvh_ctx* c, hipStream_t s) {
     if (!c->cam_dirty) return RTBVH_OK;
     for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT; k++)
@@ -588,8 +591,8 @@ rtbvh_status sync_camera(rtbvh_ctx* c, hipStream_t s) {
             HIPC(c, hipStreamWaitEvent(c->stream, c->ev_slot[k], 0));
             c->slot_busy[k] = false;
         }
-    HIPC(c, hipMemcpyAsync(c->d_cam, c->wvp, sizeof(c->wvp), hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipMemcpyAsync(c->d_cam + 16, c->wv, sizeof(c->wv), hipMemcpyHostToDevice, c->stream));
+    launch_set_camera(c->wvp, c->wv, c->d_cam, c->stream);
+    HIPC(c, hipGetLastError());
     if (s != c->stream) {
         HIPC(c, hipEventRecord(c->ev_built, c->stream));
         HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));

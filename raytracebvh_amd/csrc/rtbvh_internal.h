@@ -213,6 +213,9 @@ void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qi
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s,
                          const Redo* redo = nullptr);
 // *diff += the number of the n float4 pixels of a and b whose bits differ
+// the context's device camera (WVP then WV, 32 floats) written by one dispatch in stream order
+struct CameraWords { float w[32]; };
+void launch_set_camera(const float* wvp, const float* wv, float* cam, hipStream_t s);
 void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long long* diff, hipStream_t s);
 void launch_count_diff32(const float* a, const float* b, size_t n, unsigned long long* diff, hipStream_t s);
 // frame from per-rank compact band buffers (stride_rows rows apart), see rtbvh_assemble_bands

@@ -2108,6 +2108,21 @@ void launch_present(const float4* color, uint32_t W, uint32_t H, uint32_t* out, 
     if (n) hipLaunchKernelGGL(k_present, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, color, W, H, out);
 }
 
+// the camera upload (sync_camera): the 32 floats travel as the kernel's by-value argument, so the copy is
+// one dispatch in stream order -- no DMA engine, no staging of the pageable host matrices
+__global__ __launch_bounds__(64) void k_set_camera(CameraWords m, float* __restrict__ cam) {
+    if (threadIdx.x < 32) cam[threadIdx.x] = m.w[threadIdx.x];
+}
+
+void launch_set_camera(const float* wvp, const float* wv, float* cam, hipStream_t s) {
+    CameraWords m;
+    for (int i = 0; i < 16; i++) {
+        m.w[i] = wvp[i];
+        m.w[16 + i] = wv[i];
+    }
+    hipLaunchKernelGGL(k_set_camera, dim3(1), dim3(64), 0, s, m, cam);
+}
+
 void launch_count_diff(const float4* a, const float4* b, size_t n, unsigned long long* diff, hipStream_t s) {
     if (n == 0) return;
     size_t blocks = (n + BLOCK - 1) / BLOCK;
