@@ -887,6 +887,10 @@ static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 4 x 4 bloc
 #define RTBVH_PB_RASTER_BLOCK 256
 #endif
 constexpr uint32_t PB_RASTER_BLOCK = RTBVH_PB_RASTER_BLOCK;   // threads per tile of k_primary_binned
+// cost probes (A/B builds only, wrong frames): 1 = no fine phase, 2 = the fine phase's tests skipped
+#ifndef RTBVH_PB_PROBE
+#define RTBVH_PB_PROBE 0
+#endif
 #ifndef RTBVH_PB_ROWMAJOR
 #define RTBVH_PB_ROWMAJOR 0   // the fine phase's lanes: 0 = 8x8 / 16x4 / 32x2 pixel blocks, 1 = row-major (A/B)
 #endif
@@ -968,7 +972,7 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs
         uint32_t qn = 0;
         const auto flush = [&]() {
             PB_T(3);
-            for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
+            for (uint32_t q0 = 0; q0 < (RTBVH_PB_PROBE == 2 ? 0u : qn); q0 += 64) {
                 const bool act = q0 + lane < qn;
                 const uint32_t v = act ? sq[q0 + lane] : 0u;
                 const int k = (int)(v >> 10);
@@ -1002,7 +1006,7 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs
             PB_T(4);
         };
         // 3: fine, survivor by survivor
-        for (uint64_t todo = __ballot(surv); todo; todo &= todo - 1) {
+        for (uint64_t todo = RTBVH_PB_PROBE == 1 ? 0ull : __ballot(surv); todo; todo &= todo - 1) {
             const int k = __ffsll((unsigned long long)todo) - 1;
             const bool sg = __builtin_amdgcn_readlane((int)gen, k) != 0;
             const int sx0 = __builtin_amdgcn_readlane(rx0, k), sx1 = __builtin_amdgcn_readlane(rx1, k);
@@ -1376,6 +1380,11 @@ __device__ __forceinline__ bool qbox_fast(const QAxis& x, const QAxis& y, const 
     return 0 <= mx && mn <= mx && (!hit || mn <= best);
 }
 
+// A/B builds only (not certified): 1 = no margin (the unchecked walk's pruning inside the certified
+// code), 2 = the margin's range taken as unbounded
+#ifndef RTBVH_CERT_AB
+#define RTBVH_CERT_AB 0
+#endif
 // GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it).
 // CERT (MODE 2 only): the certified walk.  Every box test's entry distance is taken on the
 // box grown by the margin rho(best) (margin.h: no hit the triangle test accepts at t <= best lies outside
@@ -1607,9 +1616,9 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     key = k < key ? k : key;
                     if (CERT) {   // the pruning bound and the margin of the new best
                         const float tk = key_t(key);
-                        const bool cov = tk <= mg.tcap;
-                        kb = cov ? tk : __builtin_inff();
-                        rr = cov ? fmaf(mg.r1, tk, mg.r0) : 0.f;
+                        const bool cov = RTBVH_CERT_AB == 2 || tk <= mg.tcap;
+                        kb = cov || RTBVH_CERT_AB == 1 ? tk : __builtin_inff();
+                        rr = cov && RTBVH_CERT_AB != 1 ? fmaf(mg.r1, tk, mg.r0) : 0.f;
                     }
                 }
                 if (!done && node == INVALID) {   // pop, dropping entries that cannot improve

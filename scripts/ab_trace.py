@@ -71,7 +71,7 @@ def main():
             for _ in range(3):
                 ctx.trace(W, H, 1, sync=False)
             st = ctx.stats()
-            res[(v, srt)].append((st["ms_stage"][5], st["ms_stage"][6], st["ms_trace"]))
+            res[(v, srt)].append((st["ms_stage"][5], st["ms_stage"][6], st["ms_trace"], st["ms_stage"][7]))
             if r == 0:
                 fb = ctx.read_framebuffer()
                 if ref is None:
@@ -87,12 +87,14 @@ def main():
             print(json.dumps({"variant": v, "packet_steps": list(st["packet_steps"]),
                               "internal_visits": list(st["internal_visits"]), "leaf_visits": list(st["leaf_visits"]),
                               "trav_wave_steps": st["trav_wave_steps"], "bin_entries": list(st["bin_entries"]),
-                              "redo_rays": list(st["redo_rays"])}))
+                              "redo_rays": list(st["redo_rays"]), "trav_max_steps": st["trav_max_steps"],
+                              "trav_steps_log2": list(st["trav_steps_log2"])}))
     for (v, srt), xs in res.items():
         a = np.array(xs)
         print(json.dumps({"variant": v, "primary_ms_med": float(np.median(a[:, 0])),
                           "bounce_ms_med": float(np.median(a[:, 1])), "trace_ms_med": float(np.median(a[:, 2])),
-                          "trace_ms_min": float(a[:, 2].min())}))
+                          "trace_ms_min": float(a[:, 2].min()), "bounce_trav_ms_med": float(np.median(a[:, 3])),
+                          "bounce_trav_ms_min": float(a[:, 3].min())}))
 
 
 if __name__ == "__main__":
