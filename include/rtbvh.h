@@ -216,6 +216,9 @@ typedef struct {
     /* RTBVH_FLAG_AUTO_WALK, last trace: the rays re-traced in the reference order because their certificate
      * failed, of the primary pass [0] and of the bounce passes [1] */
     uint64_t redo_rays[2];
+    /* RTBVH_FLAG_COUNT_VISITS with RTBVH_FLAG_REFILL_BOUNCE, last trace: the longest bounce walk, as its
+     * loop iterations << 32 | the pixel (framebuffer index) of its ray */
+    uint64_t trav_longest;
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 

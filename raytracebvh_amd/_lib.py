@@ -81,7 +81,8 @@ class Stats(ctypes.Structure):
                 ("graph_captures", ctypes.c_uint64), ("walk_flags", ctypes.c_uint32),
                 ("walk_state", ctypes.c_uint32), ("packet_steps", ctypes.c_uint64 * 2),
                 ("walk_checks", ctypes.c_uint64), ("walk_fallbacks", ctypes.c_uint64),
-                ("bin_entries", ctypes.c_uint64 * 2), ("redo_rays", ctypes.c_uint64 * 2)]
+                ("bin_entries", ctypes.c_uint64 * 2), ("redo_rays", ctypes.c_uint64 * 2),
+                ("trav_longest", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         d = {}

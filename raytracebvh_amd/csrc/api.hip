@@ -1673,6 +1673,7 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         out->textured_hits = cnt[9];
         out->trav_wave_steps = cnt[10];
         out->trav_max_steps = cnt[13];
+        out->trav_longest = cnt[20];
         for (int k = 0; k < 32; k++) out->trav_steps_log2[k] = cnt[32 + k];
         out->trav_mixed_steps = cnt[11];
         out->trav_active_lanes = cnt[12];

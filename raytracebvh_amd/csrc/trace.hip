@@ -1703,6 +1703,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                 const uint32_t steps = 2 * T + 2 - guard;
                 atomicAdd(&counters[32 + (31 - __clz(steps | 1u))], 1ull);
                 atomicMax(&counters[13], (unsigned long long)steps);
+                atomicMax(&counters[20], (unsigned long long)steps << 32 | qin[r].idx);   // (the longest: its pixel)
             }
         }
     }
