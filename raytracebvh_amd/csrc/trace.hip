@@ -1617,8 +1617,24 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     if (CERT) {   // the pruning bound and the margin of the new best
                         const float tk = key_t(key);
                         const bool cov = RTBVH_CERT_AB == 2 || tk <= mg.tcap;
-                        kb = cov || RTBVH_CERT_AB == 1 ? tk : __builtin_inff();
+                        const float kbn = cov || RTBVH_CERT_AB == 1 ? tk : __builtin_inff();
                         rr = cov && RTBVH_CERT_AB != 1 ? fmaf(mg.r1, tk, mg.r0) : 0.f;
+                        if (kb == __builtin_inff() && kbn != __builtin_inff() && RTBVH_CERT_AB != 1) {
+                            // the first finite bound: the stacked entries' distances were taken without a
+                            // margin (nothing was pruned by distance before), and from now on the pops
+                            // compare them with the bound -- lower each to a bound on its box's entry grown
+                            // by rr (max over axes of near - rr |1/d| >= entry - rr max |1/d|)
+                            const float dm = rr * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
+                            for (int s2 = 0; s2 < sp; s2++) {
+                                if (s2 < SW) {
+                                    s_wt[s2][tid] = bf16_down(bf16_up(s_wt[s2][tid]) - dm);
+                                } else {
+                                    uint2& e = wstack[s2 - SW];
+                                    e.y = __float_as_uint(__uint_as_float(e.y) - dm);
+                                }
+                            }
+                        }
+                        kb = kbn;
                     }
                 }
                 if (!done && node == INVALID) {   // pop, dropping entries that cannot improve
