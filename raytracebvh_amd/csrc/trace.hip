@@ -1590,6 +1590,11 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     float k0, k1, k2, k3;
                     uint32_t i0, i1, i2, i3;
                     qchildren(q0, q1, q2, q3, k0, k1, k2, k3, i0, i1, i2, i3);
+#ifdef RTBVH_DEBUG_PIXEL   // (scripts/debug_walk.py: one ray's walk, step by step, from the COUNT kernel)
+                    if (COUNT && qin[r].idx == (uint32_t)RTBVH_DEBUG_PIXEL)
+                        printf("DBG %d q %u sp %d kb %.6g key %.6g | %.6g %x %.6g %x %.6g %x %.6g %x\n", (int)CERT, node,
+                               sp, kb, key_t(key), k0, i0, k1, i1, k2, i2, k3, i3);
+#endif
                     const bool lf0 = i0 != INVALID && (i0 & LEAF_BIT);
                     L = lf0 ? i0 : INVALID;
                     node = lf0 ? i1 : i0;   // INVALID when no child is left -> pop below
@@ -1603,6 +1608,10 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                         if (!lf0 && i1 != INVALID) wpush(i1, k1);
                     }
                 }
+#ifdef RTBVH_DEBUG_PIXEL
+                if (COUNT && L != INVALID && qin[r].idx == (uint32_t)RTBVH_DEBUG_PIXEL)
+                    printf("DBG %d leaf %x sp %d kb %.6g key %.6g\n", (int)CERT, L, sp, kb, key_t(key));
+#endif
                 if (L != INVALID) {   // branch-free test (the same accept predicate), u64 key minimum
                     const uint32_t j = L & ~LEAF_BIT;
                     const v4f* lr = reinterpret_cast<const v4f*>(leaf + 4 * (size_t)j);
