@@ -232,6 +232,8 @@ void rtbvh_destroy(rtbvh_ctx* ctx);
 /* Last error message of this context (or of the last failed rtbvh_create when ctx == NULL). */
 const char* rtbvh_last_error(const rtbvh_ctx* ctx);
 int rtbvh_abi_version(void);
+/* sizeof(rtbvh_stats) as this library was built: a binding checks its mirror of the struct against it */
+uint32_t rtbvh_stats_size(void);
 
 /* ---- inputs (the binding contract, RayTraceGlobal.hlsl:87-120) ------------ */
 /* SRV t0 verts, t1 indices, t2 matIndices, t3 materials, t4.. textures:

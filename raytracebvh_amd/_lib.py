@@ -30,7 +30,7 @@ FLAG_GRAPH = 1 << 20    # compute_bvh replays a captured hipGraph of the frame
 
 # every symbol include/rtbvh.h declares (tests check the library exports them all)
 EXPORTS = [
-    "rtbvh_config_default", "rtbvh_create", "rtbvh_destroy", "rtbvh_last_error", "rtbvh_abi_version",
+    "rtbvh_config_default", "rtbvh_create", "rtbvh_destroy", "rtbvh_last_error", "rtbvh_abi_version", "rtbvh_stats_size",
     "rtbvh_set_scene", "rtbvh_set_camera", "rtbvh_build", "rtbvh_build_async", "rtbvh_trace",
     "rtbvh_trace_async", "rtbvh_compute_bvh", "rtbvh_trace_band_async", "rtbvh_band_rows", "rtbvh_verify_walk",
     "rtbvh_deal_bands", "rtbvh_deal_rows", "rtbvh_set_band_deal",
@@ -124,6 +124,7 @@ def lib() -> ctypes.CDLL:
         "rtbvh_destroy": (None, [vp]),
         "rtbvh_last_error": (ctypes.c_char_p, [vp]),
         "rtbvh_abi_version": (i32, []),
+        "rtbvh_stats_size": (ctypes.c_uint32, []),
         "rtbvh_set_scene": (i32, [vp, vp, u32, vp, u32, vp, vp, u32, vp, u32]),
         "rtbvh_set_camera": (i32, [vp, vp, vp]),
         "rtbvh_build": (i32, [vp]),

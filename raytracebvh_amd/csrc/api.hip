@@ -863,6 +863,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
 extern "C" {
 
 int rtbvh_abi_version(void) { return RTBVH_ABI_VERSION; }
+uint32_t rtbvh_stats_size(void) { return (uint32_t)sizeof(rtbvh_stats); }
 
 void rtbvh_config_default(rtbvh_config* cfg) {
     if (!cfg) return;

@@ -1,6 +1,7 @@
 """CPU-only checks of librtbvh.so: it loads, exports every symbol include/rtbvh.h
 declares, and its host-side pieces (OBJ loader, synthetic generator, camera,
 band split) agree with independent restatements.  No compute call needs a GPU."""
+import ctypes
 import os
 import re
 
@@ -26,6 +27,12 @@ def test_library_exports_every_header_symbol():
 
 def test_layout_sizes():
     assert rt.NODE_DTYPE.itemsize == 44 and rt.MATERIAL_DTYPE.itemsize == 68
+
+
+def test_stats_mirror_matches_the_library():
+    # the ctypes mirror of rtbvh_stats against the struct the library was built with (a field added on one
+    # side only would shift every field after it)
+    assert ctypes.sizeof(_lib.Stats) == rt.lib().rtbvh_stats_size()
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference/Obj"), reason="reference not mounted")
