@@ -1380,6 +1380,23 @@ __device__ __forceinline__ bool qbox_fast(const QAxis& x, const QAxis& y, const 
     return 0 <= mx && mn <= mx && (!hit || mn <= best);
 }
 
+// The certified walk's box test: qbox_fast, and the box's stack key.  After the first bound the key is the
+// entry (of the box grown by rr, qaxis<true>).  Before it (best +inf: nothing pruned by distance, rr = 0)
+// it is the entry of the box grown by rho(t_e), t_e its margin-free entry (`mg`: the margin): pops compare
+// a key with later, finite bounds kb, and for kb <= t_e, rho(kb) <= rho(t_e), so the key is at most the
+// entry of the box grown by rho(kb) -- a box the certified walk must visit (that entry <= kb) keeps
+// key <= kb; for kb > t_e the key (<= t_e) is kept anyway, the margin-free entry being below the bound.
+// The grown entry is the max over axes of near - rho |1/d| (branch-free: rho = 0 after the first bound).
+__device__ __forceinline__ bool qbox_fast_cert(const QAxis& x, const QAxis& y, const QAxis& z, int c, float best,
+                                               const MtMargin& mg, f3 ainv, float& key) {
+    const float nx = qt(x.nw, c, x.b, x.an), ny = qt(y.nw, c, y.b, y.an), nz = qt(z.nw, c, z.b, z.an);
+    const float mn = fmaxf(fmaxf(nx, ny), nz);
+    const float mx = fminf(fminf(qt(x.fw, c, x.b, x.af), qt(y.fw, c, y.b, y.af)), qt(z.fw, c, z.b, z.af));
+    const float rb = best == __builtin_inff() ? fmaf(mg.r1, fmaxf(mn, 0.f), mg.r0) : 0.f;
+    key = fmaxf(fmaxf(fmaf(-rb, ainv.x, nx), fmaf(-rb, ainv.y, ny)), fmaf(-rb, ainv.z, nz));
+    return 0 <= mx && mn <= mx && mn <= best;
+}
+
 // A/B builds only (not certified): 1 = no margin (the unchecked walk's pruning inside the certified
 // code), 2 = the margin's range taken as unbounded
 #ifndef RTBVH_CERT_AB
@@ -1465,10 +1482,18 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                 const QAxis X = qaxis<CERT>(ox, sx, lx, hx, o.x, inv.x, rr),
                             Y = qaxis<CERT>(oy, sy, ly, hy, o.y, inv.y, rr),
                             Z = qaxis<CERT>(oz, sz, lz, hz, o.z, inv.z, rr);
-                h0 = qbox_fast(X, Y, Z, 0, true, kbb, t0);
-                h1 = qbox_fast(X, Y, Z, 1, true, kbb, t1);
-                h2 = qbox_fast(X, Y, Z, 2, true, kbb, t2);
-                h3 = qbox_fast(X, Y, Z, 3, true, kbb, t3);
+                if (CERT) {
+                    const f3 ai = mk(fabsf(inv.x), fabsf(inv.y), fabsf(inv.z));
+                    h0 = qbox_fast_cert(X, Y, Z, 0, kbb, mg, ai, t0);
+                    h1 = qbox_fast_cert(X, Y, Z, 1, kbb, mg, ai, t1);
+                    h2 = qbox_fast_cert(X, Y, Z, 2, kbb, mg, ai, t2);
+                    h3 = qbox_fast_cert(X, Y, Z, 3, kbb, mg, ai, t3);
+                } else {
+                    h0 = qbox_fast(X, Y, Z, 0, true, kbb, t0);
+                    h1 = qbox_fast(X, Y, Z, 1, true, kbb, t1);
+                    h2 = qbox_fast(X, Y, Z, 2, true, kbb, t2);
+                    h3 = qbox_fast(X, Y, Z, 3, true, kbb, t3);
+                }
             } else {
     #define RTBVH_QBOX(c, t)                                                                                      \
 ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
@@ -1626,24 +1651,8 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     if (CERT) {   // the pruning bound and the margin of the new best
                         const float tk = key_t(key);
                         const bool cov = RTBVH_CERT_AB == 2 || tk <= mg.tcap;
-                        const float kbn = cov || RTBVH_CERT_AB == 1 ? tk : __builtin_inff();
+                        kb = cov || RTBVH_CERT_AB == 1 ? tk : __builtin_inff();
                         rr = cov && RTBVH_CERT_AB != 1 ? fmaf(mg.r1, tk, mg.r0) : 0.f;
-                        if (kb == __builtin_inff() && kbn != __builtin_inff() && RTBVH_CERT_AB != 1) {
-                            // the first finite bound: the stacked entries' distances were taken without a
-                            // margin (nothing was pruned by distance before), and from now on the pops
-                            // compare them with the bound -- lower each to a bound on its box's entry grown
-                            // by rr (max over axes of near - rr |1/d| >= entry - rr max |1/d|)
-                            const float dm = rr * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
-                            for (int s2 = 0; s2 < sp; s2++) {
-                                if (s2 < SW) {
-                                    s_wt[s2][tid] = bf16_down(bf16_up(s_wt[s2][tid]) - dm);
-                                } else {
-                                    uint2& e = wstack[s2 - SW];
-                                    e.y = __float_as_uint(__uint_as_float(e.y) - dm);
-                                }
-                            }
-                        }
-                        kb = kbn;
                     }
                 }
                 if (!done && node == INVALID) {   // pop, dropping entries that cannot improve
