@@ -405,7 +405,14 @@ def main():
              "nearest-first-wide": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH,
              "nearest-first-wide-binned": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH | rt.FLAG_BINNED_PRIMARY,
              "certified": rt.FLAG_CERTIFIED}
-    res = {m: timed(f) for m, f in modes.items()}
+    # two interleaved rounds over the modes, each mode's faster kept (one slow moment on the box -- seen
+    # as a 15% swing of one mode in one round -- would otherwise pick the headline mode)
+    res = {}
+    for _ in range(2):
+        for m, f in modes.items():
+            r = timed(f)
+            if m not in res or r["ms_step"] < res[m]["ms_step"]:
+                res[m] = r
     ref = res["reference-order"]
     traversal = {"frames_identical": {}}
     use_name = "reference-order"
