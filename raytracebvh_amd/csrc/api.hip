@@ -72,6 +72,7 @@ struct rtbvh_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
     bool pseudo_ok = false;      // the built tree has its leaf pseudo-records (read by the packet walks only)
+    bool qnode_ok = false;       // the built tree has its QNodes (read by the 4-wide bounce walk only)
     // rtbvh_compute_bvh: the build leaves its crossing nodes (launch_refit_tail) to the frame's binned
     // pass, which runs them in its bin launches (launch_pb_bin_tail); any other first use of the tree
     // runs them first (flush_tail)
@@ -691,6 +692,14 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
+    if (!c->qnode_ok && bounces > 0 && wk.refill && wk.bounce == BounceWalk::WIDE_QUANTIZED) {
+        // a 4-wide bounce walk over a one-workgroup build that quantized no nodes (the context's
+        // walks took none): k_qnodes now, as for the pseudo-records below
+        launch_qnodes(build_args(c), c->stream);
+        c->qnode_ok = true;
+        if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
+        if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+    }
     if (!c->pseudo_ok && (pkind == PrimaryKind::PACKET_REFERENCE || pkind == PrimaryKind::PACKET_NEAREST ||
                           pkind == PrimaryKind::PACKET_WIDE)) {
         // a packet walk over a tree built without the leaf pseudo-records (the context's walks took
@@ -1110,7 +1119,9 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         a.sorted_vals = c->d_va;
         a.pseudo = 1;   // (the one-workgroup build writes them anyway)
         launch_build_small(a, s);
-        launch_qnodes(a, s);
+        // the QNodes only for walks that read them (the 4-wide bounce walk; enqueue_walks otherwise)
+        c->qnode_ok = (c->cfg.flags & (RTBVH_FLAG_WIDE_BVH | RTBVH_FLAG_CERTIFIED)) != 0 || auto_checked(c);
+        if (c->qnode_ok) launch_qnodes(a, s);
         c->leaf_pending = false;
         c->tail_pending = false;
         c->pseudo_ok = true;
@@ -1135,6 +1146,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     // after the leaves (ev_leaf)
     launch_refit_leaves(a, s);
     c->pseudo_ok = a.pseudo != 0;
+    c->qnode_ok = true;   // (quantized by the refit kernels)
     c->leaf_pending = false;
     if (c->leaf_want) {
         if (!c->side) {   // high priority: its workgroups go first while the crossing nodes' fill the CUs
@@ -1584,6 +1596,10 @@ rtbvh_status rtbvh_read_qnodes(rtbvh_ctx* c, uint32_t* out, uint64_t capacity) {
     const size_t total = c->T > 1 ? 2 * (size_t)c->T - 1 : 0;
     if (capacity < total) return fail(c, RTBVH_ERR_INVALID_ARG, "read_qnodes: capacity < 2n-1");
     HIPC(c, hipSetDevice(c->cfg.device));
+    if (!c->qnode_ok) {
+        launch_qnodes(build_args(c), c->stream);
+        c->qnode_ok = true;
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     if (total) HIPC(c, hipMemcpy(out, c->d_qnode, total * sizeof(QNode), hipMemcpyDeviceToHost));
     return RTBVH_OK;

@@ -269,8 +269,7 @@ __device__ __forceinline__ uint32_t leaf_tri_word(uint32_t t, f3 lo, f3 hi) {
 // leaf record of sorted position i: gather the clip-space triangle once, store
 // (v0, e1, e2) for the triangle test (the reference's edge1/edge2, :43-44) and
 // the leaf AABB (MortonCodes.hlsl:87-96: min/max of v0, v1, v2 in that order)
-__device__ __forceinline__ void leaf_record_words(const BuildArgs& a, uint32_t i, f3& lo, f3& hi, float4 (&r)[4]) {
-    const uint32_t t = a.sorted_vals[i];
+__device__ __forceinline__ void leaf_record_words_of(const BuildArgs& a, uint32_t t, f3& lo, f3& hi, float4 (&r)[4]) {
     const float4* src = a.tclip + TCS * (size_t)t;
     const float4 s0 = src[0], s1 = src[1], s2 = src[2];
     const f3 v0 = mk(s0.x, s0.y, s0.z), v1 = mk(s1.x, s1.y, s1.z), v2 = mk(s2.x, s2.y, s2.z);
@@ -283,6 +282,9 @@ __device__ __forceinline__ void leaf_record_words(const BuildArgs& a, uint32_t i
     r[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
     r[2] = make_float4(e2.z, __uint_as_float(leaf_tri_word(t, lo, hi)), lo.x, lo.y);
     r[3] = make_float4(lo.z, hi.x, hi.y, hi.z);
+}
+__device__ __forceinline__ void leaf_record_words(const BuildArgs& a, uint32_t i, f3& lo, f3& hi, float4 (&r)[4]) {
+    leaf_record_words_of(a, a.sorted_vals[i], lo, hi, r);
 }
 // 64-B records of consecutive indices, one per lane, written with every store instruction of
 // the wave covering 1 KB contiguously (16 B per lane): each half-wave's records are staged in
@@ -984,12 +986,19 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
 // buffers), so every later kernel and export is unchanged.
 constexpr uint32_t SMALL_BLOCK = 1024;
 constexpr uint32_t SMALL_T = 2048;
+static_assert(SMALL_T == 2 * SMALL_BLOCK, "k_build_small: two keys / leaves per thread");
 
 struct LdsCodes {   // sorted code j = the high word of the sorted 64-bit key
     const uint64_t* kv;
     __device__ uint32_t operator[](int32_t j) const { return (uint32_t)(kv[j] >> 32); }
 };
 
+// RTBVH_SMALL_PROBE (A/B builds only): thread 0 prints the constant-rate clock at the phase ends
+#ifdef RTBVH_SMALL_PROBE
+#define SMALL_MARK(k) do { __syncthreads(); if (tid == 0) tmark[k] = wall_clock64(); } while (0)
+#else
+#define SMALL_MARK(k) do { } while (0)
+#endif
 template <int MODE>
 __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32_t* __restrict__ sk,
                                                              uint32_t* __restrict__ sv) {
@@ -1002,6 +1011,10 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
     __shared__ float s_red[16 * 6];
     __shared__ uint32_t s_emax;             // the largest leaf edge bound (rootbox[8], margin.h)
     const uint32_t tid = threadIdx.x, T = a.T;
+#ifdef RTBVH_SMALL_PROBE
+    uint64_t tmark[7];
+#endif
+    SMALL_MARK(0);
     for (uint32_t k = tid; k < SMALL_T; k += SMALL_BLOCK) s_cnt[k] = 0;
     if (a.morton_mode == 0) {   // k_bounds + k_bounds_final as one reduction
         f3 mn = mk(INFINITY, INFINITY, INFINITY), mx = mk(-INFINITY, -INFINITY, -INFINITY);
@@ -1035,44 +1048,94 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
         }
         __syncthreads();   // morton_tri reads the box back (same workgroup: visible)
     }
-    uint32_t n = 1;
-    while (n < T) n <<= 1;
-    for (uint32_t t = tid; t < n; t += SMALL_BLOCK)
-        s_kv[t] = t < T ? ((uint64_t)morton_tri(a, t) << 32 | t) : ~0ull;
-    __syncthreads();
-    for (uint32_t k = 2; k <= n; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = tid; i < n; i += SMALL_BLOCK) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const uint64_t x = s_kv[i], y = s_kv[l];
-                    if ((x > y) == ((i & k) == 0)) { s_kv[i] = y; s_kv[l] = x; }
-                }
-            }
+    SMALL_MARK(1);
+    // the bitonic network over all SMALL_T keys (padding ~0: above every key), thread tid holding
+    // keys 2 tid and 2 tid + 1 in registers: the compare-exchanges at distance j < 128 are within
+    // the wave (j = 1 in the thread, 2..64 across lanes tid ^ j/2), only j >= 128 goes through LDS
+    // with a barrier per step (10 of the 66 steps; all through LDS: 26 us of the 79)
+    uint64_t e[2];
+#pragma unroll
+    for (uint32_t b = 0; b < 2; b++) {
+        const uint32_t t = 2 * tid + b;
+        e[b] = t < T ? ((uint64_t)morton_tri(a, t) << 32 | t) : ~0ull;
+    }
+    SMALL_MARK(2);
+    for (uint32_t k = 2; k <= SMALL_T; k <<= 1) {
+        uint32_t j = k >> 1;
+        if (j >= 128) {
+            s_kv[2 * tid] = e[0];
+            s_kv[2 * tid + 1] = e[1];
             __syncthreads();
+            for (; j >= 128; j >>= 1) {
+                // pair tid: index i with bit j clear (tid with a 0 inserted at bit j) and i | j
+                const uint32_t i = ((tid & ~(j - 1)) << 1) | (tid & (j - 1)), l = i | j;
+                const uint64_t x = s_kv[i], y = s_kv[l];
+                const bool up = (i & k) == 0, lt = x < y;
+                s_kv[i] = up == lt ? x : y;
+                s_kv[l] = up == lt ? y : x;
+                __syncthreads();
+            }
+            e[0] = s_kv[2 * tid];
+            e[1] = s_kv[2 * tid + 1];
+        }
+        for (; j >= 2; j >>= 1) {
+            const uint32_t m = j >> 1;   // partner lane distance
+#pragma unroll
+            for (uint32_t b = 0; b < 2; b++) {
+                const uint32_t i = 2 * tid + b;
+                const uint64_t x = e[b];
+                const uint32_t ylo = (uint32_t)__shfl_xor((int)(uint32_t)x, (int)m, 64);
+                const uint32_t yhi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), (int)m, 64);
+                const uint64_t y = (uint64_t)yhi << 32 | ylo;
+                const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                e[b] = keep_min == (x < y) ? x : y;
+            }
+        }
+        const bool up = ((2 * tid) & k) == 0;   // j = 1: the thread's own pair
+        const bool sw = up != (e[0] < e[1]);
+        const uint64_t x0 = e[0];
+        e[0] = sw ? e[1] : x0;
+        e[1] = sw ? x0 : e[1];
+    }
+    s_kv[2 * tid] = e[0];
+    s_kv[2 * tid + 1] = e[1];
+    SMALL_MARK(3);
+#pragma unroll
+    for (uint32_t b = 0; b < 2; b++) {
+        const uint32_t i = 2 * tid + b;
+        if (i < T) {
+            sk[i] = (uint32_t)(e[b] >> 32);
+            sv[i] = (uint32_t)e[b];
         }
     }
-    for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
-        sk[i] = (uint32_t)(s_kv[i] >> 32);
-        sv[i] = (uint32_t)s_kv[i];
-    }
-    __syncthreads();   // sorted ids (leaf_record) and clip triangles visible to the block
+    __syncthreads();   // sorted keys in LDS; clip triangles visible to the block
     const LdsCodes codes{s_kv};
     if (tid == 0) s_emax = 0u;
     __syncthreads();
-    for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
-        f3 lo, hi;
-        float4 r[4];
-        leaf_record_words(a, i, lo, hi, r);
-        float4* dst = a.leaf + 4 * (size_t)i;
-        dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2]; dst[3] = r[3];
-        float em, zkey;
-        leaf_margin(r, lo.z, hi.z, em, zkey);
-        a.lfp[i] = leaf_footprint(lo, hi, zkey);
-        atomicMax(&s_emax, __float_as_uint(em));   // (non-negative floats order as their bits)
-        if (i + 1 < T) karras_node<MODE>(codes, T, i, a.topo, a.pleaf, a.pint);
+    // leaves i = tid, tid + SMALL_BLOCK: records, margins, Karras nodes; the boxes stay in registers
+    // for the refit (the triangle id from the sorted key in LDS)
+    f3 llo[2], lhi[2];
+#pragma unroll
+    for (uint32_t b = 0; b < 2; b++) {
+        const uint32_t i = tid + b * SMALL_BLOCK;
+        llo[b] = lhi[b] = mk(0.f, 0.f, 0.f);
+        if (i < T) {
+            f3 lo, hi;
+            float4 r[4];
+            leaf_record_words_of(a, (uint32_t)s_kv[i], lo, hi, r);
+            float4* dst = a.leaf + 4 * (size_t)i;
+            dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2]; dst[3] = r[3];
+            float em, zkey;
+            leaf_margin(r, lo.z, hi.z, em, zkey);
+            a.lfp[i] = leaf_footprint(lo, hi, zkey);
+            atomicMax(&s_emax, __float_as_uint(em));   // (non-negative floats order as their bits)
+            if (i + 1 < T) karras_node<MODE>(codes, T, i, a.topo, a.pleaf, a.pint);
+            llo[b] = lo;
+            lhi[b] = hi;
+        }
     }
     if (tid == 0 && T > 1) a.pint[0] = INVALID;
+    SMALL_MARK(4);
     __syncthreads();   // links written by other threads: copy them into LDS
     if (tid == 0) a.rootbox[8] = __uint_as_float(s_emax);
     for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
@@ -1084,10 +1147,15 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < T; i += SMALL_BLOCK) {
-        const float4* r = a.leaf + 4 * (size_t)i;
-        const float4 b0 = r[2], b1 = r[3];
-        f3 lo = mk(b0.z, b0.w, b1.x), hi = mk(b1.y, b1.z, b1.w);
+    SMALL_MARK(5);
+    // k_refit's in-block protocol, in LDS only: the second arriver at a node unites the two child
+    // boxes (left first, as k_refit) and climbs on; the node records are written afterwards, one
+    // thread per node (a store per level kept the climb's chain waiting on the store queue)
+#pragma unroll
+    for (uint32_t b = 0; b < 2; b++) {
+        const uint32_t i = tid + b * SMALL_BLOCK;
+        if (i >= T) continue;
+        f3 lo = llo[b], hi = lhi[b];
         if (T == 1) {
             a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
             a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
@@ -1096,7 +1164,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
         }
         uint32_t e = s_pleaf[i];
         store_pseudo_record(a.rec + e, LEAF_BIT | i, lo, hi);
-        for (int level = 0; level < 2 * STACK_SIZE; level++) {   // k_refit's in-block protocol
+        for (int level = 0; level < 2 * STACK_SIZE; level++) {
             const uint32_t p = e >> 1, side = e & 1u;
             float* sb = s_box[p][side];
             sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
@@ -1105,10 +1173,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const float* ob = s_box[p][side ^ 1u];
             const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
-            const uint2 ids = s_ids[p];
             e = s_pint[p];
-            if (side) store_record(a.rec + slot_of(e, T), smin, smax, lo, hi, ids.x, ids.y, p);
-            else      store_record(a.rec + slot_of(e, T), lo, hi, smin, smax, ids.x, ids.y, p);
             if (side) { lo = vmin(smin, lo); hi = vmax(smax, hi); }
             else      { lo = vmin(lo, smin); hi = vmax(hi, smax); }
             if (e == INVALID) {
@@ -1119,6 +1184,22 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
             }
         }
     }
+    __syncthreads();   // every node's two child boxes in LDS
+    for (uint32_t p = tid; p + 1 < T; p += SMALL_BLOCK) {
+        const float* l = s_box[p][0];
+        const float* r = s_box[p][1];
+        const uint2 ids = s_ids[p];
+        store_record(a.rec + slot_of(s_pint[p], T), mk(l[0], l[1], l[2]), mk(l[3], l[4], l[5]), mk(r[0], r[1], r[2]),
+                     mk(r[3], r[4], r[5]), ids.x, ids.y, p);
+    }
+#ifdef RTBVH_SMALL_PROBE
+    SMALL_MARK(6);
+    if (tid == 0)
+        printf("SMALLPROBE T=%u bounds %llu morton %llu sort %llu leaves+karras %llu links %llu refit %llu (x10ns)\n", T,
+               (unsigned long long)(tmark[1] - tmark[0]), (unsigned long long)(tmark[2] - tmark[1]),
+               (unsigned long long)(tmark[3] - tmark[2]), (unsigned long long)(tmark[4] - tmark[3]),
+               (unsigned long long)(tmark[5] - tmark[4]), (unsigned long long)(tmark[6] - tmark[5]));
+#endif
 }
 
 // reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k
