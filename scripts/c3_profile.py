@@ -20,7 +20,8 @@ def main():
     # C3_MODE: the walks (default AUTO_WALK: the reference order's plain kernels at this size); "fast": the
     # reference order's packet primary + refill bounce kernels; "certified": the certified fast walks
     walk = {"auto": rt.FLAG_AUTO_WALK, "fast": rt.FLAG_PACKET_PRIMARY | rt.FLAG_REFILL_BOUNCE,
-            "certified": rt.FLAG_CERTIFIED, "plain": 0}[os.environ.get("C3_MODE", "auto")]
+            "certified": rt.FLAG_CERTIFIED, "plain": 0, "sort": rt.FLAG_SORT_BOUNCE,
+            "packet+sort": rt.FLAG_PACKET_PRIMARY | rt.FLAG_SORT_BOUNCE}[os.environ.get("C3_MODE", "auto")]
     # C3_SCENE=Image_Test C3_BOUNCES=0: C2
     scene = rt.load_npz(os.path.join(REPO, "tests", "golden", "scenes", os.environ.get("C3_SCENE", "Test") + ".npz"))
     B = int(os.environ.get("C3_BOUNCES", "1"))
