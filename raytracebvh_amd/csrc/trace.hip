@@ -109,9 +109,16 @@ __device__ __forceinline__ bool ray_box_xy(f3 o, f3 inv, f2v lo, f2v hi, float l
 // the stack is cached in a register (`top`), so a pop hands over the next node at
 // once and refills `top` from scratch in the background.  Returns hit;
 // best_leaf = sorted leaf index.  `limit` <= STACK_SIZE entries.
-template <bool COUNT, bool NEAREST>
+// LSB > 0: stack entries [0, LSB) in LDS (`lst`: this lane's column, entry k at lst[k * BLOCK]; a
+// wave's lanes on 64 distinct banks), deeper ones in scratch (the one-ray-per-lane kernels)
+#ifndef RTBVH_LANE_LSB
+#define RTBVH_LANE_LSB 16
+#endif
+constexpr int LANE_LSB = RTBVH_LANE_LSB;
+template <bool COUNT, bool NEAREST, int LSB = 0>
 __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const float4* __restrict__ leaf, uint32_t T,
-                                         f3 o, f3 d, f3 inv, int limit, float& best, uint32_t& best_leaf, Counts& c) {
+                                         f3 o, f3 d, f3 inv, int limit, float& best, uint32_t& best_leaf, Counts& c,
+                                         uint32_t* lst = nullptr) {
     bool hit = false;
     best = 0.f;
     best_leaf = 0;
@@ -136,7 +143,7 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
                 hit = true;
             }
             node = top;                                 // pop
-            if (--sp >= 0) top = stack[sp];
+            if (--sp >= 0) top = LSB > 0 && sp < LSB ? lst[sp * BLOCK] : stack[sp];
             continue;
         }
         if (COUNT) c.internal++;
@@ -149,17 +156,19 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
         const bool rh = ray_box_xy(o, inv, q1.xy, q1.zw, q2.z, q2.w, hit, best, tr);
         if (!lh && !rh) {
             node = top;                                 // pop
-            if (--sp >= 0) top = stack[sp];
+            if (--sp >= 0) top = LSB > 0 && sp < LSB ? lst[sp * BLOCK] : stack[sp];
         } else {
             const bool swap = NEAREST && lh && rh && tr < tl;
             if (lh && rh) {
                 if (sp + 1 >= limit) {
                     c.overflow++;
                     node = top;
-                    if (--sp >= 0) top = stack[sp];
+                    if (--sp >= 0) top = LSB > 0 && sp < LSB ? lst[sp * BLOCK] : stack[sp];
                     continue;
                 }
-                stack[sp++] = top;                      // push the second child
+                if (LSB > 0 && sp < LSB) lst[sp * BLOCK] = top;   // push the second child
+                else stack[sp] = top;
+                sp++;
                 top = swap ? cl : cr;
             }
             node = swap ? cr : (lh ? cl : cr);
@@ -735,6 +744,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     const int lim = LIM ? a.stack_limit : STACK_SIZE, lim4 = LIM ? a.stack_limit4 : STACK4;
     constexpr int PST = PW::WIDE ? 3 * (STACK4 + 1) : 3 * STACK_SIZE;   // per-wave packet stack words (+ sentinel)
     __shared__ uint32_t s_pst[PW::PACKET ? 4 * PST : 1];
+    __shared__ uint32_t s_lst[PW::PACKET || LANE_LSB == 0 ? 1 : LANE_LSB * BLOCK];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t k = a.band0 + blockIdx.y * a.bstep;   // the rank's k-th band
@@ -762,7 +772,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
         phit = traverse_packet<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, valid, lim, best, bl, c,
                                                    s_pst + w * PST);
     if (valid) {
-        const bool h = PW::PACKET ? phit : traverse<COUNT, PW::NEAREST>(a.inner, a.leaf, a.T, o, d, inv, lim, best, bl, c);
+        const bool h = PW::PACKET ? phit
+                                  : traverse<COUNT, PW::NEAREST, PW::PACKET ? 0 : LANE_LSB>(a.inner, a.leaf, a.T, o, d, inv, lim,
+                                                                                           best, bl, c, s_lst + threadIdx.x);
         live = primary_pixel(a, out, o, d, h, best, bl, hits, tex, e);
     }
     const uint32_t slot = wave_append(emit && live, qcount);
@@ -1217,6 +1229,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __
                                                      const uint32_t* __restrict__ qin_count,
                                                      const uint32_t* __restrict__ perm, RayQ* __restrict__ qout,
                                                      uint32_t* __restrict__ qout_count, int emit) {
+    __shared__ uint32_t s_lst[LANE_LSB == 0 ? 1 : LANE_LSB * BLOCK];
     const uint32_t n = *qin_count;
     Counts c = {0, 0, 0, 0, 0};
     uint32_t hits = 0, tex = 0;
@@ -1232,8 +1245,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __
             uint32_t bl;
             float4 col = a.color[e.idx];
             float intensity = e.intensity;
-            if (traverse<COUNT, NEAREST>(a.inner, a.leaf, a.T, o, d, inv, LIM ? a.stack_limit : STACK_SIZE, best, bl,
-                                         c)) {
+            if (traverse<COUNT, NEAREST, LANE_LSB>(a.inner, a.leaf, a.T, o, d, inv, LIM ? a.stack_limit : STACK_SIZE,
+                                                   best, bl, c, s_lst + threadIdx.x)) {
                 hits++;
                 const HitInfo h = shade_hit(a, bl, o, d, best);
                 tex += h.textured;
