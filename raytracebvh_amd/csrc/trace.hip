@@ -110,7 +110,9 @@ __device__ __forceinline__ bool ray_box_xy(f3 o, f3 inv, f2v lo, f2v hi, float l
 // once and refills `top` from scratch in the background.  Returns hit;
 // best_leaf = sorted leaf index.  `limit` <= STACK_SIZE entries.
 // LSB > 0: stack entries [0, LSB) in LDS (`lst`: this lane's column, entry k at lst[k * BLOCK]; a
-// wave's lanes on 64 distinct banks), deeper ones in scratch (the one-ray-per-lane kernels)
+// wave's lanes on 64 distinct banks), deeper ones in scratch (the one-ray-per-lane kernels).  The pop
+// compiles to one flat load of a selected pointer (LDS or scratch); forcing ds_read (a module-scope
+// array, every lane reading LDS and the deeper ones scratch as well) was 1-2% slower at C3
 #ifndef RTBVH_LANE_LSB
 #define RTBVH_LANE_LSB 16
 #endif
@@ -1245,8 +1247,18 @@ __global__ __launch_bounds__(BLOCK, 8) void k_bounce(TraceArgs a, const RayQ* __
             uint32_t bl;
             float4 col = a.color[e.idx];
             float intensity = e.intensity;
+#ifdef RTBVH_BOUNCE_PROBE   // cost probes (A/B builds, wrong frames): 1 no walk (every ray misses), 2 no shading
+            const bool th = RTBVH_BOUNCE_PROBE == 1 ? false
+                                                    : traverse<COUNT, NEAREST, LANE_LSB>(a.inner, a.leaf, a.T, o, d, inv,
+                                                          LIM ? a.stack_limit : STACK_SIZE, best, bl, c, s_lst + threadIdx.x);
+            if (RTBVH_BOUNCE_PROBE == 2 && th) {
+                hits++;
+                col = make_float4(best, (float)bl, 0.f, 1.f);
+            } else if (th) {
+#else
             if (traverse<COUNT, NEAREST, LANE_LSB>(a.inner, a.leaf, a.T, o, d, inv, LIM ? a.stack_limit : STACK_SIZE,
                                                    best, bl, c, s_lst + threadIdx.x)) {
+#endif
                 hits++;
                 const HitInfo h = shade_hit(a, bl, o, d, best);
                 tex += h.textured;
