@@ -25,10 +25,11 @@ interaction, the eye orbiting by Graphics::onKeyDown every frame ("c5_orbit": re
 camera per frame under RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_GRAPH, frames checked against the reference
 order; beside it the same cameras' frames with the eye standing still, and the C5 camera under the
 same flags).  value = all rays of the frame (W*H primary + every live bounce ray, summed over ranks) /
-max-over-ranks time per step.  The reported traversal is the fastest mode whose frame is identical to
-the reference order's in this run (checked every run), or the certified walk of RTBVH_FLAG_AUTO_WALK
-(DESIGN.md 3: the reference-order frame by construction, per-ray certificates) when within 2% of it;
-the certified mode's rate is at the line's top level either way (certified_mrays_s).
+max-over-ranks time per step.  The reported traversal is the drop-in's own mode: the certified walks of
+RTBVH_FLAG_AUTO_WALK (RTBVH_FLAG_CERTIFIED; DESIGN.md 3: the reference-order frame by construction,
+per-ray certificates), its frame checked against the reference order's in this run; the unchecked
+walks (exact only when their frame matches, which is checked per run) are reported beside it
+(traversal.fastest_identical_*).  Each mode is timed in three interleaved rounds, the median kept.
 
 Parity at the headline size (N = 1, rank 0, inside the cpu_baseline leg): the oracle builds
 its own tree of the same 10M triangles (compared with the GPU tree field by field) and traces
@@ -405,14 +406,13 @@ def main():
              "nearest-first-wide": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH,
              "nearest-first-wide-binned": FAST | rt.FLAG_NEAREST_FIRST | rt.FLAG_WIDE_BVH | rt.FLAG_BINNED_PRIMARY,
              "certified": rt.FLAG_CERTIFIED}
-    # two interleaved rounds over the modes, each mode's faster kept (one slow moment on the box -- seen
-    # as a 15% swing of one mode in one round -- would otherwise pick the headline mode)
-    res = {}
-    for _ in range(2):
+    # three interleaved rounds over the modes, each mode's median run kept (one slow moment on the box --
+    # seen as a 15% swing of one mode in one round -- moves no number)
+    runs = {m: [] for m in modes}
+    for _ in range(3):
         for m, f in modes.items():
-            r = timed(f)
-            if m not in res or r["ms_step"] < res[m]["ms_step"]:
-                res[m] = r
+            runs[m].append(timed(f))
+    res = {m: sorted(rs, key=lambda r: r["ms_step"])[len(rs) // 2] for m, rs in runs.items()}
     ref = res["reference-order"]
     traversal = {"frames_identical": {}}
     use_name = "reference-order"
@@ -429,15 +429,19 @@ def main():
         traversal["frames_identical"][m] = ident
         if ident and args.traversal != "reference" and r["ms_step"] < res[use_name]["ms_step"]:
             use_name = m
-    # the headline: the fastest mode whose frame equals the reference order's in this run (checked above on
-    # every rank's bands), the certified mode (RTBVH_FLAG_AUTO_WALK's: the reference frame by construction,
-    # DESIGN.md 3) when within 2% of it; the certified mode's own rate is reported beside it either way
+    # the headline: the certified mode (RTBVH_FLAG_AUTO_WALK's walks at C5: the reference frame by
+    # construction; its frame checked above against the reference order's). The fastest mode
+    # whose frame equalled the reference order's in this run is reported beside it: the unchecked walks
+    # are exact only when containment holds (tests/containment.py), so they are never the headline.
     traversal["fastest_identical_mode"] = use_name
     traversal["fastest_identical_mrays_s"] = round(res[use_name]["value"], 2)
-    pref = "certified"
-    if use_name != pref and traversal["frames_identical"].get(pref) and args.traversal != "reference" \
-            and res[pref]["ms_step"] <= 1.02 * res[use_name]["ms_step"]:
-        use_name = pref
+    traversal["fastest_identical_ms"] = round(res[use_name]["ms_step"], 4)
+    traversal["runs_ms"] = {m: [round(r["ms_step"], 4) for r in rs] for m, rs in runs.items()}
+    if args.traversal != "reference":
+        use_name = "certified"
+        if not traversal["frames_identical"].get("certified"):   # a bug, never expected: say so loudly
+            log("ERROR: the certified frame differs from the reference order's; reporting the reference order")
+            use_name = "reference-order"
     use = res[use_name]
     traversal["mode"] = use_name
     # each rank's own ms per step before the closing barrier (rank 0 also receives and assembles the

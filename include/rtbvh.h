@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RTBVH_ABI_VERSION 6
+#define RTBVH_ABI_VERSION 7
 
 typedef enum {
     RTBVH_OK = 0,
@@ -208,8 +208,10 @@ typedef struct {
      * wave each) at internal nodes [0] and at leaves [1] */
     uint64_t packet_steps[2];
     /* RTBVH_FLAG_AUTO_WALK: traces run with the certified walks since rtbvh_create, and the rays the last
-     * one re-traced in the reference order (no certificate: redo_rays[0] + redo_rays[1]) */
-    uint64_t walk_checks, walk_fallbacks;
+     * one re-traced in the reference order (no certificate: redo_rays[0] + redo_rays[1]).  ABI 7 renamed
+     * them (ABI <= 5: walk_checks counted device frame checks and walk_fallbacks frame keys that fell back
+     * to the reference order; a re-traced ray is normal, not a wrong fast walk) */
+    uint64_t cert_traces, redo_total;
     /* RTBVH_FLAG_COUNT_VISITS, RTBVH_FLAG_BINNED_PRIMARY: (leaf, screen tile) bin entries of the primary
      * pass [0] and those that passed the tile's 8 x 8-block bound test [1] (one leaf-record fetch each) */
     uint64_t bin_entries[2];

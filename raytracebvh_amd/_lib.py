@@ -80,7 +80,7 @@ class Stats(ctypes.Structure):
                 ("trav_max_steps", ctypes.c_uint64), ("trav_steps_log2", ctypes.c_uint64 * 32),
                 ("graph_captures", ctypes.c_uint64), ("walk_flags", ctypes.c_uint32),
                 ("walk_state", ctypes.c_uint32), ("packet_steps", ctypes.c_uint64 * 2),
-                ("walk_checks", ctypes.c_uint64), ("walk_fallbacks", ctypes.c_uint64),
+                ("cert_traces", ctypes.c_uint64), ("redo_total", ctypes.c_uint64),
                 ("bin_entries", ctypes.c_uint64 * 2), ("redo_rays", ctypes.c_uint64 * 2),
                 ("trav_longest", ctypes.c_uint64)]
 

@@ -151,7 +151,7 @@ struct rtbvh_ctx {
     // set, the list of rays a pass re-traces in the reference order (their counts: d_qcount 16..31)
     uint32_t* d_redo[MAXSPLIT] = {};
     size_t cap_redo[MAXSPLIT] = {};
-    uint64_t walk_checks = 0;                         // certified traces so far
+    uint64_t cert_traces = 0;                         // certified traces so far
     uint32_t last_walk = 0;                           // walk flags of the last trace
     uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
     bool last_cert = false;                           // the last trace was certified (its re-trace counts)
@@ -165,6 +165,8 @@ struct rtbvh_ctx {
         uint32_t H, nranks, share;
         uint32_t* d;
         std::vector<uint32_t> off;   // rank r's bands at d[off[r] .. off[r + 1])
+        uint32_t* h;                 // its pinned staging copy (the upload is asynchronous; freed with d)
+        hipEvent_t ready;            // recorded after the upload on the context stream
     };
     std::deque<DealTab> deals;       // the MAX_DEALS most recently used (H, nranks, share), most recent first
     static constexpr size_t MAX_DEALS = 8;
@@ -405,9 +407,18 @@ uint32_t deal_max_rows(uint32_t H, uint32_t nranks, uint32_t share) {
 rtbvh_status sync_all(rtbvh_ctx* c);
 // The device table of a weighted deal (null for round-robin: the kernels compute it).  Uploaded on
 // first use (a few KB, once per frame size and deal), so not from inside a graph capture (whose frames
-// have one rank).  The MAX_DEALS most recently used tables are kept; evicting one first waits for the
-// context's work (traces in flight may read it).
-rtbvh_status get_deal(rtbvh_ctx* c, uint32_t H, uint32_t nranks, const rtbvh_ctx::DealTab** out) {
+// have one rank): an asynchronous copy from pinned staging on the context stream, and an event the
+// caller's stream `s` waits for (a trace on a caller stream, an assembly on another).  The MAX_DEALS
+// most recently used tables are kept; evicting one first waits for the context's work (traces in
+// flight may read it).
+void free_deal(rtbvh_ctx::DealTab& t) {
+    dfree(t.d);
+    if (t.h) (void)hipHostFree(t.h);
+    if (t.ready) (void)hipEventDestroy(t.ready);
+    t.h = nullptr;
+    t.ready = nullptr;
+}
+rtbvh_status get_deal(rtbvh_ctx* c, uint32_t H, uint32_t nranks, const rtbvh_ctx::DealTab** out, hipStream_t s) {
     *out = nullptr;
     if (c->root_share == 16 || nranks <= 1) return RTBVH_OK;
     for (auto it = c->deals.begin(); it != c->deals.end(); ++it)
@@ -418,31 +429,42 @@ rtbvh_status get_deal(rtbvh_ctx* c, uint32_t H, uint32_t nranks, const rtbvh_ctx
                 c->deals.push_front(std::move(t));
             }
             *out = &c->deals.front();
+            if (s != c->stream && !c->capturing) HIPC(c, hipStreamWaitEvent(s, c->deals.front().ready, 0));
             return RTBVH_OK;
         }
     if (c->capturing) return fail(c, RTBVH_ERR_INVALID_ARG, "a new band deal inside a graph capture");
     if (c->deals.size() >= rtbvh_ctx::MAX_DEALS) {
         rtbvh_status st = sync_all(c);
         if (st) return st;
-        dfree(c->deals.back().d);
+        free_deal(c->deals.back());
         c->deals.pop_back();
     }
     std::vector<uint32_t> owner;
     deal_owners(H, nranks, c->root_share, owner);
     const uint32_t nb = (uint32_t)owner.size();
-    rtbvh_ctx::DealTab t{H, nranks, c->root_share, nullptr, std::vector<uint32_t>(nranks + 1, 0)};
-    std::vector<uint32_t> host(2 * (size_t)nb + 1), cnt(nranks, 0);
+    rtbvh_ctx::DealTab t{H, nranks, c->root_share, nullptr, std::vector<uint32_t>(nranks + 1, 0), nullptr, nullptr};
+    const size_t words = 2 * (size_t)nb + 1;
+    std::vector<uint32_t> cnt(nranks, 0);
+    if (hipHostMalloc((void**)&t.h, words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void**)&t.d, words * sizeof(uint32_t)) != hipSuccess ||
+        hipEventCreateWithFlags(&t.ready, hipEventDisableTiming) != hipSuccess) {
+        free_deal(t);
+        return fail(c, RTBVH_ERR_OOM, "band deal table");
+    }
     for (uint32_t b = 0; b < nb; b++) t.off[owner[b] + 1]++;
     for (uint32_t r = 0; r < nranks; r++) t.off[r + 1] += t.off[r];
+    t.h[2 * nb] = 0;
     for (uint32_t b = 0; b < nb; b++) {
         const uint32_t r = owner[b], pos = cnt[r]++;
-        host[t.off[r] + pos] = b;           // rank r's pos-th band
-        host[nb + b] = r << 24 | pos;       // where band b sits (k_assemble)
+        t.h[t.off[r] + pos] = b;           // rank r's pos-th band
+        t.h[nb + b] = r << 24 | pos;       // where band b sits (k_assemble)
     }
-    HIPC(c, hipMalloc((void**)&t.d, host.size() * sizeof(uint32_t)));
-    HIPC(c, hipMemcpy(t.d, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->deals.push_front(std::move(t));
-    *out = &c->deals.front();
+    rtbvh_ctx::DealTab& f = c->deals.front();
+    HIPC(c, hipMemcpyAsync(f.d, f.h, words * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipEventRecord(f.ready, c->stream));
+    if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, f.ready, 0));
+    *out = &f;
     return RTBVH_OK;
 }
 
@@ -633,7 +655,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool timing = timed && (c->cfg.flags & RTBVH_FLAG_TIMING) != 0 && s == c->stream && !c->capturing;
     TraceArgs a = trace_args(c, W, H, rank, nranks, color, inten);
     const rtbvh_ctx::DealTab* deal = nullptr;
-    rtbvh_status dst = get_deal(c, H, nranks, &deal);
+    rtbvh_status dst = get_deal(c, H, nranks, &deal, s);
     if (dst) return dst;
     if (deal) {
         a.my_bands = deal->off[rank + 1] - deal->off[rank];
@@ -863,7 +885,7 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (st) return st;
     const TracePlan p = plan_trace(c, c->cfg.flags);
     c->last_walk_state = p.state;
-    if (p.cert && !c->capturing) c->walk_checks++;
+    if (p.cert && !c->capturing) c->cert_traces++;
     return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, p.flags, true, p.cert);
 }
 
@@ -989,7 +1011,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_ovf);
     for (auto& r : c->d_redo) dfree(r);
     dfree(c->d_cam);
-    for (auto& t : c->deals) dfree(t.d);
+    for (auto& t : c->deals) free_deal(t);
     if (c->h_ovf) (void)hipHostFree(c->h_ovf);
     for (auto& row : c->evb)
         for (auto& e : row)
@@ -1271,7 +1293,7 @@ static rtbvh_status compute_graph(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
     c->last_walk = g.walk;
     c->last_walk_state = g.walk_state;
     c->last_cert = g.cert;
-    if (g.cert) c->walk_checks++;
+    if (g.cert) c->cert_traces++;
     c->rank = 0;
     c->nranks = 1;
     c->last_slot = 0;
@@ -1406,10 +1428,11 @@ rtbvh_status rtbvh_assemble_bands(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t
         return RTBVH_ERR_INVALID_ARG;
     HIPC(c, hipSetDevice(c->cfg.device));
     const rtbvh_ctx::DealTab* deal = nullptr;
-    rtbvh_status st = get_deal(c, H, nranks, &deal);
+    const hipStream_t as = stream ? (hipStream_t)stream : c->stream;
+    rtbvh_status st = get_deal(c, H, nranks, &deal, as);
     if (st) return st;
     launch_assemble((const float4*)dev_bands, deal ? deal->d + (H + 7) / 8 : nullptr, stride_rows, W, H, nranks,
-                    (float4*)dev_frame, stream ? (hipStream_t)stream : c->stream);
+                    (float4*)dev_frame, as);
     return check_launch(c, "assemble bands");
 }
 
@@ -1484,7 +1507,7 @@ rtbvh_status rtbvh_trace_tiles(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bo
     if (e != ncclSuccess) return fail(c, RTBVH_ERR_COMM, std::string("band gather: ") + r.GetErrorString(e));
     if (rank == 0) {
         const rtbvh_ctx::DealTab* deal = nullptr;
-        st = get_deal(c, H, nranks, &deal);
+        st = get_deal(c, H, nranks, &deal, c->stream);
         if (st) return st;
         launch_assemble(c->d_band, deal ? deal->d + (H + 7) / 8 : nullptr, rows0, W, H, nranks, c->d_color,
                         c->stream);
@@ -1706,14 +1729,14 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
     }
     out->walk_flags = c->last_walk;
     out->walk_state = c->last_walk_state;
-    out->walk_checks = c->walk_checks;
+    out->cert_traces = c->cert_traces;
     if (c->traced && c->last_cert && c->d_qcount) {   // the last trace's re-trace counts (d_qcount 16..)
         uint32_t q[32];
         HIPC(c, hipMemcpy(q, c->d_qcount + 32 * c->last_slot, sizeof(q), hipMemcpyDeviceToHost));
         out->redo_rays[0] = q[16];
         for (uint32_t k = 0; k < c->bounces && k < 15; k++) out->redo_rays[1] += q[17 + k];
     }
-    out->walk_fallbacks = out->redo_rays[0] + out->redo_rays[1];
+    out->redo_total = out->redo_rays[0] + out->redo_rays[1];
     return RTBVH_OK;
 }
 

@@ -457,22 +457,44 @@ __device__ __forceinline__ void complete_node(const BuildArgs& a, uint32_t p, ui
     }
 }
 
+// The largest leaf edge bound below a node (margin.h: its QNode's margin codes).  Where a QNode is
+// built from the records (k_qnodes_cross, k_qnodes) it is read from inner[k].aux0, written by
+// whoever completes node k outside k_refit's in-block climb (refit_climb, refit_top_node,
+// k_build_small); inner[p].child_l / child_r carry a child's bound through the climb's hand-off,
+// beside its box (the hand-off uses no other word of inner[p]).
+__device__ __forceinline__ float* hand_edge(const BuildArgs& a, uint32_t p, uint32_t side) {
+    return reinterpret_cast<float*>(&a.inner[p].child_l) + side;
+}
+__device__ __forceinline__ float* node_edge(const BuildArgs& a, uint32_t k) {
+    return reinterpret_cast<float*>(&a.inner[k].aux0);
+}
+__device__ __forceinline__ void st_edge_sc1(float* dst, float E) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), __float_as_uint(E), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_edge_sc1(const float* src) {
+    return __uint_as_float(
+        __hip_atomic_load(reinterpret_cast<const uint32_t*>(src), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // The global climb, for the nodes whose leaf range crosses a refit workgroup: from a complete
-// node (box lo, hi; e = its parent link) upward, the child box handed over through inner[p]
-// (sc1) and a per-node ticket; the second arriver completes p and goes on.  k_qnodes_cross
-// quantizes these nodes afterwards.
-__device__ __forceinline__ void refit_climb(f3 lo, f3 hi, uint32_t e, const BuildArgs& a) {
+// node (box lo, hi, edge bound em; e = its parent link) upward, the child box and bound handed
+// over through inner[p] (sc1) and a per-node ticket; the second arriver completes p and goes on.
+// k_qnodes_cross quantizes these nodes afterwards.
+__device__ __forceinline__ void refit_climb(f3 lo, f3 hi, float em, uint32_t e, const BuildArgs& a) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
     for (int level = 0; e != INVALID && level < 2 * STACK_SIZE; level++) {
         const uint32_t p = e >> 1, side = e & 1u;
         st_box_sc1(side ? a.inner[p].rmin : a.inner[p].lmin, lo, hi);
+        st_edge_sc1(hand_edge(a, p, side), em);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the box stores before the ticket
         const uint32_t old = __hip_atomic_fetch_add(&a.refit_cnt[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == 0) return;
         asm volatile("" ::: "memory");
         f3 smin, smax;
         ld_box_sc1(side ? a.inner[p].lmin : a.inner[p].rmin, smin, smax);
+        em = fmaxf(em, ld_edge_sc1(hand_edge(a, p, side ^ 1u)));
+        *node_edge(a, p) = em;   // (read by k_qnodes_cross / k_qnodes, later launches)
         e = a.pint[p];
         if (side) complete_node(a, p, e, smin, smax, lo, hi, lo, hi);
         else      complete_node(a, p, e, lo, hi, smin, smax, lo, hi);
@@ -529,16 +551,24 @@ __device__ __forceinline__ bool quantize_axis(const float (&lo)[4], const float 
     return true;
 }
 
-// the QNode of a node from its four grandchild boxes (x/y/z min and max per grandchild c) and
-// ids, written as four 16-B stores
+// the QNode of a node from its four grandchild boxes (x/y/z min and max per grandchild c), ids and
+// the largest edge bound of the leaves below it (E, margin.h: its codes in the low 16 bits of the
+// power-of-two steps scl[1], scl[2]), written as four 16-B stores
 __device__ __forceinline__ void qnode_words(const float (&lx)[4], const float (&ly)[4], const float (&lz)[4],
                                             const float (&hx)[4], const float (&hy)[4], const float (&hz)[4], uint4 ids,
-                                            float4 (&d)[4]) {
+                                            float E, float4 (&d)[4]) {
     QNode q;
     bool ok = quantize_axis(lx, hx, q.org[0], q.scl[0], q.lo[0], q.hi[0]);
     ok = quantize_axis(ly, hy, q.org[1], q.scl[1], q.lo[1], q.hi[1]) && ok;
     ok = quantize_axis(lz, hz, q.org[2], q.scl[2], q.lo[2], q.hi[2]) && ok;
-    if (!ok) q.scl[0] = 0.f;   // the traversal reads the exact pair for this node
+    if (!ok) {
+        q.scl[0] = 0.f;   // the traversal reads the exact pair for this node
+    } else {
+        uint32_t ce, ct;
+        mt_node_codes(E, ce, ct);
+        q.scl[1] = __uint_as_float(__float_as_uint(q.scl[1]) | ce);
+        q.scl[2] = __uint_as_float(__float_as_uint(q.scl[2]) | ct);
+    }
     q.id[0] = ids.x; q.id[1] = ids.y; q.id[2] = ids.z; q.id[3] = ids.w;
     const float4* qs = reinterpret_cast<const float4*>(&q);
     d[0] = qs[0]; d[1] = qs[1]; d[2] = qs[2]; d[3] = qs[3];
@@ -569,7 +599,8 @@ __device__ __forceinline__ void qent_sel(QEnt& d, const QEnt& s, bool take) {
 }
 // Kids(e, c0, c1): the two children of internal entry e
 template <class Kids>
-__device__ __forceinline__ void greedy_qnode_words(const QEnt& e0, const QEnt& e1, Kids&& kids, float4 (&out)[4]) {
+__device__ __forceinline__ void greedy_qnode_words(const QEnt& e0, const QEnt& e1, Kids&& kids, float edge,
+                                                   float4 (&out)[4]) {
     QEnt E[4] = {e0, e1, e0, e0};
     uint32_t n = 2;
 #pragma unroll
@@ -611,13 +642,7 @@ __device__ __forceinline__ void greedy_qnode_words(const QEnt& e0, const QEnt& e
     }
     if (absent1) id[1] = INVALID;
     if (absent3) id[3] = INVALID;
-    qnode_words(lx, ly, lz, hx, hy, hz, make_uint4(id[0], id[1], id[2], id[3]), out);
-}
-template <class Kids>
-__device__ __forceinline__ void greedy_qnode(const QEnt& e0, const QEnt& e1, Kids&& kids, QNode* dst) {
-    float4 w[4];
-    greedy_qnode_words(e0, e1, kids, w);
-    store4(dst, w);
+    qnode_words(lx, ly, lz, hx, hy, hz, make_uint4(id[0], id[1], id[2], id[3]), edge, out);
 }
 // entries from the node records in global memory (record words: rtbvh_device.h)
 __device__ __forceinline__ void record_kids(const Inner* __restrict__ rec, uint32_t slot, QEnt& c0, QEnt& c1) {
@@ -632,14 +657,15 @@ __device__ __forceinline__ void record_kids(const Inner* __restrict__ rec, uint3
     c1.b[0] = w1.x; c1.b[1] = w1.y; c1.b[2] = w2.z; c1.b[3] = w1.z; c1.b[4] = w1.w; c1.b[5] = w2.w;
 }
 // the QNode of the node whose record is at `slot`, from the records (crossing nodes, small builds);
-// PSEUDO_NOGRID: a QNode without a grid gets its node's leaf pseudo-records (the bounce walk reads
-// that node's exact record pair, trace.hip qchildren), for a build that wrote none
+// E: the largest edge bound below it (node_edge); PSEUDO_NOGRID: a QNode without a grid gets its
+// node's leaf pseudo-records (the bounce walk reads that node's exact record pair, trace.hip
+// qchildren), for a build that wrote none
 template <bool PSEUDO_NOGRID = false>
-__device__ __forceinline__ void qnode_from_records(Inner* __restrict__ rec, uint32_t slot, QNode* dst) {
+__device__ __forceinline__ void qnode_from_records(Inner* __restrict__ rec, uint32_t slot, float E, QNode* dst) {
     QEnt e0, e1;
     record_kids(rec, slot, e0, e1);
     float4 w[4];
-    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { record_kids(rec, e.slot, c0, c1); }, w);
+    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { record_kids(rec, e.slot, c0, c1); }, E, w);
     store4(dst, w);
     if (PSEUDO_NOGRID && w[0].w == 0.f) {
         if (e0.id & LEAF_BIT)
@@ -652,11 +678,11 @@ __device__ __forceinline__ void qnode_from_records(Inner* __restrict__ rec, uint
 // QNodes of every internal node from the records (the one-workgroup build and
 // rtbvh_build_from_codes), one node per thread.
 __global__ __launch_bounds__(BLOCK) void k_qnodes(Inner* __restrict__ rec, const uint32_t* __restrict__ pint,
-                                                  QNode* __restrict__ qn, uint32_t T) {
+                                                  const Inner* __restrict__ inner, QNode* __restrict__ qn, uint32_t T) {
     const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
     if (k + 1 >= T) return;
     const uint32_t slot = slot_of(pint[k], T);   // pint[0] = INVALID: the root
-    qnode_from_records(rec, slot, qn + slot);
+    qnode_from_records(rec, slot, __uint_as_float(inner[k].aux0), qn + slot);
 }
 
 // The crossing nodes of refit workgroup b are xlist[b * RBLOCK, + xcnt[b]): one wave per
@@ -675,8 +701,9 @@ __device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f, uint32_t
 __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
     for_crossing(a, [&](uint32_t k) {
         const uint32_t slot = slot_of(a.pint[k], a.T);
-        if (a.pseudo) qnode_from_records<false>(a.rec, slot, a.qnode + slot);
-        else qnode_from_records<true>(a.rec, slot, a.qnode + slot);
+        const float E = *node_edge(a, k);
+        if (a.pseudo) qnode_from_records<false>(a.rec, slot, E, a.qnode + slot);
+        else qnode_from_records<true>(a.rec, slot, E, a.qnode + slot);
     });
 }
 
@@ -744,7 +771,10 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     {   // the block's depth range (min lo.z, max hi.z of its leaves) for k_zrange: the binned primary
         // pass buckets by depth as soon as the leaves are written, before the climb above the blocks
         // (and the largest edge bound: an infinite one -- a non-finite triangle -- stays infinite)
-        float zl = i < T ? lo.z : INFINITY, zh = i < T ? hi.z : -INFINITY, em = emax;
+        // (rootbox[8], the walk's scene-wide margin for keys stacked before a first hit, takes the finite
+        // bounds only: a subtree holding a non-finite triangle is never pruned by distance, its QNodes'
+        // tcap being -1)
+        float zl = i < T ? lo.z : INFINITY, zh = i < T ? hi.z : -INFINITY, em = emax < INFINITY ? emax : 0.f;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             zl = fminf(zl, __shfl_xor(zl, off, 64));
@@ -780,12 +810,18 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
         if (cross) {   // k_refit_top takes it from here (kernel boundary: plain stores)
             float* hb = side ? a.inner[p].rmin : a.inner[p].lmin;
             hb[0] = lo.x; hb[1] = lo.y; hb[2] = lo.z; hb[3] = hi.x; hb[4] = hi.y; hb[5] = hi.z;
+            *hand_edge(a, p, side) = emax;
             break;
         }
         float* sb = s_box[p - base][side];
         sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the LDS box lands before the ticket
-        if (atomicAdd(&s_cnt[p - base], 1u) == 0) break;
+        // the ticket carries the edge bound: atomicMax of (bound | bit 31) -- nonzero, ordered as the
+        // bounds (non-negative floats order as their bits) -- so the first arriver sees 0, the second
+        // the sibling's bound, and the word ends as the node's own (phase 3 reads it)
+        const uint32_t tk = atomicMax(&s_cnt[p - base], __float_as_uint(emax) | 0x80000000u);
+        if (tk == 0) break;
+        emax = fmaxf(emax, __uint_as_float(tk & 0x7FFFFFFFu));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const float* ob = s_box[p - base][side ^ 1u];
         const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
@@ -844,7 +880,8 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     };
     QEnt e0, e1;
     lds_kids(i, e0, e1);
-    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, qw);
+    const float E = __uint_as_float(s_cnt[tid] & 0x7FFFFFFFu);   // the node's edge bound (the climb's ticket)
+    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, E, qw);
     }
     if (!RTBVH_REFIT_STAGE) {
         store4(a.rec + slot, rw);
@@ -922,23 +959,29 @@ __device__ __forceinline__ void refit_top_node(const BuildArgs& a, uint32_t k) {
     const float* L = a.inner[k].lmin;
     const float* R = a.inner[k].rmin;
     f3 lo, hi;
+    float em;
     uint32_t e = a.pint[k];
     if (ncl && ncr) {
+        em = fmaxf(*hand_edge(a, k, 0), *hand_edge(a, k, 1));
+        *node_edge(a, k) = em;
         complete_node(a, k, e, mk(L[0], L[1], L[2]), mk(L[3], L[4], L[5]), mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]),
                       lo, hi);
-    } else {   // one child here: its arrival at k's ticket (the other side's box comes sc1)
+    } else {   // one child here: its arrival at k's ticket (the other side's box and bound come sc1)
         const uint32_t side = ncl ? 0u : 1u;
         const float* B = side ? R : L;
         const f3 blo = mk(B[0], B[1], B[2]), bhi = mk(B[3], B[4], B[5]);
+        em = *hand_edge(a, k, side);
         const uint32_t old = __hip_atomic_fetch_add(&a.refit_cnt[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == 0) return;
         asm volatile("" ::: "memory");
         f3 smin, smax;
         ld_box_sc1(side ? a.inner[k].lmin : a.inner[k].rmin, smin, smax);
+        em = fmaxf(em, ld_edge_sc1(hand_edge(a, k, side ^ 1u)));
+        *node_edge(a, k) = em;
         if (side) complete_node(a, k, e, smin, smax, blo, bhi, lo, hi);
         else      complete_node(a, k, e, blo, bhi, smin, smax, lo, hi);
     }
-    refit_climb(lo, hi, e, a);
+    refit_climb(lo, hi, em, e, a);
 }
 __global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
     for_crossing(a, [&](uint32_t k) { refit_top_node(a, k); });
@@ -969,7 +1012,7 @@ __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float*
         for (int k = 0; k < 6; k++) a.rootbox[k] = b[k];
         return;
     }
-    refit_climb(lo, hi, a.pleaf[i], a);
+    refit_climb(lo, hi, INFINITY, a.pleaf[i], a);   // (no triangles: no margin; the walk never prunes by distance)
 }
 
 // ---- small scenes: the whole build in one workgroup ------------------------------
@@ -1115,10 +1158,12 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
     // leaves i = tid, tid + SMALL_BLOCK: records, margins, Karras nodes; the boxes stay in registers
     // for the refit (the triangle id from the sorted key in LDS)
     f3 llo[2], lhi[2];
+    float lem[2];   // the leaves' edge bounds (the climb carries them up: each node's QNode margin)
 #pragma unroll
     for (uint32_t b = 0; b < 2; b++) {
         const uint32_t i = tid + b * SMALL_BLOCK;
         llo[b] = lhi[b] = mk(0.f, 0.f, 0.f);
+        lem[b] = 0.f;
         if (i < T) {
             f3 lo, hi;
             float4 r[4];
@@ -1128,10 +1173,12 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
             float em, zkey;
             leaf_margin(r, lo.z, hi.z, em, zkey);
             a.lfp[i] = leaf_footprint(lo, hi, zkey);
-            atomicMax(&s_emax, __float_as_uint(em));   // (non-negative floats order as their bits)
+            // (non-negative floats order as their bits; the scene-wide bound takes the finite ones, k_refit)
+            if (em < INFINITY) atomicMax(&s_emax, __float_as_uint(em));
             if (i + 1 < T) karras_node<MODE>(codes, T, i, a.topo, a.pleaf, a.pint);
             llo[b] = lo;
             lhi[b] = hi;
+            lem[b] = em;
         }
     }
     if (tid == 0 && T > 1) a.pint[0] = INVALID;
@@ -1156,6 +1203,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
         const uint32_t i = tid + b * SMALL_BLOCK;
         if (i >= T) continue;
         f3 lo = llo[b], hi = lhi[b];
+        float em = lem[b];
         if (T == 1) {
             a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
             a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
@@ -1169,7 +1217,10 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
             float* sb = s_box[p][side];
             sb[0] = lo.x; sb[1] = lo.y; sb[2] = lo.z; sb[3] = hi.x; sb[4] = hi.y; sb[5] = hi.z;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the LDS box lands before the ticket
-            if (atomicAdd(&s_cnt[p], 1u) == 0) break;
+            // the ticket carries the edge bound as k_refit's (the word ends as the node's bound)
+            const uint32_t tk = atomicMax(&s_cnt[p], __float_as_uint(em) | 0x80000000u);
+            if (tk == 0) break;
+            em = fmaxf(em, __uint_as_float(tk & 0x7FFFFFFFu));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const float* ob = s_box[p][side ^ 1u];
             const f3 smin = mk(ob[0], ob[1], ob[2]), smax = mk(ob[3], ob[4], ob[5]);
@@ -1191,6 +1242,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
         const uint2 ids = s_ids[p];
         store_record(a.rec + slot_of(s_pint[p], T), mk(l[0], l[1], l[2]), mk(l[3], l[4], l[5]), mk(r[0], r[1], r[2]),
                      mk(r[3], r[4], r[5]), ids.x, ids.y, p);
+        *node_edge(a, p) = __uint_as_float(s_cnt[p] & 0x7FFFFFFFu);   // (k_qnodes: the QNode's margin)
     }
 #ifdef RTBVH_SMALL_PROBE
     SMALL_MARK(6);
@@ -1267,7 +1319,8 @@ void launch_build_small(const BuildArgs& a, hipStream_t s) {
 }
 void launch_qnodes(const BuildArgs& a, hipStream_t s) {
     if (a.T > 1)
-        hipLaunchKernelGGL(k_qnodes, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.rec, a.pint, a.qnode, a.T);
+        hipLaunchKernelGGL(k_qnodes, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a.rec, a.pint, a.inner,
+                           a.qnode, a.T);
 }
 uint32_t refit_blocks(uint32_t T) { return (T + RBLOCK - 1) / RBLOCK; }
 // the leaves' depth range: rootbox[6..7] = min lo.z, max hi.z over k_refit's per-block ranges, and

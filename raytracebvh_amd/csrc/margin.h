@@ -44,6 +44,52 @@ RTBVH_HD inline MtMargin mt_margin(float E, float L, float A) {
     return m;
 }
 
+// ---- per-node margins (the certified bounce walk) ----------------------------------------
+// rho grows with E and tcap falls with it, so a box may use the largest edge bound E_n of the leaves BELOW
+// it instead of the scene's: every candidate x in the box has E_x <= E_n, hence rho_x(t) <= rho_n(t) and
+// tcap(E_x) >= tcap(E_n).  Each QNode carries its subtree's E_n (rounded up) and tcap(E_n) (rounded down)
+// as 16-bit codes (the high half of an fp32) in the low bits of its scl[1] / scl[2] words -- the grid steps
+// are powers of two, their mantissas are otherwise zero (build.hip qnode_words).  The walk grows the node's
+// boxes by
+//     rho_n(t) = E_n^2 (P t + Q E_n) + U1 t + U0 E_n + FLOOR      (>= mt_margin(E_n).r1 t + r0)
+// and never prunes a box by distance once its bound passes tcap(E_n) (the box's key is capped there).
+RTBVH_HD inline uint32_t mt_f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+RTBVH_HD inline float mt_u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+RTBVH_HD inline uint32_t mt_code_up(float x) { return (mt_f2u(x) + 0xFFFFu) >> 16; }   // x >= 0: decodes >= x
+RTBVH_HD inline uint32_t mt_code_down(float x) { return x >= 0.f ? mt_f2u(x) >> 16 : 0xBF80u; }   // <= x; -1
+RTBVH_HD inline float mt_code_val(uint32_t w) { return mt_u2f(w << 16); }   // (the low 16 bits of w)
+// a node's codes from the largest edge bound of its leaves (inf: a non-finite triangle below; tcap -1)
+RTBVH_HD inline void mt_node_codes(float E, uint32_t& ce, uint32_t& ct) {
+    ce = mt_code_up(E >= 0.f ? E : INFINITY);   // (NaN: inf)
+    const MtMargin m = mt_margin(mt_code_val(ce), MT_LAMBDA, MT_A);
+    ct = mt_code_down(m.tcap);
+}
+struct MtNodeK {
+    float P, Q, U1, U0;
+};
+// the coefficients of rho_n for the bounce walk (L = MT_LAMBDA, A = MT_A), each rounded up past the few
+// roundings of evaluating rho_n (the 1.01 of mt_margin already covers computing and applying the bound)
+RTBVH_HD inline MtNodeK mt_node_consts() {
+    constexpr float up = 1.f + 0x1p-18f;
+    MtNodeK k;
+    k.P = 1.01f * 35.4f * MT_U * MT_LAMBDA * MT_A * MT_A * up;
+    k.Q = 1.01f * 1.31f * 35.4f * MT_U * MT_LAMBDA * MT_A * up;
+    k.U1 = 4.04f * MT_U * MT_A * up;
+    k.U0 = 6.06f * MT_U * up;
+    return k;
+}
+// rho_n(t) in two steps, as the walk evaluates it: per node (E^2, Q E, U0 E + FLOOR), then per bound t
+struct MtNodeRho {
+    float E2, QE, UE;
+};
+RTBVH_HD inline MtNodeRho mt_node_prep(const MtNodeK& k, float E) {
+    return MtNodeRho{E * E, k.Q * E, fmaf(k.U0, E, MT_FLOOR)};
+}
+RTBVH_HD inline float mt_node_eval(const MtNodeK& k, const MtNodeRho& n, float t) {
+    return fmaf(n.E2, fmaf(k.P, t, n.QE), fmaf(k.U1, t, n.UE));
+}
+RTBVH_HD inline float mt_node_rho(const MtNodeK& k, float E, float t) { return mt_node_eval(k, mt_node_prep(k, E), t); }
+
 // the global edge bound of a triangle: max(|e1|, |e2|) rounded up (inf for a non-finite triangle)
 RTBVH_HD inline float mt_edge_bound(float e1x, float e1y, float e1z, float e2x, float e2y, float e2z) {
     const float a = e1x * e1x + e1y * e1y + e1z * e1z, b = e2x * e2x + e2y * e2y + e2z * e2z;

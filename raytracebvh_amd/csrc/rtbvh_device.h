@@ -33,6 +33,14 @@
 
 #include "margin.h"
 
+// A/B probes that render WRONG frames (the cost probes RTBVH_BOUNCE_PROBE / RTBVH_PB_PROBE /
+// RTBVH_SMALL_PROBE, the step-by-step walk prints of RTBVH_DEBUG_PIXEL) compile only into A/B
+// libraries built with -DRTBVH_AB_BUILD, which the Makefile refuses for librtbvh.so itself
+#if (defined(RTBVH_BOUNCE_PROBE) || defined(RTBVH_SMALL_PROBE) || defined(RTBVH_DEBUG_PIXEL) || \
+     (defined(RTBVH_PB_PROBE) && RTBVH_PB_PROBE != 0)) && !defined(RTBVH_AB_BUILD)
+#error "probe builds render wrong frames: A/B libraries only (-DRTBVH_AB_BUILD, OUT=<another library>)"
+#endif
+
 namespace rtbvh {
 
 constexpr uint32_t LEAF_BIT = 0x80000000u;
@@ -67,7 +75,11 @@ static_assert(sizeof(Inner) == 64, "Inner must be one 64-B record");
 // pair at slots 2k, 2k+1 (a leaf child counts once, its second entry has id INVALID) --
 // with every corner on an 8-bit per-axis grid whose origin is the min corner of k's box
 // and whose step is a power of two:
-//   org[3], scl[3]   grid origin and step (scl[0] == 0: not quantized, use the exact pair)
+//   org[3], scl[3]   grid origin and step (scl[0] == 0: not quantized, use the exact pair); the
+//                    steps are powers of two, so the low 16 bits of scl[1] / scl[2] carry the
+//                    certified walk's margin codes of the node (margin.h mt_node_codes: the largest
+//                    edge bound of its leaves, rounded up, and its margin range, rounded down) --
+//                    readers mask them off (& 0xFF800000)
 //   lo[a], hi[a]     byte c = grandchild c's min / max on axis a in grid steps
 //   id[4]            grandchildren: the slot of an internal one, LEAF_BIT | j, or INVALID
 // qdecode() is exact in the product (8-bit q times a power of two) and rounds once in

@@ -1405,35 +1405,34 @@ __device__ __forceinline__ bool qbox_fast(const QAxis& x, const QAxis& y, const 
     return 0 <= mx && mn <= mx && (!hit || mn <= best);
 }
 
-// The certified walk's box test: qbox_fast, and the box's stack key.  After the first bound the key is the
-// entry (of the box grown by rr, qaxis<true>).  Before it (best +inf: nothing pruned by distance, rr = 0)
-// it is the entry of the box grown by rho(t_e), t_e its margin-free entry (`mg`: the margin): pops compare
-// a key with later, finite bounds kb, and for kb <= t_e, rho(kb) <= rho(t_e), so the key is at most the
-// entry of the box grown by rho(kb) -- a box the certified walk must visit (that entry <= kb) keeps
-// key <= kb; for kb > t_e the key (<= t_e) is kept anyway, the margin-free entry being below the bound.
-// The grown entry is the max over axes of near - rho |1/d| (branch-free: rho = 0 after the first bound).
+// The certified walk's box test: qbox_fast, and the box's stack key, capped at its node's margin range tcn
+// (margin.h: past it the node's margin says nothing, so the box is never pruned by distance -- kept while
+// min(key, tcn) <= best, the pop's test too).  After the first bound the key is the entry of the box grown
+// by the node's margin rho_n(best) (rr, qaxis<true>).  Before it (best +inf: nothing pruned, rr = 0) it is
+// the entry of the box grown by rho_n(t_e), t_e its margin-free entry: pops compare a key with later,
+// finite bounds kb, and for kb <= t_e, rho_n(kb) <= rho_n(t_e), so the key is at most the entry of the box
+// grown by rho_n(kb) -- a box the certified walk must visit (that entry <= kb) keeps key <= kb; for
+// kb > t_e the key (<= t_e) is kept anyway, the margin-free entry being below the bound.  The grown entry
+// is the max over axes of near - rho |1/d| (branch-free: rho = 0 after the first bound).
 __device__ __forceinline__ bool qbox_fast_cert(const QAxis& x, const QAxis& y, const QAxis& z, int c, float best,
-                                               const MtMargin& mg, f3 ainv, float& key) {
+                                               const MtNodeK& nk, const MtNodeRho& nr, f3 ainv, float tcn,
+                                               float& key) {
     const float nx = qt(x.nw, c, x.b, x.an), ny = qt(y.nw, c, y.b, y.an), nz = qt(z.nw, c, z.b, z.an);
     const float mn = fmaxf(fmaxf(nx, ny), nz);
     const float mx = fminf(fminf(qt(x.fw, c, x.b, x.af), qt(y.fw, c, y.b, y.af)), qt(z.fw, c, z.b, z.af));
-    const float rb = best == __builtin_inff() ? fmaf(mg.r1, fmaxf(mn, 0.f), mg.r0) : 0.f;
-    key = fmaxf(fmaxf(fmaf(-rb, ainv.x, nx), fmaf(-rb, ainv.y, ny)), fmaf(-rb, ainv.z, nz));
-    return 0 <= mx && mn <= mx && mn <= best;
+    const float rb = best == __builtin_inff() ? mt_node_eval(nk, nr, fmaxf(mn, 0.f)) : 0.f;
+    key = fminf(fmaxf(fmaxf(fmaf(-rb, ainv.x, nx), fmaf(-rb, ainv.y, ny)), fmaf(-rb, ainv.z, nz)), tcn);
+    return 0 <= mx && mn <= mx && key <= best;
 }
-
-// A/B builds only (not certified): 1 = no margin (the unchecked walk's pruning inside the certified
-// code), 2 = the margin's range taken as unbounded
-#ifndef RTBVH_CERT_AB
-#define RTBVH_CERT_AB 0
-#endif
 // GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it).
 // CERT (MODE 2 only): the certified walk.  Every box test's entry distance is taken on the
-// box grown by the margin rho(best) (margin.h: no hit the triangle test accepts at t <= best lies outside
-// that box), so the walk sees EVERY leaf whose triangle could be accepted at t <= best: its (t, leaf)
-// minimum is the minimum over all triangles the reference could test.  A ray the bound does not cover --
-// a slack-test-free ray (qnode_fast_ray), |d| off unit, a node without a grid, a stack overflow -- is
-// flagged in its hit record (HIT_FLAG) for the reference-order re-trace (k_bounce_redo).
+// box grown by its node's margin rho_n(best) (margin.h: no hit the triangle test accepts at t <= best lies
+// outside that box; rho_n from the largest edge bound of the leaves below the node, carried by its QNode),
+// and a box is not pruned by distance at all while best is past its node's margin range: so the walk sees
+// EVERY leaf whose triangle could be accepted at t <= best, and its (t, leaf) minimum is the minimum over
+// all triangles the reference could test.  A ray the bound does not cover -- a slack-test-free ray
+// (qnode_fast_ray), |d| off unit, a node without a grid, a stack overflow -- is flagged in its hit record
+// (HIT_FLAG) for the reference-order re-trace (k_bounce_redo).
 template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
@@ -1459,11 +1458,9 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     int sp = 0;
     float best = 0.f;
     f3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
-    // CERT: the margin of the scene's edge bound (rootbox[8]); per ray the pruning bound kb (best, or +inf
-    // past the margin's range mg.tcap: no pruning) and the margin rr = rho(best), and the flag
-    MtMargin mg{0.f, 0.f, -1.f};
-    if (CERT) mg = mt_margin(rootbox[8], MT_LAMBDA, MT_A);
-    float kb = __builtin_inff(), rr = 0.f;
+    // CERT: the per-node margin's coefficients (margin.h rho_n; each QNode carries its node's edge bound
+    // and margin range) and the ray's flag
+    const MtNodeK nk = mt_node_consts();
     bool flg = false;
     __shared__ uint32_t s_stk[WIDE ? 1 : SB][WIDE ? 1 : BLOCK];   // (none for WIDE: its LDS is the 6-B stack)
     uint32_t stack[WIDE ? 1 : STACK_SIZE - SB];   // entries [SB, STACK_SIZE)
@@ -1496,23 +1493,34 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
         uint4 a3, b3;
         float t0, t1, t2, t3;
         bool h0, h1, h2, h3;
-        const float kbb = CERT ? kb : key_t(key);
+        const float kbb = key_t(key);
         if (q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
-            const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w, sy = q1.x, sz = q1.y;
+            // scl[1], scl[2] carry the node's margin codes in their (otherwise zero) mantissas (margin.h)
+            const uint32_t wy = __float_as_uint(q1.x), wz = __float_as_uint(q1.y);
+            const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w;
+            const float sy = __uint_as_float(wy & 0xFF800000u), sz = __uint_as_float(wz & 0xFF800000u);
             const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
             const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
             a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
             b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
             if (qfast) {
+                // CERT: the node's margin rho_n(best) (0 before the first bound) and its range
+                float rr = 0.f, tcn = 0.f;
+                MtNodeRho nr{0.f, 0.f, 0.f};
+                if (CERT) {
+                    nr = mt_node_prep(nk, mt_code_val(wy));
+                    tcn = mt_code_val(wz);
+                    rr = kbb < __builtin_inff() ? mt_node_eval(nk, nr, kbb) : 0.f;
+                }
                 const QAxis X = qaxis<CERT>(ox, sx, lx, hx, o.x, inv.x, rr),
                             Y = qaxis<CERT>(oy, sy, ly, hy, o.y, inv.y, rr),
                             Z = qaxis<CERT>(oz, sz, lz, hz, o.z, inv.z, rr);
                 if (CERT) {
                     const f3 ai = mk(fabsf(inv.x), fabsf(inv.y), fabsf(inv.z));
-                    h0 = qbox_fast_cert(X, Y, Z, 0, kbb, mg, ai, t0);
-                    h1 = qbox_fast_cert(X, Y, Z, 1, kbb, mg, ai, t1);
-                    h2 = qbox_fast_cert(X, Y, Z, 2, kbb, mg, ai, t2);
-                    h3 = qbox_fast_cert(X, Y, Z, 3, kbb, mg, ai, t3);
+                    h0 = qbox_fast_cert(X, Y, Z, 0, kbb, nk, nr, ai, tcn, t0);
+                    h1 = qbox_fast_cert(X, Y, Z, 1, kbb, nk, nr, ai, tcn, t1);
+                    h2 = qbox_fast_cert(X, Y, Z, 2, kbb, nk, nr, ai, tcn, t2);
+                    h3 = qbox_fast_cert(X, Y, Z, 3, kbb, nk, nr, ai, tcn, t3);
                 } else {
                     h0 = qbox_fast(X, Y, Z, 0, true, kbb, t0);
                     h1 = qbox_fast(X, Y, Z, 1, true, kbb, t1);
@@ -1599,9 +1607,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     node = root_slot(T);
                     guard = 2 * T + 2;
                     if (CERT) {   // a ray the margin does not cover ends at its first step, flagged
-                        kb = __builtin_inff();
-                        rr = 0.f;
-                        flg = !(qfast && dot(d, d) <= MT_DD && mg.tcap > EPSILON);
+                        flg = !(qfast && dot(d, d) <= MT_DD);
                         if (flg) node = INVALID;
                     }
                 }
@@ -1643,7 +1649,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
 #ifdef RTBVH_DEBUG_PIXEL   // (scripts/debug_walk.py: one ray's walk, step by step, from the COUNT kernel)
                     if (COUNT && qin[r].idx == (uint32_t)RTBVH_DEBUG_PIXEL)
                         printf("DBG %d q %u sp %d kb %.6g key %.6g | %.6g %x %.6g %x %.6g %x %.6g %x\n", (int)CERT, node,
-                               sp, kb, key_t(key), k0, i0, k1, i1, k2, i2, k3, i3);
+                               sp, key_t(key), key_t(key), k0, i0, k1, i1, k2, i2, k3, i3);
 #endif
                     const bool lf0 = i0 != INVALID && (i0 & LEAF_BIT);
                     L = lf0 ? i0 : INVALID;
@@ -1660,7 +1666,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                 }
 #ifdef RTBVH_DEBUG_PIXEL
                 if (COUNT && L != INVALID && qin[r].idx == (uint32_t)RTBVH_DEBUG_PIXEL)
-                    printf("DBG %d leaf %x sp %d kb %.6g key %.6g\n", (int)CERT, L, sp, kb, key_t(key));
+                    printf("DBG %d leaf %x sp %d kb %.6g key %.6g\n", (int)CERT, L, sp, key_t(key), key_t(key));
 #endif
                 if (L != INVALID) {   // branch-free test (the same accept predicate), u64 key minimum
                     const uint32_t j = L & ~LEAF_BIT;
@@ -1673,12 +1679,6 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
                     btri = k < key ? __float_as_uint(lc.y) & ~LEAF_BIT : btri;
                     key = k < key ? k : key;
-                    if (CERT) {   // the pruning bound and the margin of the new best
-                        const float tk = key_t(key);
-                        const bool cov = RTBVH_CERT_AB == 2 || tk <= mg.tcap;
-                        kb = cov || RTBVH_CERT_AB == 1 ? tk : __builtin_inff();
-                        rr = cov && RTBVH_CERT_AB != 1 ? fmaf(mg.r1, tk, mg.r0) : 0.f;
-                    }
                 }
                 if (!done && node == INVALID) {   // pop, dropping entries that cannot improve
                     while (sp > 0) {
@@ -1686,7 +1686,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                         uint2 e;
                         if (sp < SW) e = make_uint2(s_wid[sp][tid], __float_as_uint(bf16_up(s_wt[sp][tid])));
                         else e = wstack[sp - SW];
-                        if (__uint_as_float(e.y) <= (CERT ? kb : key_t(key))) {
+                        if (__uint_as_float(e.y) <= key_t(key)) {
                             node = e.x;
                             break;
                         }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One C5 bounce ray's walk, step by step (a RTBVH_DEBUG_PIXEL build prints them from the COUNT kernel),
 in the certified and the unchecked 4-wide walks.  RTBVH_LIB = that build:
-  make -C raytracebvh_amd/csrc OUT=../librtbvh_dbg.so OBJDIR=../../build/obj_dbg EXTRA=-DRTBVH_DEBUG_PIXEL=<pixel>
+  make -C raytracebvh_amd/csrc OUT=../librtbvh_dbg.so OBJDIR=../../build/obj_dbg EXTRA="-DRTBVH_AB_BUILD -DRTBVH_DEBUG_PIXEL=<pixel>"
 (the pixel from stats trav_longest, scripts/longest_walk.py; profiles/r04_n_longest_walk_debug.log)."""
 import os
 import sys

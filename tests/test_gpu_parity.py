@@ -539,7 +539,10 @@ def test_qnodes_contain_the_exact_boxes(scene):
     steps, the entries of the largest-area greedy collapse (build.hip greedy_qnode: from k's
     two children, the internal entry with the largest box surface replaced by its children,
     twice; internal entries by their slots), and decoded corners (origin + q * step in fp32,
-    the traversal's arithmetic) that contain every entry's exact box."""
+    the traversal's arithmetic) that contain every entry's exact box.  The low 16 bits of the
+    steps scl[1] / scl[2] carry the certified walk's per-node margin codes (margin.h
+    mt_node_codes): the largest edge bound of the node's leaves rounded up -- exactly, from the
+    clip-space triangles -- and a margin range no larger than that bound's."""
     if scene == "synthetic":
         s = rt.synthetic(20_000, seed=7, half_extent=(30, 30, 20))
     elif scene == "general boxes":
@@ -563,6 +566,9 @@ def test_qnodes_contain_the_exact_boxes(scene):
         return 2 * (par[x] - T) + (0 if cl[par[x]] == x else 1)
 
     q = q[[slot(T + k) for k in range(T - 1)]]   # node-indexed from here on
+    codes_e, codes_t = q[:, 4] & 0xFFFF, q[:, 5] & 0xFFFF
+    q = q.copy()
+    q[:, 3:6] &= np.uint32(0xFF800000)   # the steps without the margin codes
     f = q.view(np.float32)
     org, scl = f[:, 0:3], f[:, 3:6]
     assert (scl[:, 0] != 0).all()   # every node of these scenes has a finite grid
@@ -612,6 +618,40 @@ def test_qnodes_contain_the_exact_boxes(scene):
     half = scl / np.float32(2)
     reach = org + np.float32(255) * half   # product exact, one rounding in the add
     assert ((reach < top) | (half < np.float32(2.0 ** -120))).all(), "grid step not minimal"
+    # the margin codes: E_k = max over node k's leaves of margin.h mt_edge_bound on the clip-space
+    # triangle (rtbvh_device.h xform_point's operation order, no FMA: numpy float32), rounded up
+    wvp = rt.camera_reference(320, 240)[0].reshape(4, 4)
+    P = s.vertices[:, :3].astype(np.float32)
+    clip = ((P[:, 0:1] * wvp[0] + P[:, 1:2] * wvp[1]) + P[:, 2:3] * wvp[2]) + wvp[3]
+    tri = clip[s.indices.reshape(-1, 3), :3]
+    e1, e2 = tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]
+    sq = lambda e: (e[:, 0] * e[:, 0] + e[:, 1] * e[:, 1]) + e[:, 2] * e[:, 2]
+    with np.errstate(invalid="ignore"):
+        eb = np.sqrt(np.maximum(sq(e1), sq(e2))) * np.float32(1 + 2.0 ** -20)
+    eb = np.where(np.isnan(eb), np.float32(np.inf), eb).astype(np.float32)
+    leaf_e = eb[nodes["index"][:T] // 3]
+    node_e = np.zeros(T - 1, np.float32)
+    order = []   # internal nodes, children before parents
+    st = [T]
+    while st:
+        x = st.pop()
+        order.append(x)
+        st.extend(c for c in (cl[x], cr[x]) if c >= T)
+
+    def ev(c):
+        return leaf_e[c] if c < T else node_e[c - T]
+    for x in reversed(order):
+        node_e[x - T] = max(ev(cl[x]), ev(cr[x]))
+    want_e = ((node_e.view(np.uint32).astype(np.uint64) + 0xFFFF) >> 16).astype(np.uint32)
+    np.testing.assert_array_equal(codes_e, want_e)
+    eq = (codes_e << 16).view(np.float32).astype(np.float64)
+    tcn = (codes_t << 16).view(np.float32).astype(np.float64)
+    c = 28.3 * 100.01 * (1 + 2.0 ** -18) * 2.0 ** -24 * eq   # margin.h mt_margin's condition (C)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tcap = np.where(np.isfinite(eq), (0.2 / c - 2 * eq) / (1 + 2.0 ** -18) * 0.999, -1.0)
+    assert ((tcn <= tcap * (1 + 1e-5)) | ((tcn == -1) & (tcap < 0))).all()
+    big = tcap >= 1   # (the 16-bit code truncates: within 2^-8)
+    assert (tcn[big] >= 0.99 * tcap[big]).all()
 
 
 def _general_box(lo, hi):
@@ -973,7 +1013,7 @@ def test_verify_walk_and_auto_walk():
             for k in range(2):
                 st = auto.stats()
                 assert st["walk_flags"] == walk and st["walk_state"] == (2 if walk else 0)
-                assert st["walk_checks"] == (k + 1 if walk else 0)
+                assert st["cert_traces"] == (k + 1 if walk else 0)
                 np.testing.assert_array_equal(auto.read_framebuffer(), want)
                 np.testing.assert_array_equal(auto.read_intensity(), ref.read_intensity())
                 auto.compute_bvh(W, H, 1)
@@ -1012,7 +1052,7 @@ def test_containment_failure_auto_walk_returns_the_reference_frame():
             for _ in range(3):
                 st = c.stats()
                 assert st["walk_state"] == 2 and st["walk_flags"] == CERT_WALKS
-                assert st["redo_rays"][0] >= 1 and st["walk_fallbacks"] >= 1
+                assert st["redo_rays"][0] >= 1 and st["redo_total"] >= 1
                 np.testing.assert_array_equal(c.read_framebuffer(), want)
                 c.set_camera(wvp.copy(), wv.copy())   # every frame, unchanged (Graphics::onUpdate)
                 c.compute_bvh(W, H, 1)
@@ -1055,21 +1095,123 @@ def test_auto_walk_orbit_replays_one_graph():
         assert len({c[0].tobytes() for c in cams}) == 5
 
 
-def test_certified_walks_flag_rays_past_the_margin():
-    """A ray the certified bounce walk cannot vouch for -- here every ray of a scene whose triangles are
-    too large for the margin's range (margin.h: condition (C) fails for edges of ~60 units at any t) --
-    is re-traced in the reference order: the frame equals the reference's, and the bounce pass's
-    re-trace count is the whole live queue."""
-    rng = np.random.default_rng(7)
-    n = 70_000
-    cen = np.stack([rng.uniform(-60, 60, n), rng.uniform(-60, 60, n), rng.uniform(-20, 20, n)], 1)
-    off = rng.uniform(-8, 8, (n, 3, 3))   # object-space edges up to ~28: clip-space edges of ~60
+def _material(ns=300.0):
+    m = np.zeros(1, rt._lib.MATERIAL_DTYPE)
+    m[0]["diffuse"] = (0.64, 0.64, 0.64, 1.0)
+    m[0]["specular"] = (0.5, 0.5, 0.5, 1.0)
+    m[0]["shininess"] = ns
+    m[0]["alpha"] = 1.0
+    m[0]["tex_num"] = -1
+    return m
+
+
+def _mesh(tris, normals):
+    """rt.Scene from (n, 3, 3) positions and (n, 3) per-triangle vertex normals, one material."""
+    n = len(tris)
     v = np.zeros((3 * n, 8), np.float32)
-    v[:, :3] = (cen[:, None, :] + off).reshape(-1, 3)
+    v[:, :3] = tris.reshape(-1, 3)
+    v[:, 3:6] = np.repeat(normals, 3, axis=0)
+    return rt.Scene(v, np.arange(3 * n, dtype=np.uint32), np.zeros(n, np.uint32), _material())
+
+
+def _grid(n0, n1, lo0, lo1, step):
+    """Two triangles per cell of an n0 x n1 grid (cell corners at lo + step * i): (2 n0 n1, 3, 2)."""
+    i, j = np.meshgrid(np.arange(n0), np.arange(n1), indexing="ij")
+    a0, a1 = (lo0 + step * i).ravel(), (lo1 + step * j).ravel()
+    b0, b1 = a0 + step, a1 + step
+    t1 = np.stack([np.stack([a0, a1], 1), np.stack([b0, a1], 1), np.stack([b0, b1], 1)], 1)
+    t2 = np.stack([np.stack([a0, a1], 1), np.stack([b0, b1], 1), np.stack([a0, b1], 1)], 1)
+    return np.concatenate([t1, t2])
+
+
+def _far_wall_scene(big=True):
+    """Identity camera (clip space = object space; tests/containment.py): a mirror of small triangles
+    in the plane z = 10 over the frame, whose shading normal (~(0.70, 0.02, -0.714)) reflects the
+    primary rays (d = +z) to ~(1, 0.03, -0.02), and a wall of small triangles at x = 450 facing them:
+    almost every bounce ray's hit lies at t ~ 370..530.  With `big`, one huge triangle far outside every ray's path makes
+    the scene's largest edge ~1000: the scene-wide margin's range (margin.h tcap) is then negative --
+    round 4's certified walk could prune no bounce box by distance past t ~ 0 and walked exhaustively;
+    per-node margins (the mirror's and the wall's QNodes carry edges ~1.4, tcap ~ 840) prune as
+    usual."""
+    g = _grid(160, 120, -80.0, -60.0, 1.0)   # x, y
+    mirror = np.concatenate([g, np.full(g.shape[:2] + (1,), 10.0)], 2)
+    w = _grid(170, 40, -85.0, -20.0, 1.0)    # y, z
+    wall = np.concatenate([np.full(w.shape[:2] + (1,), 450.0), w], 2)
+    tris = [mirror, wall]
+    nrm = [np.tile([0.70, 0.02, -0.714], (len(mirror), 1)), np.tile([-1.0, 0.0, 0.0], (len(wall), 1))]
+    if big:
+        tris.append(np.array([[[0.0, 3000.0, 0.0], [1000.0, 3000.0, 0.0], [0.0, 3000.0, 1000.0]]]))
+        nrm.append(np.array([[0.0, -1.0, 0.0]]))
+    return _mesh(np.concatenate(tris).astype(np.float32), np.concatenate(nrm).astype(np.float32))
+
+
+def _counts(s, wvp, wv, W, H, flags):
+    with rt.Context(device=0, flags=flags | rt.FLAG_COUNT_VISITS) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        return c.read_framebuffer(), c.stats()
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_certified_walk_prunes_past_the_scene_margin_range(big):
+    """bounce hits past the scene-wide margin's range (margin.h tcap of the largest
+    edge; with `big` every t is past it).  The certified walk grows each box by its OWN node's margin
+    (the largest edge bound below it, carried by the QNode), so it still prunes by distance there: its
+    frame equals the reference order's (and the oracle's), its bounce visits stay within 1.3x the
+    unchecked 4-wide walk's (round 4's walk, which stopped pruning past the scene's range, visited every
+    box the rays crossed), and (almost) no ray is re-traced."""
+    from tests.containment import identity_camera
+    s = _far_wall_scene(big)
+    wvp, wv = identity_camera()
+    W, H = 640, 480
+    ref, _ = _counts(s, wvp, wv, W, H, 0)
+    os_ = _oscene(s)
+    ofb, _, _ = orc.trace(os_, orc.build(os_, wvp), wvp, wv, W, H, 1, 0, H, 4)
+    np.testing.assert_array_equal(ref[0:H:4], ofb)
+    cert, cst = _counts(s, wvp, wv, W, H, rt.FLAG_CERTIFIED)
+    fast, fst = _counts(s, wvp, wv, W, H, TRACE_MODES["nearest+packet+wide"])
+    np.testing.assert_array_equal(cert, ref)
+    assert cst["bounce_rays"] > 200_000 and cst["hits"][1] > 0.9 * cst["bounce_rays"]
+    assert cst["redo_rays"][1] <= 0.001 * cst["bounce_rays"]
+    assert cst["internal_visits"][1] <= 1.3 * fst["internal_visits"][1], (cst["internal_visits"], fst["internal_visits"])
+
+
+def test_certified_walks_with_a_few_huge_triangles():
+    """one large triangle used to set the scene-wide edge bound, collapsing the margin's range
+    for every ray (every bounce ray re-traced in the reference order).  A C5-like 200k-triangle scene plus
+    three triangles of ~60-unit edges off to the side: the certified frame (RTBVH_FLAG_AUTO_WALK) equals
+    the reference order's, (almost) no bounce ray is re-traced, and the walk stays within 1.3x the unchecked
+    walk's visits -- only the few subtrees holding the huge triangles lose distance pruning."""
+    base = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    huge = np.array([[[-190, -190, 40], [-120, -190, 40], [-190, -120, 45]],
+                     [[190, 190, -40], [120, 190, -40], [190, 120, -45]],
+                     [[-190, 190, 0], [-150, 150, 30], [-120, 190, -30]]], np.float32)
+    v = np.zeros((9, 8), np.float32)
+    v[:, :3] = huge.reshape(-1, 3)
     v[:, 5] = -1.0
-    base = rt.synthetic(1, seed=1, half_extent=(1, 1, 1))
-    s = rt.Scene(v, np.arange(3 * n, dtype=np.uint32), np.zeros(n, np.uint32), base.material_blob)
-    W, H = 320, 240
+    V0 = len(base.vertices)
+    s = rt.Scene(np.concatenate([base.vertices, v]), np.concatenate([base.indices, V0 + np.arange(9, dtype=np.uint32)]),
+                 np.concatenate([base.mat_indices, np.zeros(3, np.uint32)]), base.materials)
+    W, H = 800, 450
+    wvp, wv = rt.camera_reference(W, H)
+    ref, _ = _counts(s, wvp, wv, W, H, 0)
+    auto, ast = _counts(s, wvp, wv, W, H, rt.FLAG_AUTO_WALK)
+    fast, fst = _counts(s, wvp, wv, W, H, TRACE_MODES["nearest+packet+wide"])
+    np.testing.assert_array_equal(auto, ref)
+    assert ast["walk_state"] == 2 and ast["bounce_rays"] > 0
+    assert ast["redo_rays"][1] <= 0.001 * ast["bounce_rays"]
+    assert ast["internal_visits"][1] <= 1.3 * fst["internal_visits"][1], (ast["internal_visits"], fst["internal_visits"])
+
+
+def test_certified_walks_flag_rays_they_cannot_take():
+    """Rays the certified bounce walk cannot vouch for are re-traced in the reference order: here the
+    bounce rays of triangles whose shading normal is (0, 0, -1) -- under the reference camera (WV's x
+    axis is exactly (1, 0, 0)) they reflect the primary rays' d = (0, 0, 1) into a direction with an
+    exact zero x component, |1/d.x| = inf, which the slack test (qnode_fast_ray) cannot take.  The frame
+    equals the reference's, and the re-trace count is the number of such rays."""
+    s = _flat_normal_scene()   # every 7th triangle's normals (0, 0, -1)
+    W, H = 640, 360
     with rt.Context(device=0) as ref, rt.Context(device=0, flags=rt.FLAG_AUTO_WALK) as auto:
         for c in (ref, auto):
             c.set_scene(s)
@@ -1079,7 +1221,64 @@ def test_certified_walks_flag_rays_past_the_margin():
         np.testing.assert_array_equal(auto.read_intensity(), ref.read_intensity())
         st = auto.stats()
         assert st["walk_state"] == 2 and st["bounce_rays"] > 0
-        assert st["redo_rays"][1] == st["bounce_rays"]
+        assert 0.05 * st["bounce_rays"] < st["redo_rays"][1] < 0.3 * st["bounce_rays"]
+
+
+def _flat_normal_scene():
+    s = rt.synthetic(200_000, seed=0x5EED0005, half_extent=(100, 100, 50))
+    v = s.vertices.copy()
+    v[(np.arange(len(v)) // 3) % 7 == 0, 3:6] = (0.0, 0.0, -1.0)
+    return rt.Scene(v, s.indices, s.mat_indices, s.materials)
+
+
+@pytest.mark.parametrize("nranks,share", [(2, 16), (3, 11), (8, 13)])
+def test_certified_band_traces_and_frames_in_flight(nranks, share):
+    """the certified walks on band traces (nranks > 1, the weighted deal) and on
+    caller-stream slots (frames in flight), with re-traced rays on every rank and slot: the per-slot
+    re-trace lists and k_primary_redo / k_bounce_redo's compact-row pixel index.  Each rank's bands,
+    traced alone and as three frames in flight, put back in their rows, give the reference-order frame;
+    bounce rays are re-traced on every rank (the scene's flat-normal triangles), and the containment
+    scene's primary pixel is re-traced on the rank that owns its row."""
+    import torch
+
+    from raytracebvh_amd.tiles import band_row_ids
+    from tests.containment import PIXEL, containment_scene, identity_camera
+    cases = [(_flat_normal_scene(), 640, 357, rt.camera_reference(640, 357), 1),
+             (containment_scene(), 64, 64, identity_camera(), 0)]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    for s, W, H, (wvp, wv), kind in cases:
+        with rt.Context(device=0) as ref, rt.Context(device=0, flags=rt.FLAG_CERTIFIED) as c:
+            for x in (ref, c):
+                x.set_scene(s)
+                x.set_camera(wvp, wv)
+                x.compute_bvh(W, H, 1)
+            want = ref.read_framebuffer()
+            np.testing.assert_array_equal(c.read_framebuffer(), want)
+            c.set_band_deal(share)
+            frame = np.zeros_like(want)
+            redo = []
+            for r in range(nranks):
+                rows = rt.lib().rtbvh_deal_rows(H, r, nranks, share)
+                alone = torch.full((rows, W, 4), -1.0, dtype=torch.float32, device="cuda:0")
+                bufs = [torch.full((rows, W, 4), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(3)]
+                torch.cuda.synchronize()
+                c.trace_band_async(W, H, 1, r, nranks, alone.data_ptr())
+                c.synchronize()
+                redo.append(c.stats()["redo_rays"][kind])
+                for i, b in enumerate(bufs):
+                    c.trace_band_async(W, H, 1, r, nranks, b.data_ptr(), stream_ptr=streams[i].cuda_stream)
+                c.synchronize()
+                torch.cuda.synchronize()
+                for i, b in enumerate(bufs):
+                    assert torch.equal(b, alone), (r, i)
+                assert c.stats()["redo_rays"][kind] == redo[-1]
+                frame[band_row_ids(H, r, nranks, share)] = alone.cpu().numpy()
+            np.testing.assert_array_equal(frame, want)
+            if kind == 1:
+                assert all(n > 0 for n in redo), redo
+            else:
+                owner = [r for r in range(nranks) if PIXEL[1] in band_row_ids(H, r, nranks, share)]
+                assert redo[owner[0]] >= 1, redo
 
 
 @pytest.mark.parametrize("nranks,share", [(2, 16), (3, 16), (8, 16), (3, 11), (8, 13)])

@@ -5,7 +5,8 @@ triangle test, build.hip quantize_axis, the certified slack test of trace.hip --
 itself) over C5-like triangles, grazing rays whose determinant sits just above the 0.01 rejection,
 flat and coplanar triangles, near-edge hits, the orthographic primary rays and several scales.  No
 accepted hit may lie farther than the margin, no certified box test may prune a box holding it, and no
-primary depth key may exceed its t.  With a margin 1000x too small the check must fail: it bites."""
+primary depth key may exceed its t; the per-node margins (a node's largest leaf edge bound and its margin
+range, coded in its QNode) bound every such hit of the leaves below the node.  With a margin 1000x too small the check must fail: it bites."""
 import json
 import os
 import subprocess
@@ -35,6 +36,9 @@ def test_margin_contains_every_accepted_hit(tmp_path, seed):
     assert r["walk_checked"] > 500_000 and r["zkey_checked"] > 100_000
     assert r["dist_violations"] == 0 and r["dist_violations_tight"] == 0, r
     assert r["walk_violations"] == 0 and r["zkey_violations"] == 0, r
+    # the per-node margins of the certified bounce walk (margin.h mt_node_codes / mt_node_rho, round 5)
+    assert r["node_checked"] > 1_000_000 and r["node_walk_checked"] > 500_000
+    assert r["node_violations"] == 0 and r["node_walk_violations"] == 0, r
     assert 0 < r["max_ratio"] < 1 and 0 < r["max_ratio_tight"] < 1
     assert rc == 0
 
@@ -42,3 +46,4 @@ def test_margin_contains_every_accepted_hit(tmp_path, seed):
 def test_margin_check_detects_a_small_margin(tmp_path):
     rc, r = _run(_build(tmp_path, "margin_check_small", ["-DMARGIN_SCALE=1e-3f"]), 200_000, 1)
     assert rc == 1 and r["dist_violations"] > 0 and r["max_ratio"] > 1, r
+    assert r["node_violations"] > 0, r

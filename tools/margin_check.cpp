@@ -10,7 +10,12 @@
 //  * walk: the bounce walk's expanded slack test (trace.hip qaxis with the margin, qbox_fast) on a
 //    quantized box containing the triangle passes at any bound best >= t, whenever the exact box passes
 //    the reference slab test -- so the certified walk never prunes a box holding a hit it must see;
-//  * zkey: for the primary rays, the leaf's depth key (margin.h mt_primary_zkey) is <= t.
+//  * zkey: for the primary rays, the leaf's depth key (margin.h mt_primary_zkey) is <= t;
+//  * node: the per-node margin of the certified bounce walk (margin.h mt_node_codes / mt_node_rho, round 5):
+//    for a node whose leaves' largest edge bound E_n >= the triangle's own, the decoded E_n >= E_n, the
+//    decoded range tcap_n <= mt_margin(E_n).tcap, rho_n(t) >= mt_margin(E_n)'s rho(t) at every t <= tcap_n,
+//    and the real point lies within rho_n(t) of the box whenever t <= tcap_n; and the walk's expanded
+//    slack test with the node's margin at any bound best in [t, tcap_n] passes.
 // Restates the device arithmetic with the same fp32 operations (-ffp-contract=off).  Reports the worst
 // ratio of the real distance to the margin (how tight the bound is).  Built with -DMARGIN_SCALE=1e-3f
 // (a margin 1000x too small) it must find violations: the check bites.  Used by tests/test_margin.py.
@@ -142,7 +147,8 @@ V unit(double x, double y, double z) {
 
 struct Stats {
     long tests = 0, accepted = 0, dist_checked = 0, dist_viol = 0, dist_viol_tight = 0, walk_checked = 0,
-         walk_viol = 0, zkey_checked = 0, zkey_viol = 0, uncovered = 0;
+         walk_viol = 0, zkey_checked = 0, zkey_viol = 0, uncovered = 0, node_checked = 0, node_viol = 0,
+         node_walk_checked = 0, node_walk_viol = 0;
     double max_ratio = 0, max_ratio_tight = 0;
 };
 
@@ -218,6 +224,49 @@ void check(Stats& s, Rng& rng, V o, V d, V p0, V p1, V p2, bool primary) {
         } else {
             ++s.uncovered;
         }
+    }
+    // the per-node margin: a node above this triangle, whose largest edge bound is E or larger
+    if (dd <= MT_DD) {
+        const float En = rng.next() % 3 ? E : E * (float)(1.0 + 3.0 * rng.u01());
+        uint32_t ce, ct;
+        mt_node_codes(En, ce, ct);
+        const float Eq = mt_code_val(ce), tcn = mt_code_val(ct);
+        const MtMargin mn = mt_margin(En, MT_LAMBDA, MT_A);
+        const MtNodeK nk = mt_node_consts();
+        ++s.node_checked;
+        // (a negative range covers no t > EPSILON either way: the codes keep -1)
+        bool bad = !(Eq >= En) || !(tcn <= mn.tcap || (tcn < 0.f && mn.tcap < 0.f));
+        if (t <= tcn) {
+            const float rn = mt_node_rho(nk, Eq, t) * MARGIN_SCALE;
+            if (!(rn >= mn.r1 * t + mn.r0) && MARGIN_SCALE == 1.0f) bad = true;
+            if (dist > rn) bad = true;
+            // the walk's expanded test with the node's margin at a bound best in [t, tcap_n]
+            const float o3[3] = {o.x, o.y, o.z};
+            const float inv[3] = {1.f / d.x, 1.f / d.y, 1.f / d.z};
+            if (fast_ray(o3, inv) && slab(o3, inv, lo, hi)) {
+                float org[3], scl[3];
+                uint32_t lw[3] = {0, 0, 0}, hw[3] = {0, 0, 0};
+                bool ok = true;
+                for (int a = 0; a < 3; a++) {
+                    float clo[4] = {lo[a], lo[a], lo[a], lo[a]}, chi[4] = {hi[a], hi[a], hi[a], hi[a]};
+                    const float w = (hi[a] - lo[a]) + 1.f;
+                    clo[3] = lo[a] - (float)rng.u01() * 8.f * w;   // a sibling stretching the grid
+                    uint32_t ql[4], qh[4];
+                    ok = quantize_axis(clo, chi, org[a], scl[a], ql, qh) && ok;
+                    for (int c = 0; c < 4; c++) { lw[a] |= ql[c] << (8 * c); hw[a] |= qh[c] << (8 * c); }
+                }
+                float best = rng.next() % 2 ? t : t * (float)(1.0 + rng.u01());
+                if (ok && best <= tcn) {
+                    const float rr = mt_node_rho(nk, Eq, best) * MARGIN_SCALE;
+                    const QAxis X = qaxis(org[0], scl[0], lw[0], hw[0], o.x, inv[0], rr);
+                    const QAxis Y = qaxis(org[1], scl[1], lw[1], hw[1], o.y, inv[1], rr);
+                    const QAxis Z = qaxis(org[2], scl[2], lw[2], hw[2], o.z, inv[2], rr);
+                    ++s.node_walk_checked;
+                    if (!qbox_fast(X, Y, Z, 0, best)) ++s.node_walk_viol;
+                }
+            }
+        }
+        if (bad) ++s.node_viol;
     }
     // the build's per-triangle margin (L = 1/|det|): the primary rays' depth keys
     {
@@ -317,8 +366,10 @@ int main(int argc, char** argv) {
     }
     printf("{\"tests\": %ld, \"accepted\": %ld, \"dist_checked\": %ld, \"dist_violations\": %ld, "
            "\"dist_violations_tight\": %ld, \"walk_checked\": %ld, \"walk_violations\": %ld, \"zkey_checked\": %ld, "
-           "\"zkey_violations\": %ld, \"uncovered\": %ld, \"max_ratio\": %.6g, \"max_ratio_tight\": %.6g}\n",
+           "\"zkey_violations\": %ld, \"uncovered\": %ld, \"max_ratio\": %.6g, \"max_ratio_tight\": %.6g, "
+           "\"node_checked\": %ld, \"node_violations\": %ld, \"node_walk_checked\": %ld, \"node_walk_violations\": %ld}\n",
            s.tests, s.accepted, s.dist_checked, s.dist_viol, s.dist_viol_tight, s.walk_checked, s.walk_viol,
-           s.zkey_checked, s.zkey_viol, s.uncovered, s.max_ratio, s.max_ratio_tight);
-    return (s.dist_viol || s.dist_viol_tight || s.walk_viol || s.zkey_viol) ? 1 : 0;
+           s.zkey_checked, s.zkey_viol, s.uncovered, s.max_ratio, s.max_ratio_tight, s.node_checked, s.node_viol,
+           s.node_walk_checked, s.node_walk_viol);
+    return (s.dist_viol || s.dist_viol_tight || s.walk_viol || s.zkey_viol || s.node_viol || s.node_walk_viol) ? 1 : 0;
 }
