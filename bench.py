@@ -134,6 +134,16 @@ def load_pmc(workload, mode, kernel):
         return None
 
 
+def load_pmc_meta(workload, mode):
+    """The PMC profile's header (its commit, source directory), or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_{workload}_{mode}.json")
+    try:
+        d = json.load(open(path))
+        return {"commit": d.get("commit"), "source": d.get("source")}
+    except Exception:
+        return None
+
+
 def build_pmc(workload, mode):
     """Summed per-launch HBM bytes of the build kernels in the same PMC profile, or None."""
     path = os.path.join(REPO, "profiles", f"pmc_{workload}_{mode}.json")
@@ -529,8 +539,12 @@ def main():
                 "bytes_model": "algorithmic_bytes / requested_*: this layout's bytes, 64 B per record fetch (QNode, "
                                "child-pair record, leaf record; a 4-wide primary step = 2) + per-ray queue/hit/colour "
                                "bytes (DESIGN.md 7.1); L2 and the Infinity Cache serve part of them",
-                "traffic_source": f"PMC profiles/pmc_{args.workload}_{use_name}.json (N=1), per record fetch x "
-                                  f"this launch's {recs[dom]} record fetches" if measured else None}
+                "traffic_source": f"PMC profiles/pmc_{args.workload}_{use_name}.json (N=1, collected at commit "
+                                  f"{(load_pmc_meta(args.workload, use_name) or {}).get('commit')}), per record fetch x "
+                                  f"this launch's {recs[dom]} record fetches" if measured else None,
+                "kernel_trace_source": "profiles/r05_*_one_frame_kernel_stats.csv: rocprofv3 --kernel-trace --stats of "
+                                       "scripts/profile_trace.py in the same mode, one frame at a time (kernel_ms is "
+                                       "this run's HIP-event duration of the same launch, one frame at a time)"}
     if measured:
         roofline["cache_served_frac"] = round(max(0.0, 1.0 - kd["traffic"] / kd["bytes"]), 4)
     pm = load_pmc(args.workload, use_name, dom)

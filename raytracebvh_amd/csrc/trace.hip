@@ -908,11 +908,25 @@ constexpr uint32_t PB_RASTER_BLOCK = RTBVH_PB_RASTER_BLOCK;   // threads per til
 #ifndef RTBVH_PB_ROWMAJOR
 #define RTBVH_PB_ROWMAJOR 0   // the fine phase's lanes: 0 = 8x8 / 16x4 / 32x2 pixel blocks, 1 = row-major (A/B)
 #endif
-template <bool COUNT>
+template <bool COUNT, bool CERT, uint32_t NT, class KeyAt>
+__device__ __forceinline__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at, RayQ* __restrict__ q,
+                                              uint32_t* __restrict__ qcount, int emit, uint32_t* __restrict__ redo,
+                                              uint32_t* __restrict__ redo_count, uint32_t* s_cnt, uint64_t* s_mask,
+                                              uint32_t& s_base);
+// FUSE (RTBVH_PB_FUSE builds, A/B): the tile's shading (k_pb_shade's work, pb_shade_tile) at the end of the
+// same workgroup, from the keys in LDS -- no keys round trip through HBM, one launch fewer, and a tile's
+// dependent shading gathers run beside other tiles' rasterisation on the CU
+#ifndef RTBVH_PB_FUSE
+#define RTBVH_PB_FUSE 0
+#endif
+template <bool COUNT, bool CERT = false, bool FUSE = false>
 __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
                                                              const uint4* __restrict__ bins, uint32_t cap,
                                                              uint32_t ntx, uint32_t rows,
-                                                             unsigned long long* __restrict__ keys) {
+                                                             unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
+                                                             uint32_t* __restrict__ qcount, int emit,
+                                                             uint32_t* __restrict__ redo,
+                                                             uint32_t* __restrict__ redo_count) {
     __shared__ unsigned long long s_key[PB_TILE * PB_KS];
     __shared__ float s_bmax[(PB_TILE / 8) * (PB_TILE / 8)];
     __shared__ uint32_t s_q[PB_RASTER_BLOCK / 64][PB_QCAP];
@@ -1075,10 +1089,19 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs
         PB_T(5);
     }
     __syncthreads();
-    // the tile's keys, row segments of 32 pixels
-    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += PB_RASTER_BLOCK) {
-        const uint32_t px = i % PB_TILE, py = i / PB_TILE;
-        if (X0 + px < a.W && C0 + py < rows) keys[(size_t)(C0 + py) * a.W + X0 + px] = s_key[py * PB_KS + px];
+    if (FUSE) {
+        __shared__ uint32_t s_cnt[(PB_TILE / 8) * (PB_TILE / 8)];
+        __shared__ uint64_t s_mask[2 * (PB_TILE / 8) * (PB_TILE / 8)];
+        __shared__ uint32_t s_base;
+        pb_shade_tile<COUNT, CERT, PB_RASTER_BLOCK>(
+            a, rows, [&](uint32_t crow, uint32_t x) { return s_key[(crow - C0) * PB_KS + (x - X0)]; }, q, qcount, emit,
+            redo, redo_count, s_cnt, s_mask, s_base);
+    } else {
+        // the tile's keys, row segments of 32 pixels
+        for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += PB_RASTER_BLOCK) {
+            const uint32_t px = i % PB_TILE, py = i / PB_TILE;
+            if (X0 + px < a.W && C0 + py < rows) keys[(size_t)(C0 + py) * a.W + X0 + px] = s_key[py * PB_KS + px];
+        }
     }
 #ifdef RTBVH_PB_PROF
     PB_T(6);
@@ -1106,57 +1129,58 @@ constexpr uint32_t PB_SHADE_BLOCK = RTBVH_PB_SHADE_BLOCK;
 // the leaf's own box passes the reference slab test with the bound t (k_bounce_shade's leaf_certified,
 // here from the leaf record's box).  Pixels that fail it go to the re-trace list (redo: compact pixel
 // index) and are left to k_primary_redo, outside the block's bounce-queue claim.
-template <bool COUNT, bool CERT>
-__global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, const uint32_t* __restrict__ off, uint32_t cap,
-                                                    uint32_t ntx, uint32_t rows,
-                                                    const unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
-                                                    uint32_t* __restrict__ qcount, int emit,
-                                                    uint32_t* __restrict__ redo, uint32_t* __restrict__ redo_count) {
-    __shared__ uint32_t s_cnt[(PB_TILE / 8) * (PB_TILE / 8)];
-    __shared__ uint32_t s_base;
+// One tile of k_pb_shade's work over NT threads, the pixels' keys from key_at(compact row, x).  s_cnt: 16
+// words of LDS, s_mask: 2 x 16 words, s_base: one.  The 16 sub-tiles of 8 x 8 pixels go to the waves in
+// turn; a first pass counts each one's live rays (and certificates) into LDS, the tile claims its queue
+// range, then a second pass shades them (no per-sub-tile registers held across the claim).
+template <bool COUNT, bool CERT, uint32_t NT, class KeyAt>
+__device__ __forceinline__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at, RayQ* __restrict__ q,
+                                              uint32_t* __restrict__ qcount, int emit, uint32_t* __restrict__ redo,
+                                              uint32_t* __restrict__ redo_count, uint32_t* s_cnt, uint64_t* s_mask,
+                                              uint32_t& s_base) {
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t tile = blockIdx.y * ntx + blockIdx.x;
-    if (off[(tile + 1) * PB_NZ] > cap) return;
     const uint32_t X0 = blockIdx.x * PB_TILE, C0 = blockIdx.y * PB_TILE;
-    constexpr uint32_t NST = (PB_TILE / 8) * (PB_TILE / 8) / (PB_SHADE_BLOCK / 64);   // sub-tiles per wave
-    uint32_t x[NST], crow[NST];
-    uint64_t key[NST];
-    bool valid[NST];
-    uint64_t livem[NST], flagm[NST];
+    constexpr uint32_t NST = (PB_TILE / 8) * (PB_TILE / 8) / (NT / 64);   // sub-tiles per wave
+    constexpr uint32_t NSUB = (PB_TILE / 8) * (PB_TILE / 8);
     const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
-#pragma unroll
-    for (uint32_t i = 0; i < NST; i++) {
-        const uint32_t st = w + i * (PB_SHADE_BLOCK / 64);
-        x[i] = X0 + (st % (PB_TILE / 8)) * 8 + (lane & 7u);
-        crow[i] = C0 + (st / (PB_TILE / 8)) * 8 + (lane >> 3);
-        valid[i] = x[i] < a.W && crow[i] < rows;
-        key[i] = valid[i] ? keys[(size_t)crow[i] * a.W + x[i]] : NO_HIT;
-    }
+    const auto pixel = [&](uint32_t i, uint32_t& x, uint32_t& crow) {
+        const uint32_t st = w + i * (NT / 64);
+        x = X0 + (st % (PB_TILE / 8)) * 8 + (lane & 7u);
+        crow = C0 + (st / (PB_TILE / 8)) * 8 + (lane >> 3);
+        return x < a.W && crow < rows;
+    };
     // the live reflection rays: hit, and the hit material's shininess > 0
-#pragma unroll
+#pragma unroll 1
     for (uint32_t i = 0; i < NST; i++) {
+        uint32_t x, crow;
+        const bool valid = pixel(i, x, crow);
+        const uint64_t key = valid ? key_at(crow, x) : NO_HIT;
         bool live = false, flag = false;
-        if (CERT && key[i] != NO_HIT) {   // the certificate: the leaf's box, the reference slab test at t
-            const float4 b2 = a.leaf[4 * (size_t)(uint32_t)key[i] + 2], b3 = a.leaf[4 * (size_t)(uint32_t)key[i] + 3];
-            const f3 o = mk(((float)x[i] - hw) / 4.f, ((float)pb_image_row(a, crow[i]) - hh) / 4.f, 0.f);
+        if (CERT && key != NO_HIT) {   // the certificate: the leaf's box, the reference slab test at t
+            const float4 b2 = a.leaf[4 * (size_t)(uint32_t)key + 2], b3 = a.leaf[4 * (size_t)(uint32_t)key + 3];
+            const f3 o = mk(((float)x - hw) / 4.f, ((float)pb_image_row(a, crow) - hh) / 4.f, 0.f);
             const f3 d = mk(0.f, 0.f, 1.f);
             float tm;
             flag = !ray_box(o, mk(1.f / d.x, 1.f / d.y, 1.f / d.z), b2.z, b2.w, b3.x, b3.y, b3.z, b3.w, true,
-                            key_t(key[i]), tm);
+                            key_t(key), tm);
         }
-        flagm[i] = CERT ? __ballot(flag) : 0ull;
-        if (emit && key[i] != NO_HIT && !flag) {
-            const uint32_t tri = __float_as_uint(a.leaf[4 * (size_t)(uint32_t)key[i] + 2].y) & ~LEAF_BIT;
+        if (emit && key != NO_HIT && !flag) {
+            const uint32_t tri = __float_as_uint(a.leaf[4 * (size_t)(uint32_t)key + 2].y) & ~LEAF_BIT;
             const uint32_t mi = TCS == 4 ? __float_as_uint(a.tclip[TCS * (size_t)tri + 3].w) : a.matidx[tri];
             live = 0 < a.mats[mi].shininess / 1000.f * 1;
         }
-        livem[i] = __ballot(live);
-        if (lane == 0) s_cnt[w + i * (PB_SHADE_BLOCK / 64)] = (uint32_t)__popcll(livem[i]);
+        const uint64_t livem = __ballot(live), flagm = CERT ? __ballot(flag) : 0ull;
+        const uint32_t st = w + i * (NT / 64);
+        if (lane == 0) {
+            s_cnt[st] = (uint32_t)__popcll(livem);
+            s_mask[st] = livem;
+            s_mask[NSUB + st] = flagm;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t run = 0;
-        for (uint32_t k = 0; k < (PB_TILE / 8) * (PB_TILE / 8); k++) {
+        for (uint32_t k = 0; k < NSUB; k++) {
             const uint32_t v = s_cnt[k];
             s_cnt[k] = run;
             run += v;
@@ -1165,30 +1189,49 @@ __global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, con
     }
     __syncthreads();
     uint32_t hits = 0, tex = 0;
-#pragma unroll
+#pragma unroll 1
     for (uint32_t i = 0; i < NST; i++) {
-        const bool flag = CERT && ((flagm[i] >> lane) & 1u);
-        if (CERT && flagm[i]) {   // (rare) the re-trace list, one atomic per wave
+        uint32_t x, crow;
+        const bool valid = pixel(i, x, crow);
+        const uint32_t st = w + i * (NT / 64);
+        const uint64_t livem = s_mask[st], flagm = CERT ? s_mask[NSUB + st] : 0ull;
+        const bool flag = CERT && ((flagm >> lane) & 1u);
+        if (CERT && flagm) {   // (rare) the re-trace list, one atomic per wave
             const uint32_t slot = wave_append(flag, redo_count);
-            if (flag) redo[slot] = crow[i] * a.W + x[i];
+            if (flag) redo[slot] = crow * a.W + x;
         }
-        if (valid[i] && !flag) {
-            const f3 o = mk(((float)x[i] - hw) / 4.f, ((float)pb_image_row(a, crow[i]) - hh) / 4.f, 0.f);
-            const bool phit = key[i] != NO_HIT;
+        if (valid && !flag) {
+            const uint64_t key = key_at(crow, x);
+            const f3 o = mk(((float)x - hw) / 4.f, ((float)pb_image_row(a, crow) - hh) / 4.f, 0.f);
+            const bool phit = key != NO_HIT;
             uint32_t h1 = 0, t1 = 0;
             RayQ e;
-            const bool live = primary_pixel(a, (size_t)crow[i] * a.W + x[i], o, mk(0.f, 0.f, 1.f), phit,
-                                            phit ? key_t(key[i]) : 0.f, phit ? (uint32_t)key[i] : 0u, h1, t1, e);
+            const bool live = primary_pixel(a, (size_t)crow * a.W + x, o, mk(0.f, 0.f, 1.f), phit,
+                                            phit ? key_t(key) : 0.f, phit ? (uint32_t)key : 0u, h1, t1, e);
             hits += h1;
             tex += t1;
-            if (emit && live)
-                q[s_base + s_cnt[w + i * (PB_SHADE_BLOCK / 64)] + (uint32_t)__popcll(livem[i] & ((1ull << lane) - 1))] = e;
+            if (emit && live) q[s_base + s_cnt[st] + (uint32_t)__popcll(livem & ((1ull << lane) - 1))] = e;
         }
     }
     if (COUNT) {
         Counts c = {0, 0, 0, 0, 0};
         flush_counts<COUNT>(a, c, hits, tex, 2);
     }
+}
+template <bool COUNT, bool CERT>
+__global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, const uint32_t* __restrict__ off, uint32_t cap,
+                                                    uint32_t ntx, uint32_t rows,
+                                                    const unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
+                                                    uint32_t* __restrict__ qcount, int emit,
+                                                    uint32_t* __restrict__ redo, uint32_t* __restrict__ redo_count) {
+    __shared__ uint32_t s_cnt[(PB_TILE / 8) * (PB_TILE / 8)];
+    __shared__ uint64_t s_mask[2 * (PB_TILE / 8) * (PB_TILE / 8)];
+    __shared__ uint32_t s_base;
+    const uint32_t tile = blockIdx.y * ntx + blockIdx.x;
+    if (off[(tile + 1) * PB_NZ] > cap) return;
+    pb_shade_tile<COUNT, CERT, PB_SHADE_BLOCK>(
+        a, rows, [&](uint32_t crow, uint32_t x) { return keys[(size_t)crow * a.W + x]; }, q, qcount, emit, redo,
+        redo_count, s_cnt, s_mask, s_base);
 }
 
 // The reference-order re-trace of the pixels a certified primary pass flagged (redo: compact pixel
@@ -1442,8 +1485,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          unsigned long long* __restrict__ overflow, int stack_limit,
-                                                          const float* __restrict__ rootbox) {
+                                                          unsigned long long* __restrict__ overflow, int stack_limit) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
@@ -2015,7 +2057,7 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
 #define RTBVH_BT(L, G, C)                                                                                              \
     hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
-                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, a.rootbox)
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
     if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
@@ -2068,19 +2110,23 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
     hipLaunchKernelGGL(k_pb_scan, dim3(sb), dim3(PB_SCAN), 0, s, pb.off, pb.cur, pb.sums, keys);
     hipLaunchKernelGGL((k_pb_bin<true>), lg, dim3(BLOCK), 0, s, a, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
     const dim3 grid(pb.ntx, pb.nty);
-    if (count)
-        hipLaunchKernelGGL((k_primary_binned<true>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
-                           pb.keys);
-    else
-        hipLaunchKernelGGL((k_primary_binned<false>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows,
-                           pb.keys);
     uint32_t* rl = redo ? redo->list : nullptr;
     uint32_t* rc = redo ? redo->count : nullptr;
+#define RTBVH_PBR(C, R, F)                                                                                          \
+    hipLaunchKernelGGL((k_primary_binned<C, R, F>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off, pb.bins, pb.cap,    \
+                       pb.ntx, rows, pb.keys, q, qcount, (int)emit, rl, rc)
 #define RTBVH_PBS(C, R)                                                                                              \
     hipLaunchKernelGGL((k_pb_shade<C, R>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q, \
                        qcount, (int)emit, rl, rc)
+#if RTBVH_PB_FUSE
+    if (count) { if (redo) RTBVH_PBR(true, true, true); else RTBVH_PBR(true, false, true); }
+    else { if (redo) RTBVH_PBR(false, true, true); else RTBVH_PBR(false, false, true); }
+#else
+    if (count) RTBVH_PBR(true, false, false); else RTBVH_PBR(false, false, false);
     if (count) { if (redo) RTBVH_PBS(true, true); else RTBVH_PBS(true, false); }
     else { if (redo) RTBVH_PBS(false, true); else RTBVH_PBS(false, false); }
+#endif
+#undef RTBVH_PBR
 #undef RTBVH_PBS
     if (redo) {   // the flagged pixels, in the reference order
         const dim3 rg(REDO_BLOCKS);

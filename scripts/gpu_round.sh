@@ -21,8 +21,10 @@ if [ -z "$SKIP_PMC" ]; then
   cp gpurun_out/pmc_c5_round.json profiles/pmc_c5_$PMC_NAME.json
   echo "pmc ok"
 fi
-timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench.err; exit 1; }
-cat gpurun_out/bench.json
+if [ -z "$SKIP_BENCH" ]; then
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench.err; exit 1; }
+  cat gpurun_out/bench.json
+fi
 if [ -z "$SKIP_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_bench -o run -- python3 $R/bench.py ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err || { echo "PROF FAILED"; tail -20 gpurun_out/prof_bench.err; exit 1; }
   echo "prof ok"

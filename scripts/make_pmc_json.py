@@ -12,7 +12,7 @@ FETCH_SIZE (= RDREQ x 64 B) reports exactly the record bytes.  Counters are summ
 over the TCC channels and averaged over the profiled dispatches of each kernel.
 records_per_launch (optional COUNTS.json: the stats of one PROF_COUNTS trace of the same mode)
 is each kernel's record fetches, so bench.py can scale the bytes to another launch's fetches.
-Usage: make_pmc_json.py PMC_DIR MODE WORKLOAD OUT.json [COUNTS.json]"""
+Usage: make_pmc_json.py PMC_DIR MODE WORKLOAD OUT.json [COUNTS.json]   (env PMC_COMMIT: the code's commit)"""
 import collections
 import csv
 import glob
@@ -64,7 +64,7 @@ if parts:
     kern["k_primary_pass"] = {"instance": parts, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                               "hbm_bytes_per_launch": rd + wr,
                               "records_per_launch": counts["bin_entries"][0] if counts else None}
-json.dump({"workload": workload, "mode": mode, "source": d,
+json.dump({"workload": workload, "mode": mode, "source": d, "commit": os.environ.get("PMC_COMMIT"),
            "method": __doc__.split("Usage")[0].strip(), "kernels": kern}, open(out, "w"), indent=1)
 for k, v in kern.items():
     print(k, v["instance"], "%.3f GB read, %.3f GB write" % (v["hbm_read_bytes_per_launch"] / 1e9,

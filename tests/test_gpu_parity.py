@@ -1133,7 +1133,7 @@ def _far_wall_scene(big=True):
     round 4's certified walk could prune no bounce box by distance past t ~ 0 and walked exhaustively;
     per-node margins (the mirror's and the wall's QNodes carry edges ~1.4, tcap ~ 840) prune as
     usual."""
-    g = _grid(160, 120, -80.0, -60.0, 1.0)   # x, y
+    g = _grid(161, 121, -80.1, -60.1, 1.0)   # x, y (no cell edge on the primary rays' quarter grid)
     mirror = np.concatenate([g, np.full(g.shape[:2] + (1,), 10.0)], 2)
     w = _grid(170, 40, -85.0, -20.0, 1.0)    # y, z
     wall = np.concatenate([np.full(w.shape[:2] + (1,), 450.0), w], 2)
