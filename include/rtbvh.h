@@ -355,7 +355,12 @@ rtbvh_status rtbvh_read_wide(rtbvh_ctx* ctx, uint32_t* records, uint64_t capacit
  * slots of leaves unused): words 0-2 grid origin xyz, 3-5 grid step xyz (f32; step x ==
  * 0: not quantized), 6-8 lo bytes x/y/z, 9-11 hi bytes x/y/z (byte c = grandchild c),
  * 12-15 grandchildren (slot, 0x80000000 | leaf, or 0xFFFFFFFF); decoded corner = origin +
- * q * step.  capacity in records (>= 2n-1). */
+ * q * step.  The low 16 bits of words 4 and 5 carry the certified walk's margin codes (the
+ * largest edge bound of the node's leaves and its margin range, as the high half of an f32):
+ * mask them off (& 0xFF800000) to read the steps.  Only the QNodes the walk reads are
+ * written -- the root's and, recursively, those of the internal grandchildren listed in words
+ * 12-15 (a build of more than 2048 triangles leaves the others untouched); capacity in records
+ * (>= 2n-1). */
 rtbvh_status rtbvh_read_qnodes(rtbvh_ctx* ctx, uint32_t* nodes, uint64_t capacity);
 /* Per-triangle Morton codes in triangle order (MortonCodes.hlsl:104-112). */
 rtbvh_status rtbvh_read_morton(rtbvh_ctx* ctx, uint32_t* codes);

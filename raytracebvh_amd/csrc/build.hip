@@ -34,9 +34,6 @@ constexpr uint32_t BLOCK = 256;
 // leaves (and node indices) per k_refit workgroup: the nodes whose leaf range lies inside
 // one join in LDS; the others ("crossing") climb in k_refit_top
 constexpr uint32_t RBLOCK = RTBVH_REFIT_BLOCK;
-#ifndef RTBVH_REFIT_STAGE
-#define RTBVH_REFIT_STAGE 1   // k_refit phase 4: records, pseudo-records and QNodes out through LDS
-#endif
 #ifndef RTBVH_REFIT_STAGE_SLOTS
 #define RTBVH_REFIT_STAGE_SLOTS 512   // slots per phase-4 round (32 KB; C4 A/B: 256 and 512 alike, 1024 slower)
 #endif
@@ -600,7 +597,7 @@ __device__ __forceinline__ void qent_sel(QEnt& d, const QEnt& s, bool take) {
 // Kids(e, c0, c1): the two children of internal entry e
 template <class Kids>
 __device__ __forceinline__ void greedy_qnode_words(const QEnt& e0, const QEnt& e1, Kids&& kids, float edge,
-                                                   float4 (&out)[4]) {
+                                                   float4 (&out)[4], uint32_t (&ent)[4]) {
     QEnt E[4] = {e0, e1, e0, e0};
     uint32_t n = 2;
 #pragma unroll
@@ -642,6 +639,10 @@ __device__ __forceinline__ void greedy_qnode_words(const QEnt& e0, const QEnt& e
     }
     if (absent1) id[1] = INVALID;
     if (absent3) id[3] = INVALID;
+#pragma unroll
+    for (int k = 0; k < 4; k++) ent[k] = P[k].id;   // the entries as node ids (internal k, LEAF_BIT | j)
+    if (absent1) ent[1] = INVALID;
+    if (absent3) ent[3] = INVALID;
     qnode_words(lx, ly, lz, hx, hy, hz, make_uint4(id[0], id[1], id[2], id[3]), edge, out);
 }
 // entries from the node records in global memory (record words: rtbvh_device.h)
@@ -665,7 +666,9 @@ __device__ __forceinline__ void qnode_from_records(Inner* __restrict__ rec, uint
     QEnt e0, e1;
     record_kids(rec, slot, e0, e1);
     float4 w[4];
-    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { record_kids(rec, e.slot, c0, c1); }, E, w);
+    uint32_t ent[4];
+    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { record_kids(rec, e.slot, c0, c1); }, E, w,
+                       ent);
     store4(dst, w);
     if (PSEUDO_NOGRID && w[0].w == 0.f) {
         if (e0.id & LEAF_BIT)
@@ -854,10 +857,10 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     if (tid == 0) a.xcnt[blockIdx.x] = s_xn;
     // 3. the block's in-block nodes: record, leaf pseudo-records, QNode
     const bool mine = i + 1 < T && !xnode;
-    if (!RTBVH_REFIT_STAGE && !mine) return;
     f3 l0 = mk(0.f, 0.f, 0.f), l1 = l0, r0 = l0, r1 = l0;
     uint32_t slot = INVALID;
     float4 rw[4], qw[4];
+    uint32_t ent[4] = {INVALID, INVALID, INVALID, INVALID};
     if (mine) {
     const float* L = s_box[tid][0];
     const float* R = s_box[tid][1];
@@ -881,16 +884,45 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     QEnt e0, e1;
     lds_kids(i, e0, e1);
     const float E = __uint_as_float(s_cnt[tid] & 0x7FFFFFFFu);   // the node's edge bound (the climb's ticket)
-    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, E, qw);
+    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, E, qw, ent);
     }
-    if (!RTBVH_REFIT_STAGE) {
-        store4(a.rec + slot, rw);
-        const bool pw = mine && (PSEUDO || qw[0].w == 0.f);   // (no grid: the bounce walk reads them)
-        if (pw && (q.x & LEAF_BIT)) store_leaf_record(a.rec, i, 0, q.x, l0, l1);
-        if (pw && (q.y & LEAF_BIT)) store_leaf_record(a.rec, i, 1, q.y, r0, r1);
-        store4(a.qnode + slot, qw);
-        return;
+    // Which of the block's QNodes the 4-wide walk reads: it steps from a QNode to its internal
+    // entries only, so a node's QNode is read iff the node is the root or an entry of a read QNode.  A QNode's
+    // entries lie 1..3 levels below its node, so every node within 3 levels below a node the block does not own
+    // (the root's parent, a crossing node, whose QNode k_qnodes_cross builds) is taken as read, and the rest is
+    // decided top-down inside the block, one QNode level per round.  Of the others (about two in three: the
+    // greedy collapse expands them) no QNode is written.
+    uint32_t* s_read = s_cnt;   // (the edge bounds were read above)
+    __syncthreads();
+    {
+        bool near = false;
+        uint32_t x = i;
+        for (int up = 0; mine && up < 3 && !near; up++) {
+            const uint32_t e = s_pint[x - base];
+            const uint32_t p = e >> 1;
+            near = e == INVALID || !(p >= base && p < end) || !(s_topo[p - base].z >= base && s_topo[p - base].w < end);
+            x = p;
+        }
+        s_read[tid] = mine && near ? 1u : 0u;
     }
+    bool pending = mine;   // its entries are not marked yet
+    for (;;) {
+        __syncthreads();
+        bool changed = false;
+        if (pending && s_read[tid]) {
+            pending = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t e = ent[k];   // (an internal entry of an owned node is owned)
+                if (e != INVALID && !(e & LEAF_BIT) && s_read[e - base] == 0) {
+                    s_read[e - base] = 1;
+                    changed = true;
+                }
+            }
+        }
+        if (!__syncthreads_or(changed)) break;
+    }
+    const bool rd = mine && s_read[tid] != 0;
     // 4. the outputs through LDS.  Every slot this block writes in phase 3 lies in its window
     // [2 base, 2 base + 2 RBLOCK) -- a node's record / QNode at 2 parent + side with the parent in
     // the block, a leaf child's pseudo-record at 2 i + side -- except the record and QNode of a
@@ -908,7 +940,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     const bool rin = mine && slot - w0 < 2 * RBLOCK;
     if (mine && !rin) {
         store4(a.rec + slot, rw);
-        store4(a.qnode + slot, qw);
+        if (rd) store4(a.qnode + slot, qw);
     }
     const uint32_t nslots = 2 * T - 1;
 #pragma unroll
@@ -928,10 +960,10 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
                     atomicOr(&s_own[k >> 5], 1u << (k & 31));
                 }
             };
-            if (rin) put(slot, kind ? qw : rw);
+            if (rin && (kind == 0 || rd)) put(slot, kind ? qw : rw);
             // the leaf children's pseudo-records: all (PSEUDO), or those of a node whose QNode has no
-            // grid (the bounce walk reads that node's exact record pair)
-            if (kind == 0 && mine && (PSEUDO || qw[0].w == 0.f)) {
+            // grid and is read (the bounce walk reads that node's exact record pair)
+            if (kind == 0 && mine && (PSEUDO || (qw[0].w == 0.f && rd))) {
                 float4 pw[4];
                 if (q.x & LEAF_BIT) { pseudo_words(q.x, l0, l1, pw); put(2 * i, pw); }
                 if (q.y & LEAF_BIT) { pseudo_words(q.y, r0, r1, pw); put(2 * i + 1, pw); }

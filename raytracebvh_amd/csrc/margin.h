@@ -78,17 +78,17 @@ RTBVH_HD inline MtNodeK mt_node_consts() {
     k.U0 = 6.06f * MT_U * up;
     return k;
 }
-// rho_n(t) in two steps, as the walk evaluates it: per node (E^2, Q E, U0 E + FLOOR), then per bound t
+// rho_n(t) as the walk evaluates it: per node the line rho_n(t) = s t + c, s = E^2 P + U1, c = E^2 Q E + U0 E
+// + FLOOR (each a few roundings, inside the constants' margin), then one fma per bound t
 struct MtNodeRho {
-    float E2, QE, UE;
+    float s, c;
 };
 RTBVH_HD inline MtNodeRho mt_node_prep(const MtNodeK& k, float E) {
-    return MtNodeRho{E * E, k.Q * E, fmaf(k.U0, E, MT_FLOOR)};
+    const float E2 = E * E;
+    return MtNodeRho{fmaf(E2, k.P, k.U1), fmaf(E2, k.Q * E, fmaf(k.U0, E, MT_FLOOR))};
 }
-RTBVH_HD inline float mt_node_eval(const MtNodeK& k, const MtNodeRho& n, float t) {
-    return fmaf(n.E2, fmaf(k.P, t, n.QE), fmaf(k.U1, t, n.UE));
-}
-RTBVH_HD inline float mt_node_rho(const MtNodeK& k, float E, float t) { return mt_node_eval(k, mt_node_prep(k, E), t); }
+RTBVH_HD inline float mt_node_eval(const MtNodeRho& n, float t) { return fmaf(n.s, t, n.c); }
+RTBVH_HD inline float mt_node_rho(const MtNodeK& k, float E, float t) { return mt_node_eval(mt_node_prep(k, E), t); }
 
 // the global edge bound of a triangle: max(|e1|, |e2|) rounded up (inf for a non-finite triangle)
 RTBVH_HD inline float mt_edge_bound(float e1x, float e1y, float e1z, float e2x, float e2y, float e2z) {

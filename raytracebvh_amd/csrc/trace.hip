@@ -917,7 +917,7 @@ __device__ __forceinline__ void pb_shade_tile(const TraceArgs& a, uint32_t rows,
 // same workgroup, from the keys in LDS -- no keys round trip through HBM, one launch fewer, and a tile's
 // dependent shading gathers run beside other tiles' rasterisation on the CU
 #ifndef RTBVH_PB_FUSE
-#define RTBVH_PB_FUSE 0
+#define RTBVH_PB_FUSE 1
 #endif
 template <bool COUNT, bool CERT = false, bool FUSE = false>
 __global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
@@ -1463,10 +1463,15 @@ __device__ __forceinline__ bool qbox_fast_cert(const QAxis& x, const QAxis& y, c
     const float nx = qt(x.nw, c, x.b, x.an), ny = qt(y.nw, c, y.b, y.an), nz = qt(z.nw, c, z.b, z.an);
     const float mn = fmaxf(fmaxf(nx, ny), nz);
     const float mx = fminf(fminf(qt(x.fw, c, x.b, x.af), qt(y.fw, c, y.b, y.af)), qt(z.fw, c, z.b, z.af));
-    const float rb = best == __builtin_inff() ? mt_node_eval(nk, nr, fmaxf(mn, 0.f)) : 0.f;
+    const float rb = best == __builtin_inff() ? mt_node_eval(nr, fmaxf(mn, 0.f)) : 0.f;
     key = fminf(fmaxf(fmaxf(fmaf(-rb, ainv.x, nx), fmaf(-rb, ainv.y, ny)), fmaf(-rb, ainv.z, nz)), tcn);
     return 0 <= mx && mn <= mx && key <= best;
 }
+// CERT on the exact decode for the rays the slack test cannot take (1), or those rays flagged for the
+// reference-order re-trace (0, A/B)
+#ifndef RTBVH_CERT_EXACT
+#define RTBVH_CERT_EXACT 1
+#endif
 // GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it).
 // CERT (MODE 2 only): the certified walk.  Every box test's entry distance is taken on the
 // box grown by its node's margin rho_n(best) (margin.h: no hit the triangle test accepts at t <= best lies
@@ -1548,11 +1553,11 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
             if (qfast) {
                 // CERT: the node's margin rho_n(best) (0 before the first bound) and its range
                 float rr = 0.f, tcn = 0.f;
-                MtNodeRho nr{0.f, 0.f, 0.f};
+                MtNodeRho nr{0.f, 0.f};
                 if (CERT) {
                     nr = mt_node_prep(nk, mt_code_val(wy));
                     tcn = mt_code_val(wz);
-                    rr = kbb < __builtin_inff() ? mt_node_eval(nk, nr, kbb) : 0.f;
+                    rr = kbb < __builtin_inff() ? mt_node_eval(nr, kbb) : 0.f;
                 }
                 const QAxis X = qaxis<CERT>(ox, sx, lx, hx, o.x, inv.x, rr),
                             Y = qaxis<CERT>(oy, sy, ly, hy, o.y, inv.y, rr),
@@ -1569,7 +1574,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                     h2 = qbox_fast(X, Y, Z, 2, true, kbb, t2);
                     h3 = qbox_fast(X, Y, Z, 3, true, kbb, t3);
                 }
-            } else {
+            } else if (!CERT || !RTBVH_CERT_EXACT) {
     #define RTBVH_QBOX(c, t)                                                                                      \
 ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
         qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), true, kbb, t)
@@ -1578,6 +1583,33 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                 h2 = RTBVH_QBOX(2, t2);
                 h3 = RTBVH_QBOX(3, t3);
     #undef RTBVH_QBOX
+            } else {
+                // CERT, a ray the slack test cannot take (|1/d| > 2^20 or |o| > 2^90: rare): the exact decode,
+                // each decoded box grown by the node's margin rho_n(best) with outward rounding (one ulp past
+                // the rounded sum), the reference slab test on it; keys capped at the node's range, and -inf
+                // before the first bound (such an entry is never dropped on a pop)
+                const MtNodeRho nr = mt_node_prep(nk, mt_code_val(wy));
+                const float tcn = mt_code_val(wz);
+                const bool bnd = kbb < __builtin_inff();
+                const float rr = bnd ? mt_node_eval(nr, kbb) : 0.f;
+                const auto lo = [&](float D) { return rr > 0.f ? nextafterf(D - rr, -INFINITY) : D; };
+                const auto hi = [&](float D) { return rr > 0.f ? nextafterf(D + rr, INFINITY) : D; };
+    #define RTBVH_QBOXC(c, t)                                                                                     \
+ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdecode(oz, sz, lz, c)),            \
+        hi(qdecode(ox, sx, hx, c)), hi(qdecode(oy, sy, hy, c)), hi(qdecode(oz, sz, hz, c)), false, 0.f, t)
+                h0 = RTBVH_QBOXC(0, t0);
+                h1 = RTBVH_QBOXC(1, t1);
+                h2 = RTBVH_QBOXC(2, t2);
+                h3 = RTBVH_QBOXC(3, t3);
+    #undef RTBVH_QBOXC
+                t0 = bnd ? fminf(t0, tcn) : -INFINITY;
+                t1 = bnd ? fminf(t1, tcn) : -INFINITY;
+                t2 = bnd ? fminf(t2, tcn) : -INFINITY;
+                t3 = bnd ? fminf(t3, tcn) : -INFINITY;
+                h0 = h0 && t0 <= kbb;
+                h1 = h1 && t1 <= kbb;
+                h2 = h2 && t2 <= kbb;
+                h3 = h3 && t3 <= kbb;
             }
             h1 = h1 & (a3.y != INVALID);
             h3 = h3 & (b3.y != INVALID);
@@ -1649,7 +1681,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     node = root_slot(T);
                     guard = 2 * T + 2;
                     if (CERT) {   // a ray the margin does not cover ends at its first step, flagged
-                        flg = !(qfast && dot(d, d) <= MT_DD);
+                        flg = !((qfast || RTBVH_CERT_EXACT) && dot(d, d) <= MT_DD);   // (exact decode: slack-free rays)
                         if (flg) node = INVALID;
                     }
                 }
