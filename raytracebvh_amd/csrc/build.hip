@@ -34,6 +34,9 @@ constexpr uint32_t BLOCK = 256;
 // leaves (and node indices) per k_refit workgroup: the nodes whose leaf range lies inside
 // one join in LDS; the others ("crossing") climb in k_refit_top
 constexpr uint32_t RBLOCK = RTBVH_REFIT_BLOCK;
+#ifndef RTBVH_QSKIP
+#define RTBVH_QSKIP 1   // k_refit writes only the QNodes the 4-wide walk reads (0: all, A/B)
+#endif
 #ifndef RTBVH_REFIT_STAGE_SLOTS
 #define RTBVH_REFIT_STAGE_SLOTS 512   // slots per phase-4 round (32 KB; C4 A/B: 256 and 512 alike, 1024 slower)
 #endif
@@ -560,7 +563,7 @@ __device__ __forceinline__ void qnode_words(const float (&lx)[4], const float (&
     ok = quantize_axis(lz, hz, q.org[2], q.scl[2], q.lo[2], q.hi[2]) && ok;
     if (!ok) {
         q.scl[0] = 0.f;   // the traversal reads the exact pair for this node
-    } else {
+    } else if (E >= 0.f || E != E) {   // (E < 0: the caller adds the codes, qnode_codes)
         uint32_t ce, ct;
         mt_node_codes(E, ce, ct);
         q.scl[1] = __uint_as_float(__float_as_uint(q.scl[1]) | ce);
@@ -569,6 +572,15 @@ __device__ __forceinline__ void qnode_words(const float (&lx)[4], const float (&
     q.id[0] = ids.x; q.id[1] = ids.y; q.id[2] = ids.z; q.id[3] = ids.w;
     const float4* qs = reinterpret_cast<const float4*>(&q);
     d[0] = qs[0]; d[1] = qs[1]; d[2] = qs[2]; d[3] = qs[3];
+}
+
+// the margin codes into QNode words (qnode_words with E < 0 left them out)
+__device__ __forceinline__ void qnode_codes(float4 (&d)[4], float E) {
+    if (d[0].w == 0.f) return;
+    uint32_t ce, ct;
+    mt_node_codes(E, ce, ct);
+    d[1].x = __uint_as_float(__float_as_uint(d[1].x) | ce);
+    d[1].y = __uint_as_float(__float_as_uint(d[1].y) | ct);
 }
 
 // ---- the grouping of a QNode (greedy collapse) ------------------------------------
@@ -861,6 +873,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     uint32_t slot = INVALID;
     float4 rw[4], qw[4];
     uint32_t ent[4] = {INVALID, INVALID, INVALID, INVALID};
+    float E = 0.f;   // the node's edge bound: its QNode's margin codes, added once the QNode is known to be read
     if (mine) {
     const float* L = s_box[tid][0];
     const float* R = s_box[tid][1];
@@ -883,8 +896,8 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     };
     QEnt e0, e1;
     lds_kids(i, e0, e1);
-    const float E = __uint_as_float(s_cnt[tid] & 0x7FFFFFFFu);   // the node's edge bound (the climb's ticket)
-    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, E, qw, ent);
+    E = __uint_as_float(s_cnt[tid] & 0x7FFFFFFFu);   // the node's edge bound (the climb's ticket)
+    greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, -1.f, qw, ent);
     }
     // Which of the block's QNodes the 4-wide walk reads: it steps from a QNode to its internal
     // entries only, so a node's QNode is read iff the node is the root or an entry of a read QNode.  A QNode's
@@ -894,7 +907,9 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     // greedy collapse expands them) no QNode is written.
     uint32_t* s_read = s_cnt;   // (the edge bounds were read above)
     __syncthreads();
-    {
+    if (!RTBVH_QSKIP) {   // (A/B: every QNode written)
+        s_read[tid] = mine ? 1u : 0u;
+    } else {
         bool near = false;
         uint32_t x = i;
         for (int up = 0; mine && up < 3 && !near; up++) {
@@ -905,7 +920,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
         }
         s_read[tid] = mine && near ? 1u : 0u;
     }
-    bool pending = mine;   // its entries are not marked yet
+    bool pending = mine && RTBVH_QSKIP;   // its entries are not marked yet
     for (;;) {
         __syncthreads();
         bool changed = false;
@@ -923,6 +938,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
         if (!__syncthreads_or(changed)) break;
     }
     const bool rd = mine && s_read[tid] != 0;
+    if (rd) qnode_codes(qw, E);
     // 4. the outputs through LDS.  Every slot this block writes in phase 3 lies in its window
     // [2 base, 2 base + 2 RBLOCK) -- a node's record / QNode at 2 parent + side with the parent in
     // the block, a leaf child's pseudo-record at 2 i + side -- except the record and QNode of a

@@ -58,11 +58,27 @@ RTBVH_HD inline float mt_u2f(uint32_t u) { return __builtin_bit_cast(float, u); 
 RTBVH_HD inline uint32_t mt_code_up(float x) { return (mt_f2u(x) + 0xFFFFu) >> 16; }   // x >= 0: decodes >= x
 RTBVH_HD inline uint32_t mt_code_down(float x) { return x >= 0.f ? mt_f2u(x) >> 16 : 0xBF80u; }   // <= x; -1
 RTBVH_HD inline float mt_code_val(uint32_t w) { return mt_u2f(w << 16); }   // (the low 16 bits of w)
+// 1 / x rounded down (x > 0 finite): the hardware reciprocal (within 1 ulp) on the device, the division
+// on the host, either times 1 - 2^-21
+RTBVH_HD inline float mt_rcp_down(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x) * (1.f - 0x1p-21f);
+#else
+    return 1.f / x * (1.f - 0x1p-21f);
+#endif
+}
+// tcap of mt_margin(E, MT_LAMBDA, MT_A) from below, without a division (the build quantizes a node per thread)
+RTBVH_HD inline float mt_tcap_down(float E) {
+    if (!(E >= 0.f && E < INFINITY)) return -1.f;
+    const float c = 28.3f * MT_LAMBDA * MT_A * MT_U * E * (1.f + 0x1p-20f);   // >= mt_margin's c
+    if (!(c > 0.f)) return INFINITY;
+    return (0.2f * mt_rcp_down(c) - 2.f * E * (1.f + 0x1p-20f)) * ((1.f - 0x1p-20f) / MT_A) * 0.999f;
+}
 // a node's codes from the largest edge bound of its leaves (inf: a non-finite triangle below; tcap -1)
 RTBVH_HD inline void mt_node_codes(float E, uint32_t& ce, uint32_t& ct) {
     ce = mt_code_up(E >= 0.f ? E : INFINITY);   // (NaN: inf)
-    const MtMargin m = mt_margin(mt_code_val(ce), MT_LAMBDA, MT_A);
-    ct = mt_code_down(m.tcap);
+    // (mt_margin's other conditions, r1 < 0.5 and r0 finite, hold for every E whose tcap is >= 0: E < ~24)
+    ct = mt_code_down(mt_tcap_down(mt_code_val(ce)));
 }
 struct MtNodeK {
     float P, Q, U1, U0;

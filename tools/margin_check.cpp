@@ -364,6 +364,15 @@ int main(int argc, char** argv) {
             check(s, rng, o, d, p0, p1, p2, false);
         }
     }
+    // the division-free range of the node codes (margin.h mt_tcap_down) against mt_margin's, on a sweep of
+    // edge bounds 2^-12 .. 2^6 (every 2^-14 step of the exponent)
+    for (int k = -12 * 16384; k <= 6 * 16384; k++) {
+        const float E = std::ldexp(1.0f + 0.0f, 0) * (float)std::exp2((double)k / 16384.0);
+        const MtMargin m = mt_margin(E, MT_LAMBDA, MT_A);
+        const float tc = mt_tcap_down(E);
+        ++s.node_checked;
+        if (m.tcap >= 0.f ? !(tc <= m.tcap) : !(tc < 0.f)) ++s.node_viol;
+    }
     printf("{\"tests\": %ld, \"accepted\": %ld, \"dist_checked\": %ld, \"dist_violations\": %ld, "
            "\"dist_violations_tight\": %ld, \"walk_checked\": %ld, \"walk_violations\": %ld, \"zkey_checked\": %ld, "
            "\"zkey_violations\": %ld, \"uncovered\": %ld, \"max_ratio\": %.6g, \"max_ratio_tight\": %.6g, "
