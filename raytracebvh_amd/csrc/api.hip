@@ -1155,10 +1155,19 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         return check_launch(c, "build kernel");
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
-    launch_morton(a, s);
-    if (timing) HIPC(c, hipEventRecord(ev[2], s));
-    c->sorted = radix_sort_pairs(c->d_codes, c->d_ids, c->d_ka, c->d_va, c->d_kb, c->d_vb, c->T, 30,
-                                 c->d_sort_scratch, s);
+    if (c->T <= small_sort_max() && !(c->cfg.flags & RTBVH_FLAG_MULTI_KERNEL_BUILD)) {
+        // the Morton pass and the sort in one workgroup (build.hip k_morton_sort_small; stage "morton")
+        c->sorted = SortResult{c->d_ka, c->d_va};
+        a.sorted_keys = c->d_ka;
+        a.sorted_vals = c->d_va;
+        launch_morton_sort_small(a, s);
+        if (timing) HIPC(c, hipEventRecord(ev[2], s));
+    } else {
+        launch_morton(a, s);
+        if (timing) HIPC(c, hipEventRecord(ev[2], s));
+        c->sorted = radix_sort_pairs(c->d_codes, c->d_ids, c->d_ka, c->d_va, c->d_kb, c->d_vb, c->T, 30,
+                                     c->d_sort_scratch, s);
+    }
     if (timing) HIPC(c, hipEventRecord(ev[3], s));
     a.sorted_keys = c->sorted.keys;
     a.sorted_vals = c->sorted.vals;

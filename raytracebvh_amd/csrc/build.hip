@@ -1302,6 +1302,81 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_build_small(BuildArgs a, uint32
 #endif
 }
 
+// Scenes above k_build_small's 2048 triangles and up to 8192 (C2's Image_Test: 3072): the Morton pass
+// and the sort in one workgroup -- the same bitonic network over (code << 32 | triangle) keys as
+// k_build_small, KPT keys per thread (steps at distance < KPT in the thread, < 64 KPT across lanes, the
+// longer ones through LDS) -- in place of the Morton launch and the radix sort's twelve; the rest of the
+// multi-kernel build follows.  (k_build_small's node boxes would not fit in LDS at this size.)
+template <uint32_t KPT>
+__global__ __launch_bounds__(SMALL_BLOCK) void k_morton_sort_small(BuildArgs a, uint32_t* __restrict__ sk,
+                                                                   uint32_t* __restrict__ sv) {
+    constexpr uint32_t N = KPT * SMALL_BLOCK;
+    __shared__ uint64_t s_kv[N];
+    const uint32_t tid = threadIdx.x, T = a.T;
+    uint64_t e[KPT];
+#pragma unroll
+    for (uint32_t b = 0; b < KPT; b++) {
+        const uint32_t t = KPT * tid + b;
+        e[b] = t < T ? ((uint64_t)morton_tri(a, t) << 32 | t) : ~0ull;
+    }
+    for (uint32_t k = 2; k <= N; k <<= 1) {
+        uint32_t j = k >> 1;
+        if (j >= 64 * KPT) {
+#pragma unroll
+            for (uint32_t b = 0; b < KPT; b++) s_kv[KPT * tid + b] = e[b];
+            __syncthreads();
+            for (; j >= 64 * KPT; j >>= 1) {
+#pragma unroll
+                for (uint32_t h = 0; h < KPT / 2; h++) {
+                    const uint32_t p = tid + h * SMALL_BLOCK;   // pair p: index i with bit j clear, and i | j
+                    const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), l = i | j;
+                    const uint64_t x = s_kv[i], y = s_kv[l];
+                    const bool up = (i & k) == 0, lt = x < y;
+                    s_kv[i] = up == lt ? x : y;
+                    s_kv[l] = up == lt ? y : x;
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < KPT; b++) e[b] = s_kv[KPT * tid + b];
+        }
+        for (; j >= KPT; j >>= 1) {   // partner lane tid ^ (j / KPT)
+            const uint32_t m = j / KPT;
+#pragma unroll
+            for (uint32_t b = 0; b < KPT; b++) {
+                const uint32_t i = KPT * tid + b;
+                const uint64_t x = e[b];
+                const uint32_t ylo = (uint32_t)__shfl_xor((int)(uint32_t)x, (int)m, 64);
+                const uint32_t yhi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), (int)m, 64);
+                const uint64_t y = (uint64_t)yhi << 32 | ylo;
+                const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                e[b] = keep_min == (x < y) ? x : y;
+            }
+        }
+#pragma unroll
+        for (uint32_t jj = KPT / 2; jj >= 1; jj >>= 1) {   // in the thread (jj a constant: e stays in registers)
+            if (jj > j) continue;   // (stages k < KPT start below KPT / 2)
+#pragma unroll
+            for (uint32_t b = 0; b < KPT; b++) {
+                if (b & jj) continue;
+                const uint32_t i = KPT * tid + b;
+                const uint64_t x = e[b], y = e[b | jj];
+                const bool sw = ((i & k) == 0) != (x < y);
+                e[b] = sw ? y : x;
+                e[b | jj] = sw ? x : y;
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < KPT; b++) {
+        const uint32_t i = KPT * tid + b;
+        if (i < T) {
+            sk[i] = (uint32_t)(e[b] >> 32);
+            sv[i] = (uint32_t)e[b];
+        }
+    }
+}
+
 // reference layout (RayTraceGlobal.hlsl:39-51): leaves [0,T), internal k at T+k
 struct RefNode { uint32_t parent, child_l, child_r, code; float bb_min[3], bb_max[3]; uint32_t index; };
 static_assert(sizeof(RefNode) == 44, "44-B Node");
@@ -1359,6 +1434,15 @@ void launch_karras(const BuildArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL(k_karras<1>, dim3(blocks_for(a.T)), dim3(BLOCK), 0, s, a);
 }
 uint32_t small_build_max() { return SMALL_T; }
+uint32_t small_sort_max() { return 8 * SMALL_BLOCK; }
+void launch_morton_sort_small(const BuildArgs& a, hipStream_t s) {
+    uint32_t* sk = const_cast<uint32_t*>(a.sorted_keys);
+    uint32_t* sv = const_cast<uint32_t*>(a.sorted_vals);
+    if (a.T <= 4 * SMALL_BLOCK)
+        hipLaunchKernelGGL(k_morton_sort_small<4>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
+    else
+        hipLaunchKernelGGL(k_morton_sort_small<8>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
+}
 void launch_build_small(const BuildArgs& a, hipStream_t s) {
     uint32_t* sk = const_cast<uint32_t*>(a.sorted_keys);
     uint32_t* sv = const_cast<uint32_t*>(a.sorted_vals);

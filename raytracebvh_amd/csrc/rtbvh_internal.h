@@ -95,6 +95,10 @@ void launch_qnodes(const BuildArgs& a, hipStream_t s);
 // a.sorted_keys / a.sorted_vals, which must be writable)
 uint32_t small_build_max();
 void launch_build_small(const BuildArgs& a, hipStream_t s);
+// the Morton pass and the sort in one workgroup for T <= small_sort_max() (sorted pairs into
+// a.sorted_keys / a.sorted_vals, which must be writable); the multi-kernel build's later stages follow
+uint32_t small_sort_max();
+void launch_morton_sort_small(const BuildArgs& a, hipStream_t s);
 // reference-layout export (44-B Node), 2T-1 entries
 void launch_export(const BuildArgs& a, void* out_nodes, hipStream_t s);
 // Karras + refit from given sorted codes and leaf boxes (n x 6 floats, device)

@@ -1552,7 +1552,9 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
             const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
             a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
             b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
-            if (qfast) {
+            // (CERT without the exact-decode variant: a ray the slack test cannot take never steps -- it is
+            // flagged at its first step -- so every stepping ray takes this branch)
+            if (qfast || (CERT && !RTBVH_CERT_EXACT)) {
                 // CERT: the node's margin rho_n(best) (0 before the first bound) and its range
                 float rr = 0.f, tcn = 0.f;
                 MtNodeRho nr{0.f, 0.f};

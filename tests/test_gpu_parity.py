@@ -1560,7 +1560,7 @@ def _build_outputs(s, flags, morton_mode=0, delta_mode=0):
     return out
 
 
-@pytest.mark.parametrize("ntris", [1, 2, 3, 57, 1000, 2047, 2048, 2049])
+@pytest.mark.parametrize("ntris", [1, 2, 3, 57, 1000, 2047, 2048, 2049, 3072, 4096, 4097, 8192, 8193])
 @pytest.mark.parametrize("modes", [(0, 0), (1, 0), (0, 1)])
 def test_one_workgroup_build_equals_multi_kernel_build(ntris, modes):
     """Scenes of <= 2048 triangles build in one workgroup (build.hip k_build_small): the
