@@ -1543,7 +1543,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
         float t0, t1, t2, t3;
         bool h0, h1, h2, h3;
         const float kbb = key_t(key);
-        if (q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15
+        if (CERT || q0.w != 0.f) {   // quantized node: q0..q3 = QNode words 0..15 (CERT: the step checked)
             // scl[1], scl[2] carry the node's margin codes in their (otherwise zero) mantissas (margin.h)
             const uint32_t wy = __float_as_uint(q1.x), wz = __float_as_uint(q1.y);
             const float ox = q0.x, oy = q0.y, oz = q0.z, sx = q0.w;
@@ -1621,8 +1621,7 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
             // a node without a finite grid: its exact record pair (node = its slot; the
             // pair of its children's records is at 2 * own, own = word 14 of its record; the
             // build writes the pseudo-records of such a node's leaf children whatever the flags).
-            // Not widened by the margin: a certified walk flags the ray
-            if (CERT) flg = true;
+            // (Not widened by the margin: a certified walk ends the ray there, flagged -- below)
             const uint32_t own = __float_as_uint(reinterpret_cast<const v4f*>(inner + node)[3].z);
             const v4f* pr = reinterpret_cast<const v4f*>(inner + 2 * (size_t)own);
             q0 = pr[0]; q1 = pr[1]; q2 = pr[2]; q3 = pr[3];
@@ -1721,9 +1720,16 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
                     v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
                     pin(q0); pin(q1); pin(q2); pin(q3);
                     if (COUNT) c.internal++;
-                    float k0, k1, k2, k3;
-                    uint32_t i0, i1, i2, i3;
-                    qchildren(q0, q1, q2, q3, k0, k1, k2, k3, i0, i1, i2, i3);
+                    float k0 = 0.f, k1 = 0.f, k2 = 0.f, k3 = 0.f;
+                    uint32_t i0 = INVALID, i1 = INVALID, i2 = INVALID, i3 = INVALID;
+                    // CERT: a node without a finite grid (its corners past 2^100: the margin does not cover
+                    // its exact boxes) ends the walk, the ray flagged for the reference-order re-trace
+                    if (CERT && q0.w == 0.f) {
+                        flg = true;
+                        done = true;
+                    } else {
+                        qchildren(q0, q1, q2, q3, k0, k1, k2, k3, i0, i1, i2, i3);
+                    }
 #ifdef RTBVH_DEBUG_PIXEL   // (scripts/debug_walk.py: one ray's walk, step by step, from the COUNT kernel)
                     if (COUNT && qin[r].idx == (uint32_t)RTBVH_DEBUG_PIXEL)
                         printf("DBG %d q %u sp %d kb %.6g key %.6g | %.6g %x %.6g %x %.6g %x %.6g %x\n", (int)CERT, node,

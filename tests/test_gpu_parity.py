@@ -1213,6 +1213,28 @@ def test_certified_walks_with_a_few_huge_triangles():
     assert ast["internal_visits"][1] <= 1.3 * fst["internal_visits"][1], (ast["internal_visits"], fst["internal_visits"])
 
 
+def test_certified_walks_end_at_nodes_without_a_grid():
+    """A QNode whose boxes reach past 2^100 keeps no 8-bit grid (build.hip quantize_axis): the certified
+    walk ends a ray there, flagged, and the reference-order re-trace takes it.  A 20k-triangle scene plus
+    two triangles at x ~ 1e31: every node above them has no grid, so the certified frame must come from
+    re-traced rays wherever the walk meets one -- and equal the reference order's."""
+    base = rt.synthetic(20_000, seed=77, half_extent=(60, 60, 30))
+    far = np.array([[[1e31, 0, 10], [1.0001e31, 0, 10], [1e31, 5, 12]],
+                    [[-1e31, 0, 10], [-1.0001e31, 0, 10], [-1e31, 5, 12]]], np.float32)
+    v = np.zeros((6, 8), np.float32)
+    v[:, :3] = far.reshape(-1, 3)
+    v[:, 5] = -1.0
+    V0 = len(base.vertices)
+    s = rt.Scene(np.concatenate([base.vertices, v]), np.concatenate([base.indices, V0 + np.arange(6, dtype=np.uint32)]),
+                 np.concatenate([base.mat_indices, np.zeros(2, np.uint32)]), base.materials)
+    W, H = 320, 180
+    wvp, wv = rt.camera_reference(W, H)
+    ref, _ = _counts(s, wvp, wv, W, H, 0)
+    cert, st = _counts(s, wvp, wv, W, H, rt.FLAG_CERTIFIED)
+    np.testing.assert_array_equal(cert, ref)
+    assert st["bounce_rays"] > 0 and st["redo_rays"][1] > 0, st["redo_rays"]
+
+
 def test_certified_walks_flag_rays_they_cannot_take():
     """Rays the certified bounce walk cannot vouch for are re-traced in the reference order: here the
     bounce rays of triangles whose shading normal is (0, 0, -1) -- under the reference camera (WV's x
