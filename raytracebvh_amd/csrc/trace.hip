@@ -918,8 +918,12 @@ __device__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at,
 #ifndef RTBVH_PB_FUSE
 #define RTBVH_PB_FUSE 1
 #endif
+#ifndef RTBVH_PB_WAVES
+#define RTBVH_PB_WAVES 8   // k_primary_binned's launch bounds: 8 waves per SIMD with 37 VGPRs spilled beat
+                                   // 6 (16 spilled) and 5 (none) -- primary pass 0.87-0.89 / 0.91-0.93 / 0.98 ms
+#endif
 template <bool COUNT, bool CERT = false, bool FUSE = false>
-__global__ __launch_bounds__(PB_RASTER_BLOCK, 8) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
+__global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
                                                              const uint4* __restrict__ bins, uint32_t cap,
                                                              uint32_t ntx, uint32_t rows,
                                                              unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
