@@ -96,7 +96,10 @@ struct rtbvh_ctx {
     // pipelines 1.. of a split trace (pipeline 0 = d_q / d_hit on the context stream): a
     // rank's bands dealt over `nsplit` independent primary -> bounce chains on their own
     // streams, so one chain's kernel tail overlaps the others' work
-    static constexpr uint32_t MAXSPLIT = 4;
+#ifndef RTBVH_MAXSPLIT
+#define RTBVH_MAXSPLIT 4
+#endif
+    static constexpr uint32_t MAXSPLIT = RTBVH_MAXSPLIT;   // buffer sets: the context stream's + caller-stream slots
     RayQ* d_qs[MAXSPLIT][2] = {};
     float2* d_hits[MAXSPLIT] = {};
     size_t cap_split = 0;                     // rays per pipeline queue
@@ -1416,7 +1419,7 @@ rtbvh_status rtbvh_trace_band_async(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32
                 c->slot_stream[k] = s;
                 slot = k;
             }
-        if (!slot) return fail(c, RTBVH_ERR_INVALID_ARG, "more than 3 caller streams trace one context");
+        if (!slot) return fail(c, RTBVH_ERR_INVALID_ARG, "more caller streams trace one context than it has slots");
         if (!c->ev_slot[slot]) HIPC(c, hipEventCreateWithFlags(&c->ev_slot[slot], hipEventDisableTiming));
         c->slots_used = true;
         HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
