@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Small driver for rocprofv3 runs: builds the C5 scene once and runs a few
-builds + traces in the requested mode.  PROF_MODE is a '+'-joined list of
+builds + traces in the requested mode (PROF_COMPUTE=1: rtbvh_compute_bvh frames).  PROF_MODE is a '+'-joined list of
 reference | nearest | sort | packet | refill | wide | count (e.g. "nearest+packet")."""
 import os
 import sys
@@ -22,6 +22,9 @@ with rt.Context(device=0, flags=flags) as c:
     c.set_scene(scene)
     c.set_camera(*rt.camera_reference(W, H))
     for _ in range(int(os.environ.get("PROF_ITERS", "3"))):
+        if os.environ.get("PROF_COMPUTE"):   # the drop-in's frame: rtbvh_compute_bvh (build + trace, one call)
+            c.compute_bvh(W, H, 1)
+            continue
         c.build()
         c.trace(W, H, 1)
     if flags & rt.FLAG_COUNT_VISITS:
