@@ -1,0 +1,274 @@
+// collapse_study.cpp -- a CPU study, not part of the library: how many QNode visits and triangle tests a
+// nearest-first 4-wide walk makes over two collapses of the same binary tree (the reference's Karras
+// tree): the build's greedy rule (build.hip greedy_qnode_words: expand the largest-area internal entry,
+// twice) and an SAH-optimal cut per node (dynamic programming over the binary subtree: D(x, 1) = the cost
+// of x as an entry, D(x, j >= 2) = the cheapest cover of x's subtree by j entries; a node's QNode is its
+// cheapest cover by 2..4 entries).  Exact float boxes, no quantization and no margins: the walk is the
+// unchecked nearest-first one, counts only.
+//
+// Inputs (tests/collapse_study_inputs.py writes them, from the oracle build and trace): nodes.bin (the reference layout, 44-B records, leaves
+// [0, T), internal k at T + k, root T), tris.bin (9 floats per sorted leaf: clip-space v0, v1, v2),
+// rays.bin (6 floats per ray: origin, direction).  Usage: collapse_study DIR [C_tri]
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+struct Node {
+    uint32_t parent, child_l, child_r, code;
+    float bmin[3], bmax[3];
+    uint32_t index;
+};
+static_assert(sizeof(Node) == 44, "44-B node");
+
+static std::vector<char> slurp(const char* path) {
+    std::vector<char> d;
+    FILE* f = fopen(path, "rb");
+    if (!f) return d;
+    fseek(f, 0, SEEK_END);
+    d.resize((size_t)ftell(f));
+    fseek(f, 0, SEEK_SET);
+    if (fread(d.data(), 1, d.size(), f) != d.size()) d.clear();
+    fclose(f);
+    return d;
+}
+
+static double half_area(const Node& n) {
+    const double dx = (double)n.bmax[0] - n.bmin[0], dy = (double)n.bmax[1] - n.bmin[1],
+                 dz = (double)n.bmax[2] - n.bmin[2];
+    return std::max(dx * dy + dy * dz + dz * dx, 0.0);
+}
+
+struct QNodeE {
+    uint32_t e[4];
+    int n;
+};
+
+// the ray / box slab test (entry distance, hit)
+static bool slab(const float o[3], const float inv[3], const Node& b, float best, float& tn) {
+    float t0 = 0.f, t1 = best;
+    for (int a = 0; a < 3; a++) {
+        float lo = (b.bmin[a] - o[a]) * inv[a], hi = (b.bmax[a] - o[a]) * inv[a];
+        if (lo > hi) std::swap(lo, hi);
+        t0 = std::max(t0, lo);
+        t1 = std::min(t1, hi);
+    }
+    tn = t0;
+    return t0 <= t1;
+}
+// Moller-Trumbore as the kernels (EPSILON 0.01 on the determinant)
+static float tri_hit(const float o[3], const float d[3], const float* v) {
+    const float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+    const float h[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
+    const float a = e1[0] * h[0] + e1[1] * h[1] + e1[2] * h[2];
+    if (std::fabs(a) < 0.01f) return -1.f;
+    const float f = 1.f / a;
+    const float s[3] = {o[0] - v[0], o[1] - v[1], o[2] - v[2]};
+    const float u = f * (s[0] * h[0] + s[1] * h[1] + s[2] * h[2]);
+    if (u < 0.f || u > 1.f) return -1.f;
+    const float q[3] = {s[1] * e1[2] - s[2] * e1[1], s[2] * e1[0] - s[0] * e1[2], s[0] * e1[1] - s[1] * e1[0]};
+    const float vv = f * (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]);
+    if (vv < 0.f || u + vv > 1.f) return -1.f;
+    const float t = f * (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]);
+    return t > 0.01f ? t : -1.f;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: collapse_study DIR [C_tri]\n");
+        return 2;
+    }
+    const double CT = argc > 2 ? atof(argv[2]) : 0.5, CI = 1.0;
+    const uint32_t ML = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;   // leaf clusters: subtrees of <= ML leaves
+    char path[1024];
+    snprintf(path, sizeof path, "%s/nodes.bin", argv[1]);
+    std::vector<char> nb = slurp(path);
+    snprintf(path, sizeof path, "%s/tris.bin", argv[1]);
+    std::vector<char> tb = slurp(path);
+    snprintf(path, sizeof path, "%s/rays.bin", argv[1]);
+    std::vector<char> rb = slurp(path);
+    const Node* N = reinterpret_cast<const Node*>(nb.data());
+    const size_t NN = nb.size() / sizeof(Node);
+    const uint32_t T = (uint32_t)((NN + 1) / 2);
+    const float* tri = reinterpret_cast<const float*>(tb.data());
+    const float* rays = reinterpret_cast<const float*>(rb.data());
+    const size_t R = rb.size() / (6 * sizeof(float));
+    if (T < 2 || tb.size() != (size_t)T * 9 * sizeof(float) || R == 0) {
+        fprintf(stderr, "bad inputs (T %u, rays %zu)\n", T, R);
+        return 2;
+    }
+    const uint32_t root = T;
+    // leaves below each node (a cluster: <= ML of them, tested as one entry -- all its triangles)
+    std::vector<uint32_t> nleaf(NN, 1), first(NN);
+    for (uint32_t j = 0; j < T; j++) first[j] = j;
+    {
+        std::vector<std::pair<uint32_t, bool>> st{{T, false}};
+        while (!st.empty()) {
+            auto [x, done] = st.back();
+            st.pop_back();
+            if (x < T) continue;
+            if (done) {
+                nleaf[x] = nleaf[N[x].child_l] + nleaf[N[x].child_r];
+                first[x] = std::min(first[N[x].child_l], first[N[x].child_r]);
+                continue;
+            }
+            st.push_back({x, true});
+            st.push_back({N[x].child_l, false});
+            st.push_back({N[x].child_r, false});
+        }
+    }
+    auto leaf = [&](uint32_t x) { return x < T || nleaf[x] <= ML; };
+    // post-order of the internal nodes
+    std::vector<uint32_t> order;
+    order.reserve(T);
+    {
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        while (!st.empty()) {
+            auto [x, done] = st.back();
+            st.pop_back();
+            if (leaf(x)) continue;
+            if (done) { order.push_back(x); continue; }
+            st.push_back({x, true});
+            st.push_back({N[x].child_l, false});
+            st.push_back({N[x].child_r, false});
+        }
+    }
+    // greedy collapse (build.hip greedy_qnode_words)
+    std::vector<QNodeE> greedy(NN), sah(NN);
+    for (uint32_t x : order) {
+        uint32_t E[4] = {N[x].child_l, N[x].child_r, 0, 0};
+        int n = 2;
+        for (int step = 0; step < 2; step++) {
+            int pick = -1;
+            double best = -1;
+            for (int k = 0; k < 3 && k < n; k++)
+                if (!leaf(E[k])) {
+                    const double ar = half_area(N[E[k]]);
+                    if (ar > best) { best = ar; pick = k; }
+                }
+            if (pick < 0) break;
+            const uint32_t sel = E[pick];
+            E[pick] = N[sel].child_l;
+            E[n] = N[sel].child_r;
+            ++n;
+        }
+        QNodeE& q = greedy[x];
+        q.n = n;
+        for (int k = 0; k < 4; k++) q.e[k] = k < n ? E[k] : 0;
+    }
+    // SAH-optimal cuts: D[x][j], j = 1..4
+    const double INF = 1e300;
+    std::vector<std::array<double, 5>> D(NN);
+    std::vector<double> C(NN, 0.0);
+    for (uint32_t j = 0; j < T; j++) {
+        D[j].fill(INF);
+        D[j][1] = half_area(N[j]) * CT;
+    }
+    for (uint32_t x : order) {
+        if (leaf(x)) {
+            D[x].fill(INF);
+            D[x][1] = half_area(N[x]) * CT * nleaf[x];
+            continue;
+        }
+        const uint32_t l = N[x].child_l, r = N[x].child_r;
+        std::array<double, 5> e;
+        e.fill(INF);
+        for (int j = 2; j <= 4; j++)
+            for (int a = 1; a < j; a++) e[j] = std::min(e[j], D[l][a] + D[r][j - a]);
+        C[x] = std::min(e[2], std::min(e[3], e[4]));
+        D[x] = e;
+        D[x][1] = half_area(N[x]) * CI + C[x];
+    }
+    auto cut = [&](auto&& self, uint32_t x, int j, std::vector<uint32_t>& out) -> void {
+        if (j == 1) { out.push_back(x); return; }
+        const uint32_t l = N[x].child_l, r = N[x].child_r;
+        int ba = 1;
+        double bv = INF;
+        for (int a = 1; a < j; a++)
+            if (D[l][a] + D[r][j - a] < bv) { bv = D[l][a] + D[r][j - a]; ba = a; }
+        self(self, l, ba, out);
+        self(self, r, j - ba, out);
+    };
+    for (uint32_t x : order) {
+        int bj = 2;
+        double bv = INF;
+        for (int j = 2; j <= 4; j++) {
+            double v = INF;
+            for (int a = 1; a < j; a++) v = std::min(v, D[N[x].child_l][a] + D[N[x].child_r][j - a]);
+            if (v < bv) { bv = v; bj = j; }
+        }
+        std::vector<uint32_t> out;
+        cut(cut, x, bj, out);
+        QNodeE& q = sah[x];
+        q.n = (int)out.size();
+        for (int k = 0; k < 4; k++) q.e[k] = k < q.n ? out[k] : 0;
+    }
+    // the SAH cost of both (from the root, per unit root area)
+    auto sah_cost = [&](const std::vector<QNodeE>& Q) {
+        double c = 0;
+        std::vector<uint32_t> st{root};
+        while (!st.empty()) {
+            const uint32_t x = st.back();
+            st.pop_back();
+            if (leaf(x)) { c += half_area(N[x]) * CT * nleaf[x]; continue; }
+            c += half_area(N[x]) * CI;
+            for (int k = 0; k < Q[x].n; k++) st.push_back(Q[x].e[k]);
+        }
+        return c / half_area(N[root]);
+    };
+    // the nearest-first walk, counts
+    auto walk = [&](const std::vector<QNodeE>& Q, uint64_t& qv, uint64_t& lt, uint64_t& reached, uint64_t& lsteps) {
+        qv = lt = reached = lsteps = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : qv, lt, reached, lsteps)
+        for (size_t i = 0; i < R; i++) {
+            const float* o = rays + 6 * i;
+            const float* d = o + 3;
+            const float inv[3] = {1.f / d[0], 1.f / d[1], 1.f / d[2]};
+            float best = INFINITY;
+            std::vector<std::pair<uint32_t, float>> st;
+            st.reserve(256);
+            st.push_back({root, 0.f});
+            while (!st.empty()) {
+                auto [x, t] = st.back();
+                st.pop_back();
+                if (t > best) continue;
+                if (leaf(x)) {
+                    ++lsteps;
+                    for (uint32_t j = first[x]; j < first[x] + nleaf[x]; j++) {
+                        ++lt;
+                        const float h = tri_hit(o, d, tri + 9 * (size_t)j);
+                        if (h > 0.f && h < best) best = h;
+                    }
+                    continue;
+                }
+                ++qv;
+                std::pair<uint32_t, float> hit[4];
+                int nh = 0;
+                for (int k = 0; k < Q[x].n; k++) {
+                    float tn;
+                    if (slab(o, inv, N[Q[x].e[k]], best, tn)) hit[nh++] = {Q[x].e[k], tn};
+                }
+                std::sort(hit, hit + nh, [](auto& a, auto& b) { return a.second > b.second; });   // farthest first
+                for (int k = 0; k < nh; k++) st.push_back(hit[k]);
+            }
+            reached += best < INFINITY;
+        }
+    };
+    uint64_t gq, gl, gr, sq, sl, sr, gs, ss;
+    walk(greedy, gq, gl, gr, gs);
+    walk(sah, sq, sl, sr, ss);
+    size_t gn = 0, sn = 0, g4 = 0, s4 = 0;
+    for (uint32_t x : order) { gn += greedy[x].n; sn += sah[x].n; g4 += greedy[x].n == 4; s4 += sah[x].n == 4; }
+    printf("{\"T\": %u, \"rays\": %zu, \"C_tri\": %.3f, \"max_leaves\": %u, \"greedy\": {\"sah\": %.4f, \"qnode_visits\": %.4f, \"leaf_tests\": %.4f, \"leaf_steps\": %.4f, "
+           "\"hits\": %llu, \"four_wide_frac\": %.4f}, \"sah_opt\": {\"sah\": %.4f, \"qnode_visits\": %.4f, \"leaf_tests\": %.4f, \"leaf_steps\": %.4f, "
+           "\"hits\": %llu, \"four_wide_frac\": %.4f}}\n",
+           T, R, CT, ML, sah_cost(greedy), (double)gq / R, (double)gl / R, (double)gs / R, (unsigned long long)gr,
+           (double)g4 / order.size(), sah_cost(sah), (double)sq / R, (double)sl / R, (double)ss / R,
+           (unsigned long long)sr, (double)s4 / order.size());
+    (void)gn;
+    (void)sn;
+    return 0;
+}
