@@ -42,8 +42,9 @@ static double half_area(const Node& n) {
     return std::max(dx * dy + dy * dz + dz * dx, 0.0);
 }
 
+constexpr int WMAX = 8;
 struct QNodeE {
-    uint32_t e[4];
+    uint32_t e[WMAX];
     int n;
 };
 
@@ -83,6 +84,7 @@ int main(int argc, char** argv) {
     }
     const double CT = argc > 2 ? atof(argv[2]) : 0.5, CI = 1.0;
     const uint32_t ML = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;   // leaf clusters: subtrees of <= ML leaves
+    const int W = argc > 4 ? std::min(std::max(atoi(argv[4]), 2), WMAX) : 4;   // the greedy collapse's width
     char path[1024];
     snprintf(path, sizeof path, "%s/nodes.bin", argv[1]);
     std::vector<char> nb = slurp(path);
@@ -139,12 +141,12 @@ int main(int argc, char** argv) {
     // greedy collapse (build.hip greedy_qnode_words)
     std::vector<QNodeE> greedy(NN), sah(NN);
     for (uint32_t x : order) {
-        uint32_t E[4] = {N[x].child_l, N[x].child_r, 0, 0};
+        uint32_t E[WMAX] = {N[x].child_l, N[x].child_r};
         int n = 2;
-        for (int step = 0; step < 2; step++) {
+        for (int step = 0; step < W - 2; step++) {   // (W = 4: build.hip's rule, which looks at the first 3)
             int pick = -1;
             double best = -1;
-            for (int k = 0; k < 3 && k < n; k++)
+            for (int k = 0; k < n && k < W - 1; k++)
                 if (!leaf(E[k])) {
                     const double ar = half_area(N[E[k]]);
                     if (ar > best) { best = ar; pick = k; }
@@ -157,7 +159,7 @@ int main(int argc, char** argv) {
         }
         QNodeE& q = greedy[x];
         q.n = n;
-        for (int k = 0; k < 4; k++) q.e[k] = k < n ? E[k] : 0;
+        for (int k = 0; k < WMAX; k++) q.e[k] = k < n ? E[k] : 0;
     }
     // SAH-optimal cuts: D[x][j], j = 1..4
     const double INF = 1e300;
@@ -204,7 +206,7 @@ int main(int argc, char** argv) {
         cut(cut, x, bj, out);
         QNodeE& q = sah[x];
         q.n = (int)out.size();
-        for (int k = 0; k < 4; k++) q.e[k] = k < q.n ? out[k] : 0;
+        for (int k = 0; k < WMAX; k++) q.e[k] = k < q.n ? out[k] : 0;
     }
     // the SAH cost of both (from the root, per unit root area)
     auto sah_cost = [&](const std::vector<QNodeE>& Q) {
@@ -245,7 +247,7 @@ int main(int argc, char** argv) {
                     continue;
                 }
                 ++qv;
-                std::pair<uint32_t, float> hit[4];
+                std::pair<uint32_t, float> hit[WMAX];
                 int nh = 0;
                 for (int k = 0; k < Q[x].n; k++) {
                     float tn;
@@ -261,11 +263,11 @@ int main(int argc, char** argv) {
     walk(greedy, gq, gl, gr, gs);
     walk(sah, sq, sl, sr, ss);
     size_t gn = 0, sn = 0, g4 = 0, s4 = 0;
-    for (uint32_t x : order) { gn += greedy[x].n; sn += sah[x].n; g4 += greedy[x].n == 4; s4 += sah[x].n == 4; }
-    printf("{\"T\": %u, \"rays\": %zu, \"C_tri\": %.3f, \"max_leaves\": %u, \"greedy\": {\"sah\": %.4f, \"qnode_visits\": %.4f, \"leaf_tests\": %.4f, \"leaf_steps\": %.4f, "
+    for (uint32_t x : order) { gn += greedy[x].n; sn += sah[x].n; g4 += greedy[x].n == W; s4 += sah[x].n == 4; }
+    printf("{\"T\": %u, \"rays\": %zu, \"C_tri\": %.3f, \"max_leaves\": %u, \"width\": %d, \"greedy\": {\"sah\": %.4f, \"qnode_visits\": %.4f, \"leaf_tests\": %.4f, \"leaf_steps\": %.4f, "
            "\"hits\": %llu, \"four_wide_frac\": %.4f}, \"sah_opt\": {\"sah\": %.4f, \"qnode_visits\": %.4f, \"leaf_tests\": %.4f, \"leaf_steps\": %.4f, "
            "\"hits\": %llu, \"four_wide_frac\": %.4f}}\n",
-           T, R, CT, ML, sah_cost(greedy), (double)gq / R, (double)gl / R, (double)gs / R, (unsigned long long)gr,
+           T, R, CT, ML, W, sah_cost(greedy), (double)gq / R, (double)gl / R, (double)gs / R, (unsigned long long)gr,
            (double)g4 / order.size(), sah_cost(sah), (double)sq / R, (double)sl / R, (double)ss / R,
            (unsigned long long)sr, (double)s4 / order.size());
     (void)gn;
