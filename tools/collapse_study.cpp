@@ -8,12 +8,14 @@
 //
 // Inputs (tests/collapse_study_inputs.py writes them, from the oracle build and trace): nodes.bin (the reference layout, 44-B records, leaves
 // [0, T), internal k at T + k, root T), tris.bin (9 floats per sorted leaf: clip-space v0, v1, v2),
-// rays.bin (6 floats per ray: origin, direction).  Usage: collapse_study DIR [C_tri]
+// rays.bin (6 floats per ray: origin, direction).  Usage: collapse_study DIR [C_tri] [max leaves per cluster]
+// [width]; DUMP=path writes the greedy collapse's QNode visits per ray (uint32)
 #include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -259,6 +261,42 @@ int main(int argc, char** argv) {
             reached += best < INFINITY;
         }
     };
+    if (const char* dump = getenv("DUMP")) {   // per-ray QNode visits of the greedy collapse (uint32)
+        std::vector<uint32_t> vis(R);
+#pragma omp parallel for schedule(dynamic, 256)
+        for (size_t i = 0; i < R; i++) {
+            const float* o = rays + 6 * i;
+            const float* d = o + 3;
+            const float inv[3] = {1.f / d[0], 1.f / d[1], 1.f / d[2]};
+            float best = INFINITY;
+            uint32_t v = 0;
+            std::vector<std::pair<uint32_t, float>> st{{root, 0.f}};
+            while (!st.empty()) {
+                auto [x, t] = st.back();
+                st.pop_back();
+                if (t > best) continue;
+                if (leaf(x)) {
+                    for (uint32_t j = first[x]; j < first[x] + nleaf[x]; j++) {
+                        const float h = tri_hit(o, d, tri + 9 * (size_t)j);
+                        if (h > 0.f && h < best) best = h;
+                    }
+                    continue;
+                }
+                ++v;
+                std::pair<uint32_t, float> hit[WMAX];
+                int nh = 0;
+                for (int k = 0; k < greedy[x].n; k++) {
+                    float tn;
+                    if (slab(o, inv, N[greedy[x].e[k]], best, tn)) hit[nh++] = {greedy[x].e[k], tn};
+                }
+                std::sort(hit, hit + nh, [](auto& a, auto& b) { return a.second > b.second; });
+                for (int k = 0; k < nh; k++) st.push_back(hit[k]);
+            }
+            vis[i] = v;
+        }
+        FILE* f = fopen(dump, "wb");
+        if (f) { fwrite(vis.data(), 4, R, f); fclose(f); }
+    }
     uint64_t gq, gl, gr, sq, sl, sr, gs, ss;
     walk(greedy, gq, gl, gr, gs);
     walk(sah, sq, sl, sr, ss);
