@@ -542,9 +542,10 @@ def main():
                 "traffic_source": f"PMC profiles/pmc_{args.workload}_{use_name}.json (N=1, collected at commit "
                                   f"{(load_pmc_meta(args.workload, use_name) or {}).get('commit')}), per record fetch x "
                                   f"this launch's {recs[dom]} record fetches" if measured else None,
-                "kernel_trace_source": "profiles/r05_*_one_frame_kernel_stats.csv: rocprofv3 --kernel-trace --stats of "
-                                       "scripts/profile_trace.py in the same mode, one frame at a time (kernel_ms is "
-                                       "this run's HIP-event duration of the same launch, one frame at a time)"}
+                "kernel_trace_source": f"profiles/kernel_stats_{args.workload}_{use_name}.csv: rocprofv3 --kernel-trace "
+                                       "--stats of scripts/profile_trace.py in the same mode, one frame at a time, "
+                                       "collected in the same GPU call as the PMC file (kernel_ms is this run's "
+                                       "HIP-event duration of the same launch, one frame at a time)"}
     if measured:
         roofline["cache_served_frac"] = round(max(0.0, 1.0 - kd["traffic"] / kd["bytes"]), 4)
     pm = load_pmc(args.workload, use_name, dom)
