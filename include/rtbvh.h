@@ -130,7 +130,9 @@ enum {
     RTBVH_FLAG_AUTO_WALK = 1u << 8,       /* choose the walks, ignoring the walk flags (the four above and
                                              BINNED_PRIMARY), and return the reference-order frame always: up
                                              to 65536 triangles the reference-order kernels (exact by
-                                             construction; the fastest on the reference's own meshes); above
+                                             construction; the fastest on the reference's own meshes), the
+                                             primary rays per lane or per wave packet, whichever the first
+                                             frame of a (W, H, scene) timed faster (stats walk_flags); above
                                              that, the CERTIFIED fast walks: BINNED_PRIMARY and
                                              the 4-wide bounce walk, pruning on boxes grown by the triangle
                                              test's rounding margin so that they see every triangle that could

@@ -157,6 +157,10 @@ struct rtbvh_ctx {
     uint64_t cert_traces = 0;                         // certified traces so far
     uint32_t last_walk = 0;                           // walk flags of the last trace
     uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
+    // RTBVH_FLAG_AUTO_WALK at <= AUTO_WALK_MAX_TRIS: the primary kind, the reference order's lanes or its
+    // wave packets (the same frame), timed on this scene and frame size (enqueue_trace)
+    uint64_t small_key = 0;
+    bool small_packet = false;
     bool last_cert = false;                           // the last trace was certified (its re-trace counts)
     // tuning knobs of A/B runs, read once by rtbvh_create (RTBVH_BOUNCE_BLOCKS, RTBVH_OVERLAP,
     // RTBVH_SIDE_PRIORITY): a shipped context does not change its launches per frame
@@ -886,9 +890,47 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (!c->built) return fail(c, RTBVH_ERR_NOT_READY, "trace before build");
     rtbvh_status st = sync_camera(c, s);
     if (st) return st;
-    const TracePlan p = plan_trace(c, c->cfg.flags);
+    TracePlan p = plan_trace(c, c->cfg.flags);
     c->last_walk_state = p.state;
     if (p.cert && !c->capturing) c->cert_traces++;
+    // AUTO_WALK on a small scene: the reference order, as one-ray-per-lane walks or as wave packets (the
+    // same frame: both are the exact findCollision DFS per ray).  Which is faster depends on the scene
+    // (C3, Test.obj: packets 0.089 against lanes 0.108 ms; C2, Image_Test.obj: 0.175 against 0.073), so
+    // the first full-frame trace of a scene and frame size on the context stream times both primary
+    // passes, twice each, and keeps the packets only when they are 5% faster.  Not while capturing: a
+    // captured frame keeps the choice made before it (rtbvh_compute_bvh with RTBVH_FLAG_GRAPH traces a
+    // frame uncaptured first).  Not with a stack limit (a wave packet shares one stack: its overflows
+    // differ from a lane's) nor the CPUTests delta.
+    const uint32_t f = c->cfg.flags;
+    const bool limited = c->cfg.stack_limit != 0 && c->cfg.stack_limit < (uint32_t)STACK_SIZE;
+    if ((f & RTBVH_FLAG_AUTO_WALK) && !p.cert && c->built_clz64 && !limited) {
+        const uint64_t key = (uint64_t)W << 48 | (uint64_t)H << 32 | c->T;
+        if (c->small_key != key && !c->capturing && s == c->stream && slot == 0 && nranks == 1) {
+            hipEvent_t ev[2] = {};
+            HIPC(c, hipEventCreate(&ev[0]));
+            HIPC(c, hipEventCreate(&ev[1]));
+            float best[2] = {INFINITY, INFINITY};
+            rtbvh_status cs = RTBVH_OK;
+            for (int round = 0; round < 2 && !cs; round++)
+                for (int k = 0; k < 2 && !cs; k++) {
+                    HIPC(c, hipEventRecord(ev[0], s));
+                    cs = enqueue_walks(c, W, H, 0, 0, 1, color, inten, s, 0,
+                                       p.flags | (k ? RTBVH_FLAG_PACKET_PRIMARY : 0u), false);
+                    if (cs) break;
+                    HIPC(c, hipEventRecord(ev[1], s));
+                    HIPC(c, hipEventSynchronize(ev[1]));
+                    float ms = 0.f;
+                    HIPC(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
+                    best[k] = std::min(best[k], ms);
+                }
+            (void)hipEventDestroy(ev[0]);
+            (void)hipEventDestroy(ev[1]);
+            if (cs) return cs;
+            c->small_packet = best[1] < 0.95f * best[0];
+            c->small_key = key;
+        }
+        if (c->small_key == key && c->small_packet) p.flags |= RTBVH_FLAG_PACKET_PRIMARY;
+    }
     return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, p.flags, true, p.cert);
 }
 
@@ -1104,6 +1146,7 @@ rtbvh_status rtbvh_set_scene(rtbvh_ctx* c, const rtbvh_vertex* verts, uint32_t n
     }
     c->have_scene = true;
     c->built = false;
+    c->small_key = 0;   // (the primary kind of a small scene is timed again)
     return RTBVH_OK;
 }
 

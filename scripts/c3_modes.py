@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""C3 (Obj/Test.obj, 1952 triangles, 1920x1080, primary + 1 bounce) rebuilt every frame as one hipGraph under
+"""C3 (Obj/Test.obj, 1952 triangles, 1920x1080, primary + 1 bounce; SCENE / BOUNCES for others) rebuilt every frame as one hipGraph under
 several walk configurations, interleaved: the wall time per frame, the stage times of a timed run, and whether
 the frame equals the reference order's.  Prints one JSON line per round and configuration."""
 import json
@@ -16,7 +16,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 scene = rt.load_npz(os.path.join(REPO, "tests", "golden", "scenes", os.environ.get("SCENE", "Test") + ".npz"))
 W, H, B = 1920, 1080, int(os.environ.get("BOUNCES", "1"))
 CFG = {"auto": rt.FLAG_AUTO_WALK, "certified": rt.FLAG_CERTIFIED,
-       "binned": rt.FLAG_BINNED_PRIMARY, "binned+refill": rt.FLAG_BINNED_PRIMARY | rt.FLAG_REFILL_BOUNCE}
+       "binned": rt.FLAG_BINNED_PRIMARY, "binned+refill": rt.FLAG_BINNED_PRIMARY | rt.FLAG_REFILL_BOUNCE,
+       "packet": rt.FLAG_PACKET_PRIMARY}
+if os.environ.get("CONFIGS"):
+    CFG = {k: v for k, v in CFG.items() if k in os.environ["CONFIGS"].split(",")}
 ref = None
 with rt.Context(device=0, flags=0) as c:
     c.set_scene(scene)
@@ -45,5 +48,6 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
             out["ms_trace"] = round(q["ms_trace"], 4)
             out["ms_stage"] = [round(x, 4) for x in q["ms_stage"]]
             out["walk_state"] = q["walk_state"]
+            out["walk_flags"] = q["walk_flags"]
             out["redo_rays"] = q["redo_rays"]
         print(json.dumps(out), flush=True)
