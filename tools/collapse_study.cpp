@@ -79,6 +79,107 @@ static float tri_hit(const float o[3], const float d[3], const float* v) {
     return t > 0.01f ? t : -1.f;
 }
 
+// REBUILD=sah: a binned-SAH top-down binary tree over the same leaves (their boxes; 16 centroid bins on each
+// axis, the cheapest plane), in place of the reference's Karras tree -- what a higher-quality tree would save
+// the walk (max leaves 1 only: the leaf ranges of the Karras tree no longer hold)
+struct SahBuilder {
+    std::vector<Node>& N;
+    uint32_t T;
+    std::vector<uint32_t> idx;
+    uint32_t next;   // internal ids from T + 1 (the root is T)
+    static void grow(float (&b)[6], const Node& n) {
+        for (int a = 0; a < 3; a++) { b[a] = std::min(b[a], n.bmin[a]); b[3 + a] = std::max(b[3 + a], n.bmax[a]); }
+    }
+    static double area(const float (&b)[6]) {
+        const double dx = (double)b[3] - b[0], dy = (double)b[4] - b[1], dz = (double)b[5] - b[2];
+        return dx < 0 ? 0.0 : dx * dy + dy * dz + dz * dx;
+    }
+    uint32_t alloc() {
+        uint32_t v;
+#pragma omp atomic capture
+        v = next++;
+        return v;
+    }
+    uint32_t build(size_t lo, size_t hi, uint32_t id) {
+        if (hi - lo == 1) return idx[lo];
+        constexpr int NB = 16;
+        float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
+        float box[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        for (size_t i = lo; i < hi; i++) {
+            const Node& n = N[idx[i]];
+            grow(box, n);
+            for (int a = 0; a < 3; a++) {
+                const float c = 0.5f * (n.bmin[a] + n.bmax[a]);
+                cl[a] = std::min(cl[a], c); ch[a] = std::max(ch[a], c);
+            }
+        }
+        int ba = -1, bb = 0;
+        double bc = INFINITY;
+        for (int a = 0; a < 3; a++) {
+            if (!(ch[a] > cl[a])) continue;
+            const float sc = NB / (ch[a] - cl[a]);
+            float bx[NB][6];
+            size_t cnt[NB] = {};
+            for (auto& b : bx) { b[0] = b[1] = b[2] = INFINITY; b[3] = b[4] = b[5] = -INFINITY; }
+            for (size_t i = lo; i < hi; i++) {
+                const Node& n = N[idx[i]];
+                const int k = std::min(NB - 1, (int)((0.5f * (n.bmin[a] + n.bmax[a]) - cl[a]) * sc));
+                cnt[k]++;
+                grow(bx[k], n);
+            }
+            double ra[NB];
+            float acc[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            size_t rc = 0, rcnt[NB];
+            for (int k = NB - 1; k > 0; k--) {
+                for (int q = 0; q < 3; q++) { acc[q] = std::min(acc[q], bx[k][q]); acc[3 + q] = std::max(acc[3 + q], bx[k][3 + q]); }
+                rc += cnt[k];
+                ra[k] = area(acc);
+                rcnt[k] = rc;
+            }
+            float lacc[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            size_t lc = 0;
+            for (int k = 0; k < NB - 1; k++) {
+                for (int q = 0; q < 3; q++) { lacc[q] = std::min(lacc[q], bx[k][q]); lacc[3 + q] = std::max(lacc[3 + q], bx[k][3 + q]); }
+                lc += cnt[k];
+                if (lc == 0 || rcnt[k + 1] == 0) continue;
+                const double c = area(lacc) * lc + ra[k + 1] * rcnt[k + 1];
+                if (c < bc) { bc = c; ba = a; bb = k; }
+            }
+        }
+        size_t mid;
+        if (ba < 0) {
+            mid = (lo + hi) / 2;   // every centroid equal: halves
+        } else {
+            const float sc = NB / (ch[ba] - cl[ba]);
+            auto it = std::partition(idx.begin() + lo, idx.begin() + hi, [&](uint32_t j) {
+                const Node& n = N[j];
+                return std::min(NB - 1, (int)((0.5f * (n.bmin[ba] + n.bmax[ba]) - cl[ba]) * sc)) <= bb;
+            });
+            mid = (size_t)(it - idx.begin());
+            if (mid == lo || mid == hi) mid = (lo + hi) / 2;
+        }
+        const uint32_t il = hi - lo > 2 && mid - lo > 1 ? alloc() : 0, ir = hi - mid > 1 ? alloc() : 0;
+        uint32_t l, r;
+        if (hi - lo > 200000) {
+#pragma omp task shared(l)
+            l = build(lo, mid, il);
+#pragma omp task shared(r)
+            r = build(mid, hi, ir);
+#pragma omp taskwait
+        } else {
+            l = build(lo, mid, il);
+            r = build(mid, hi, ir);
+        }
+        Node& n = N[id];
+        n.child_l = l;
+        n.child_r = r;
+        N[l].parent = id;
+        N[r].parent = id;
+        for (int a = 0; a < 3; a++) { n.bmin[a] = box[a]; n.bmax[a] = box[3 + a]; }
+        return id;
+    }
+};
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         fprintf(stderr, "usage: collapse_study DIR [C_tri]\n");
@@ -97,6 +198,19 @@ int main(int argc, char** argv) {
     const Node* N = reinterpret_cast<const Node*>(nb.data());
     const size_t NN = nb.size() / sizeof(Node);
     const uint32_t T = (uint32_t)((NN + 1) / 2);
+    std::vector<Node> rebuilt;
+    const char* rebuild = getenv("REBUILD");
+    if (rebuild && !strcmp(rebuild, "sah") && T >= 2) {
+        rebuilt.assign(N, N + NN);
+        SahBuilder B{rebuilt, T, std::vector<uint32_t>(T), T + 1};
+        for (uint32_t j = 0; j < T; j++) B.idx[j] = j;
+#pragma omp parallel
+#pragma omp single
+        B.build(0, T, T);
+        rebuilt[T].parent = ~0u;
+        N = rebuilt.data();
+        fprintf(stderr, "rebuilt: %u internal nodes\n", B.next - T);
+    }
     const float* tri = reinterpret_cast<const float*>(tb.data());
     const float* rays = reinterpret_cast<const float*>(rb.data());
     const size_t R = rb.size() / (6 * sizeof(float));
