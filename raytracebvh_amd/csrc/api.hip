@@ -73,6 +73,8 @@ struct rtbvh_ctx {
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
     bool pseudo_ok = false;      // the built tree has its leaf pseudo-records (read by the packet walks only)
     bool qnode_ok = false;       // the built tree has its QNodes (read by the 4-wide bounce walk only)
+    bool q8_ok = false;          // RTBVH_WIDE8: the built tree has its 8-wide nodes (the certified bounce walk)
+    QNode8* d_qnode8 = nullptr;  // RTBVH_WIDE8: 8-wide nodes in slots, 2T-1
     // rtbvh_compute_bvh: the build leaves its crossing nodes (launch_refit_tail) to the frame's binned
     // pass, which runs them in its bin launches (launch_pb_bin_tail); any other first use of the tree
     // runs them first (flush_tail)
@@ -236,6 +238,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_topo, ni));
     HIPC(c, dalloc(c->d_rec, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_qnode, 2 * (size_t)n - 1));
+    if (RTBVH_WIDE8) HIPC(c, dalloc(c->d_qnode8, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_lfp, n));
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
@@ -357,6 +360,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.xcnt = c->d_xcnt;
     a.rootbox = c->d_rootbox;
     a.qnode = c->d_qnode;
+    a.qnode8 = c->d_qnode8;
     a.lfp = c->d_lfp;
     a.zpart = c->d_zpart;
     // the leaf pseudo-records cost the build 0.64 GB of writes at 10M triangles: written when the
@@ -480,6 +484,7 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.inner = c->d_rec;
     a.leaf = c->d_leaf;
     a.qnode = c->d_qnode;
+    a.qnode8 = c->d_qnode8;
     a.rootbox = c->d_rootbox;
     a.lfp = c->d_lfp;
     a.tclip = c->d_tclip;
@@ -729,6 +734,15 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
         if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
     }
+    // RTBVH_WIDE8: the certified bounce walk's 8-wide nodes, once per build, from the complete tree (the
+    // fused tail completes it inside the binned pass: then right after it, below)
+    const bool need_q8 = RTBVH_WIDE8 && cert && bounces > 0 && !c->q8_ok;
+    if (need_q8 && !fuse_tail) {
+        launch_qnodes8(build_args(c), c->stream);
+        c->q8_ok = true;
+        if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
+        if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+    }
     if (!c->pseudo_ok && (pkind == PrimaryKind::PACKET_REFERENCE || pkind == PrimaryKind::PACKET_NEAREST ||
                           pkind == PrimaryKind::PACKET_WIDE)) {
         // a packet walk over a tree built without the leaf pseudo-records (the context's walks took
@@ -800,6 +814,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
                 if (overlap) {
                     HIPC(c, hipEventRecord(c->ev_prim, sp));
                     HIPC(c, hipStreamWaitEvent(sg, c->ev_prim, 0));
+                }
+                if (need_q8 && fuse_tail) {   // (after the join: fuse_tail's sg is the context stream)
+                    launch_qnodes8(build_args(c), sg);
+                    c->q8_ok = true;
+                    if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, sg));
                 }
                 launch_pb_gate(ag, pb, q[0], &qc[0], count, bounces > 0, sg, cert);
             } else if (overlap) {   // (nothing traced: the zeroing still joins)
@@ -1045,7 +1064,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     for (auto& p : c->pb) { dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_lfp);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_qnode8); dfree(c->d_lfp);
     dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
@@ -1198,6 +1217,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
         c->built = true;
         c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
+        c->q8_ok = false;
         return check_launch(c, "build kernel");
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
@@ -1244,6 +1264,7 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
     c->built = true;
     c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
+    c->q8_ok = false;
     return check_launch(c, "build kernels");
 }
 

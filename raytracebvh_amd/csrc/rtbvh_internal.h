@@ -74,6 +74,7 @@ struct BuildArgs {
     uint4* lfp;               // [T] leaf footprints on the primary pixel grid (rtbvh_device.h leaf_footprint)
     float* zpart;             // [ZPART * refit_blocks(T)] k_refit workgroup b's leaf depth range, edge bound
     uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
+    QNode8* qnode8;           // [2T-1] RTBVH_WIDE8 builds: quantized 8-wide nodes in slots (rtbvh_device.h QNode8)
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
@@ -91,6 +92,8 @@ void launch_pseudo(const BuildArgs& a, hipStream_t s);
 uint32_t refit_blocks(uint32_t T);
 // qnode[k] of every internal node from the record pairs
 void launch_qnodes(const BuildArgs& a, hipStream_t s);
+// RTBVH_WIDE8 builds: qnode8[k] of every internal node from the records of a complete tree (node_edge set)
+void launch_qnodes8(const BuildArgs& a, hipStream_t s);
 // the whole build in one workgroup for T <= small_build_max() (sorted pairs into
 // a.sorted_keys / a.sorted_vals, which must be writable)
 uint32_t small_build_max();
@@ -141,6 +144,7 @@ struct TraceArgs {
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)
+    const QNode8* qnode8;     // [2T-1] RTBVH_WIDE8 builds: 8-wide nodes (the certified bounce walk)
 };
 // primary-ray walks (trace.hip k_primary): per lane in reference order / nearest-first, wave
 // packets in reference order / nearest-first, 4-wide wave packets (axis-parallel box test)

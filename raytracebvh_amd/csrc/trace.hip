@@ -1498,6 +1498,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           unsigned long long* __restrict__ counters,
                                                           unsigned long long* __restrict__ overflow, int stack_limit) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
+    constexpr bool W8 = CERT && RTBVH_WIDE8;   // the certified walk on the 8-wide nodes (qn: QNode8s)
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
     const uint32_t n = *qin_count;
@@ -1719,6 +1720,63 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
                 if (node & LEAF_BIT) {
                     L = node;
                     node = INVALID;
+                } else if (W8) {
+                    // RTBVH_WIDE8: the 8-wide node (rtbvh_device.h QNode8, one 128-B line): eight certified box
+                    // tests on one grid; the nearest hit entry next (a leaf: tested in this step), the other hit
+                    // entries pushed in slot order (no sort: DESIGN.md 6, the CPU study's +4% steps)
+                    const v4f* rr = reinterpret_cast<const v4f*>(qn) + 8 * (size_t)node;
+                    v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3], q4 = rr[4], q5 = rr[5], q6 = rr[6];
+                    pin(q0); pin(q1); pin(q2); pin(q3); pin(q4); pin(q5); pin(q6);
+                    if (COUNT) c.internal++;
+                    if (q0.w == 0.f || sp + 7 > limit) {   // no grid, or no room for seven pushes: flagged
+                        if (q0.w != 0.f) c.overflow++;
+                        flg = true;
+                        done = true;
+                        node = INVALID;
+                    } else {
+                        const float kbb = key_t(key);
+                        const uint32_t wy = __float_as_uint(q1.x), wz = __float_as_uint(q1.y);
+                        const float sy = __uint_as_float(wy & 0xFF800000u), sz = __uint_as_float(wz & 0xFF800000u);
+                        const MtNodeRho nr = mt_node_prep(nk, mt_code_val(wy));
+                        const float tcn = mt_code_val(wz);
+                        const float rr0 = kbb < __builtin_inff() ? mt_node_eval(nr, kbb) : 0.f;
+                        QAxis X = qaxis<true>(q0.x, q0.w, __float_as_uint(q1.z), __float_as_uint(q2.y), o.x, inv.x, rr0),
+                              Y = qaxis<true>(q0.y, sy, __float_as_uint(q1.w), __float_as_uint(q2.z), o.y, inv.y, rr0),
+                              Z = qaxis<true>(q0.z, sz, __float_as_uint(q2.x), __float_as_uint(q2.w), o.z, inv.z, rr0);
+                        const f3 ai = mk(fabsf(inv.x), fabsf(inv.y), fabsf(inv.z));
+                        float t[8];
+                        bool h[8];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) h[k] = qbox_fast_cert(X, Y, Z, k, kbb, nk, nr, ai, tcn, t[k]);
+                        // entries 4..7: the same grid, their lo / hi words (near / far by the ray's signs)
+                        X.nw = inv.x < 0.f ? __float_as_uint(q4.w) : __float_as_uint(q4.x);
+                        X.fw = inv.x < 0.f ? __float_as_uint(q4.x) : __float_as_uint(q4.w);
+                        Y.nw = inv.y < 0.f ? __float_as_uint(q5.x) : __float_as_uint(q4.y);
+                        Y.fw = inv.y < 0.f ? __float_as_uint(q4.y) : __float_as_uint(q5.x);
+                        Z.nw = inv.z < 0.f ? __float_as_uint(q5.y) : __float_as_uint(q4.z);
+                        Z.fw = inv.z < 0.f ? __float_as_uint(q4.z) : __float_as_uint(q5.y);
+#pragma unroll
+                        for (int k = 0; k < 4; k++) h[4 + k] = qbox_fast_cert(X, Y, Z, k, kbb, nk, nr, ai, tcn, t[4 + k]);
+                        const uint32_t id[8] = {__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
+                                                __float_as_uint(q3.w), __float_as_uint(q5.z), __float_as_uint(q5.w),
+                                                __float_as_uint(q6.x), __float_as_uint(q6.y)};
+                        float km = __builtin_inff();
+                        uint32_t im = INVALID, cm = 8;
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            h[k] = h[k] && id[k] != INVALID;
+                            const bool b = h[k] && (t[k] < km || im == INVALID);
+                            km = b ? t[k] : km;
+                            im = b ? id[k] : im;
+                            cm = b ? (uint32_t)k : cm;
+                        }
+#pragma unroll
+                        for (int k = 7; k >= 0; k--)
+                            if (h[k] && (uint32_t)k != cm) wpush(id[k], t[k]);
+                        const bool lf = im != INVALID && (im & LEAF_BIT);
+                        L = lf ? im : INVALID;
+                        node = lf ? INVALID : im;
+                    }
                 } else {
                     const v4f* rr = reinterpret_cast<const v4f*>(qn + node);
                     v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
@@ -2102,7 +2160,8 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
                           float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, hipStream_t s) {
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
 #define RTBVH_BT(L, G, C)                                                                                              \
-    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner,                 \
+                       (C) && RTBVH_WIDE8 ? reinterpret_cast<const QNode*>(a.qnode8) : a.qnode, a.leaf,               \
                        a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;

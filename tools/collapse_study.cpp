@@ -375,6 +375,85 @@ int main(int argc, char** argv) {
             reached += best < INFINITY;
         }
     };
+    // STEPS=1: the bounce kernel's loop (trace.hip k_bounce_trav, WIDE): a step tests one QNode and then one
+    // leaf -- the nearest child when it is a leaf (the next child goes on without a push), or the leaf the
+    // step began at -- and pops until an entry's key is within the bound.  ORDER 0: the children by entry
+    // distance (the kernel's sort); 1: the nearest first, the others pushed in slot order (no sort)
+    uint64_t deep[4] = {0, 0, 0, 0};   // steps that end with > 13 / > 20 / > 32 stack entries, pushes
+    auto steps_walk = [&](const std::vector<QNodeE>& Q, int order, double& steps, double& qv, double& lt) {
+        uint64_t S = 0, V = 0, L = 0, D0 = 0, D1 = 0, D2 = 0, PU = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : S, V, L, D0, D1, D2, PU)
+        for (size_t i = 0; i < R; i++) {
+            const float* o = rays + 6 * i;
+            const float* d = o + 3;
+            const float inv[3] = {1.f / d[0], 1.f / d[1], 1.f / d[2]};
+            float best = INFINITY;
+            std::vector<std::pair<uint32_t, float>> st;
+            st.reserve(256);
+            constexpr uint32_t NONE = ~0u;
+            uint32_t node = root;
+            while (true) {
+                ++S;
+                uint32_t lf = NONE;
+                if (leaf(node)) {
+                    lf = node;
+                    node = NONE;
+                } else {
+                    ++V;
+                    std::pair<uint32_t, float> hit[WMAX];
+                    int nh = 0;
+                    for (int k = 0; k < Q[node].n; k++) {
+                        float tn;
+                        if (slab(o, inv, N[Q[node].e[k]], best, tn)) hit[nh++] = {Q[node].e[k], tn};
+                    }
+                    if (order == 0) {
+                        std::stable_sort(hit, hit + nh, [](auto& a, auto& b) { return a.second < b.second; });
+                    } else if (nh > 1) {   // the nearest to the front, the others in slot order
+                        int m = 0;
+                        for (int k = 1; k < nh; k++) if (hit[k].second < hit[m].second) m = k;
+                        std::rotate(hit, hit + m, hit + m + 1);
+                    }
+                    int k0 = 0;
+                    node = NONE;
+                    if (nh > 0 && leaf(hit[0].first)) { lf = hit[0].first; k0 = 1; }
+                    if (k0 < nh) node = hit[k0].first;
+                    for (int k = nh - 1; k > k0; k--) st.push_back(hit[k]);
+                    PU += nh > k0 ? nh - k0 - 1 : 0;
+                }
+                D0 += st.size() > 13;
+                D1 += st.size() > 20;
+                D2 += st.size() > 32;
+                if (lf != NONE) {
+                    for (uint32_t j = first[lf]; j < first[lf] + nleaf[lf]; j++) {
+                        ++L;
+                        const float h = tri_hit(o, d, tri + 9 * (size_t)j);
+                        if (h > 0.f && h < best) best = h;
+                    }
+                }
+                while (node == NONE && !st.empty()) {
+                    auto [x, t] = st.back();
+                    st.pop_back();
+                    if (t <= best) node = x;
+                }
+                if (node == NONE) break;
+            }
+        }
+        steps = (double)S / R;
+        deep[0] = D0; deep[1] = D1; deep[2] = D2; deep[3] = PU;
+        qv = (double)V / R;
+        lt = (double)L / R;
+    };
+    if (getenv("STEPS")) {
+        for (int order = 0; order < 2; order++) {
+            double sS, sV, sL;
+            steps_walk(greedy, order, sS, sV, sL);
+            printf("{\"T\": %u, \"rays\": %zu, \"width\": %d, \"order\": \"%s\", \"steps\": %.4f, \"qnode_visits\": %.4f, "
+                   "\"leaf_tests\": %.4f, \"steps_past_13_20_32_entries\": [%.4f, %.4f, %.4f], \"pushes\": %.4f}\n", T, R, W,
+                   order ? "nearest, slot order" : "sorted", sS, sV, sL, (double)deep[0] / R, (double)deep[1] / R,
+                   (double)deep[2] / R, (double)deep[3] / R);
+        }
+        return 0;
+    }
     if (const char* dump = getenv("DUMP")) {   // per-ray QNode visits of the greedy collapse (uint32)
         std::vector<uint32_t> vis(R);
 #pragma omp parallel for schedule(dynamic, 256)
