@@ -156,6 +156,8 @@ struct rtbvh_ctx {
     // set, the list of rays a pass re-traces in the reference order (their counts: d_qcount 16..31)
     uint32_t* d_redo[MAXSPLIT] = {};
     size_t cap_redo[MAXSPLIT] = {};
+    Park* d_park_rec[MAXSPLIT] = {};     // a certified trace's parked bounce rays (trace.hip k_bounce_tail)
+    uint2* d_park_stack[MAXSPLIT] = {};
     uint64_t cert_traces = 0;                         // certified traces so far
     uint32_t last_walk = 0;                           // walk flags of the last trace
     uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
@@ -754,6 +756,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
     }
     // a certified trace's re-trace list (one chain: buffer set `slot`; counts at d_qcount 16 + pass)
+    if (cert && bounces > 0 && PARK_STEPS > 0 && !c->d_park_rec[slot]) {   // (fixed size: PARK_CAP rays)
+        drop_graph(c);
+        HIPC(c, dalloc(c->d_park_rec[slot], PARK_CAP));
+        HIPC(c, dalloc(c->d_park_stack[slot], (size_t)PARK_CAP * STACK4B));
+    }
     if (cert && c->cap_redo[slot] < P) {
         drop_graph(c);
         HIPC(c, dalloc(c->d_redo[slot], P));
@@ -796,6 +803,8 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         TraceArgs ag = a;
         ag.band0 = g;
         ag.bstep = nsplit;
+        ag.park_rec = c->d_park_rec[g + slot];
+        ag.park_stack = c->d_park_stack[g + slot];
         const uint32_t b = g + slot;   // buffer set: chain g of the context stream's trace, or the slot
         RayQ* q[2] = {b ? c->d_qs[b][0] : c->d_q[0], b ? c->d_qs[b][1] : c->d_q[1]};
         float2* hit = b ? c->d_hits[b] : c->d_hit;
@@ -1074,6 +1083,8 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_counters);
     dfree(c->d_ovf);
     for (auto& r : c->d_redo) dfree(r);
+    for (auto& r : c->d_park_rec) dfree(r);
+    for (auto& r : c->d_park_stack) dfree(r);
     dfree(c->d_cam);
     for (auto& t : c->deals) free_deal(t);
     if (c->h_ovf) (void)hipHostFree(c->h_ovf);

@@ -145,7 +145,25 @@ struct TraceArgs {
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)
     const QNode8* qnode8;     // [2T-1] RTBVH_WIDE8 builds: 8-wide nodes (the certified bounce walk)
+    // the certified bounce walk's parked rays (RTBVH_PARK_STEPS, trace.hip k_bounce_tail): per buffer set,
+    // PARK_CAP records and PARK_CAP x STACK4B stack entries
+    struct Park* park_rec;
+    uint2* park_stack;
 };
+// a certified bounce ray parked after RTBVH_PARK_STEPS steps: its ray, stack depth, best hit so far;
+// its stack entries (node id, entry key bits) at park_stack[slot * STACK4B ...]
+struct Park {
+    uint32_t r, sp, btri, pad;
+    unsigned long long key;
+    unsigned long long pad2;
+};
+#ifndef RTBVH_PARK_STEPS
+#define RTBVH_PARK_STEPS 0   // off: A/B round 5, 64 / 128 / 256 all slower at N = 1
+#endif
+#ifndef RTBVH_PARK_CAP
+#define RTBVH_PARK_CAP 32768
+#endif
+constexpr uint32_t PARK_STEPS = RTBVH_PARK_STEPS, PARK_CAP = RTBVH_PARK_CAP;
 // primary-ray walks (trace.hip k_primary): per lane in reference order / nearest-first, wave
 // packets in reference order / nearest-first, 4-wide wave packets (axis-parallel box test)
 enum class PrimaryKind { LANE_REFERENCE, LANE_NEAREST, PACKET_REFERENCE, PACKET_NEAREST, PACKET_WIDE, BINNED };

@@ -1496,8 +1496,13 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          unsigned long long* __restrict__ overflow, int stack_limit) {
+                                                          unsigned long long* __restrict__ overflow, int stack_limit,
+                                                          Park* __restrict__ park_rec, uint2* __restrict__ park_stack) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
+    // PARK: a certified ray still walking after PARK_STEPS steps is parked (its stack to park_stack, the
+    // slot from the counter next[1]) for k_bounce_tail, which walks it one ray per wave
+    constexpr bool PARK = CERT && !COUNT && PARK_STEPS > 0 && !RTBVH_WIDE8;
+    uint32_t stp = 0;
     constexpr bool W8 = CERT && RTBVH_WIDE8;   // the certified walk on the 8-wide nodes (qn: QNode8s)
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
@@ -1688,6 +1693,7 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
                     top = INVALID;
                     node = root_slot(T);
                     guard = 2 * T + 2;
+                    stp = 0;
                     if (CERT) {   // a ray the margin does not cover ends at its first step, flagged
                         flg = !((qfast || RTBVH_CERT_EXACT) && dot(d, d) <= MT_DD);   // (exact decode: slack-free rays)
                         if (flg) node = INVALID;
@@ -1706,7 +1712,24 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
             mixed += (lf != 0 && lf != act);
         }
         if (!has) continue;
-        bool done = false;
+        bool done = false, parked = false;
+        if (PARK && ++stp == PARK_STEPS) {
+            // park: the stack and the node this step would visit (key 0: visited) go to the tail kernel
+            uint32_t slot = 0;
+            slot = atomicAdd(next + 1, 1u);
+            if (slot < PARK_CAP) {
+                uint2* st = park_stack + (size_t)slot * STACK4B;
+                for (int k = 0; k < sp; k++)
+                    st[k] = k < SW ? make_uint2(s_wid[k][tid], __float_as_uint(bf16_up(s_wt[k][tid]))) : wstack[k - SW];
+                st[sp] = make_uint2(node, 0u);
+                Park pr;
+                pr.r = r; pr.sp = (uint32_t)sp + 1; pr.btri = btri; pr.pad = 0; pr.key = key; pr.pad2 = 0;
+                park_rec[slot] = pr;
+                parked = true;
+                has = false;
+            }
+        }
+        if (parked) continue;
         if (WIDE) {
             // A step: the QNode of an internal `node`, then one leaf test -- the nearest child when it
             // is a leaf (the next child is visited), or the leaf the step began at -- so a leaf found
@@ -1930,6 +1953,134 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
                 atomicAdd(&counters[8], v[2]);
                 atomicAdd(overflow, v[2]);
             }
+        }
+    }
+}
+
+// The parked rays of a certified bounce pass (k_bounce_trav PARK: still walking after PARK_STEPS steps), one
+// ray per wave: each round the wave pops up to 64 entries off the ray's stack (LDS), every lane one -- an
+// entry past the bound is dropped, a leaf is tested, an internal node's QNode gets the walk's four certified
+// box tests and its hit entries are pushed (a wave prefix sum places them) -- and the leaves' (t, leaf) keys
+// fold into the ray's minimum.  The walk visits every entry the lane walk would (an entry is dropped only by
+// the bound, as there) and perhaps more, so its (t, leaf) minimum is the same; the certificate is checked by
+// k_bounce_shade as for every ray.  A stack past TSTK entries or a node without a grid flags the ray
+// (HIT_FLAG: re-traced in the reference order by k_bounce_redo).  A long walk's dependent steps become
+// rounds of up to 64 independent fetches.
+constexpr uint32_t TSTK = 1024;   // LDS stack entries per wave (8 KB)
+__global__ __launch_bounds__(BLOCK) void k_bounce_tail(const QNode* __restrict__ qn, const float4* __restrict__ leaf,
+                                                       const RayQ* __restrict__ qin, const uint32_t* __restrict__ next,
+                                                       const Park* __restrict__ park_rec,
+                                                       const uint2* __restrict__ park_stack,
+                                                       float2* __restrict__ hitrec) {
+    __shared__ uint32_t s_id[BLOCK / 64][TSTK];
+    __shared__ float s_key[BLOCK / 64][TSTK];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t* sid = s_id[w];
+    float* skey = s_key[w];
+    const uint32_t n = min(next[1], PARK_CAP);
+    const MtNodeK nk = mt_node_consts();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t p = blockIdx.x * (BLOCK / 64) + w; p < n; p += gridDim.x * (BLOCK / 64)) {
+        const Park pr = park_rec[p];
+        const uint32_t r = pr.r;
+        uint32_t sp = min(pr.sp, (uint32_t)STACK4B);
+        uint64_t key = pr.key;
+        uint32_t btri = pr.btri;
+        const float4 q0r = reinterpret_cast<const float4*>(qin + r)[0];
+        const float4 q1r = reinterpret_cast<const float4*>(qin + r)[1];
+        const f3 o = mk(q0r.z, q0r.w, q1r.x), d = mk(q1r.y, q1r.z, q1r.w);
+        const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+        const f3 ai = mk(fabsf(inv.x), fabsf(inv.y), fabsf(inv.z));
+        for (uint32_t k = lane; k < sp; k += 64) {
+            const uint2 e = park_stack[(size_t)p * STACK4B + k];
+            sid[k] = e.x;
+            skey[k] = __uint_as_float(e.y);
+        }
+        bool flg = false;
+        while (sp > 0 && !flg) {
+            const uint32_t m = min(sp, 64u);
+            sp -= m;
+            const float kbb = key_t(key);
+            const bool act = lane < m;
+            const uint32_t id = act ? sid[sp + lane] : INVALID;
+            const float ke = act ? skey[sp + lane] : INFINITY;
+            const bool live = act && ke <= kbb;
+            // a leaf: its (t, leaf) key
+            uint64_t ck = ~0ull;
+            uint32_t ctri = INVALID;
+            if (live && (id & LEAF_BIT)) {
+                const uint32_t j = id & ~LEAF_BIT;
+                const v4f* lr = reinterpret_cast<const v4f*>(leaf + 4 * (size_t)j);
+                const v4f la = lr[0], lb = lr[1], lc = lr[2];
+                const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
+                                                   mk(lb.z, lb.w, lc.x), true);
+                if (tw != -1.f) {
+                    ck = (uint64_t)__float_as_uint(tw) << 32 | j;
+                    ctri = __float_as_uint(lc.y) & ~LEAF_BIT;
+                }
+            }
+            // an internal node: its four certified box tests (k_bounce_trav's qchildren, CERT)
+            bool h0 = false, h1 = false, h2 = false, h3 = false, nogrid = false;
+            float k0 = 0.f, k1 = 0.f, k2 = 0.f, k3 = 0.f;
+            uint32_t i0 = INVALID, i1 = INVALID, i2 = INVALID, i3 = INVALID;
+            if (live && !(id & LEAF_BIT)) {
+                const v4f* rr = reinterpret_cast<const v4f*>(qn + id);
+                const v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
+                if (q0.w == 0.f) {
+                    nogrid = true;
+                } else {
+                    const uint32_t wy = __float_as_uint(q1.x), wz = __float_as_uint(q1.y);
+                    const float sy = __uint_as_float(wy & 0xFF800000u), sz = __uint_as_float(wz & 0xFF800000u);
+                    const MtNodeRho nr = mt_node_prep(nk, mt_code_val(wy));
+                    const float tcn = mt_code_val(wz);
+                    const float rr0 = kbb < __builtin_inff() ? mt_node_eval(nr, kbb) : 0.f;
+                    const QAxis X = qaxis<true>(q0.x, q0.w, __float_as_uint(q1.z), __float_as_uint(q2.y), o.x, inv.x, rr0),
+                                Y = qaxis<true>(q0.y, sy, __float_as_uint(q1.w), __float_as_uint(q2.z), o.y, inv.y, rr0),
+                                Z = qaxis<true>(q0.z, sz, __float_as_uint(q2.x), __float_as_uint(q2.w), o.z, inv.z, rr0);
+                    h0 = qbox_fast_cert(X, Y, Z, 0, kbb, nk, nr, ai, tcn, k0);
+                    h1 = qbox_fast_cert(X, Y, Z, 1, kbb, nk, nr, ai, tcn, k1);
+                    h2 = qbox_fast_cert(X, Y, Z, 2, kbb, nk, nr, ai, tcn, k2);
+                    h3 = qbox_fast_cert(X, Y, Z, 3, kbb, nk, nr, ai, tcn, k3);
+                    i0 = __float_as_uint(q3.x); i1 = __float_as_uint(q3.y);
+                    i2 = __float_as_uint(q3.z); i3 = __float_as_uint(q3.w);
+                    h1 = h1 && i1 != INVALID;
+                    h3 = h3 && i3 != INVALID;
+                }
+            }
+            if (__ballot(nogrid)) {   // (the lane walk flags these rays too)
+                flg = true;
+                break;
+            }
+            // the wave's smallest (t, leaf) key, and its triangle
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t ok = (uint64_t)__shfl_xor((long long)ck, off, 64);
+                const uint32_t ot = (uint32_t)__shfl_xor((int)ctri, off, 64);
+                if (ok < ck) { ck = ok; ctri = ot; }
+            }
+            if (ck < key) { key = ck; btri = ctri; }
+            // the hit entries onto the stack: per child position c, the lanes with a hit in a block
+            const uint32_t nh = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
+            uint32_t tot = 0;
+            const uint64_t b0 = __ballot(h0), b1 = __ballot(h1), b2 = __ballot(h2), b3 = __ballot(h3);
+            const uint32_t c0 = (uint32_t)__popcll(b0), c1 = (uint32_t)__popcll(b1), c2 = (uint32_t)__popcll(b2),
+                           c3 = (uint32_t)__popcll(b3);
+            tot = c0 + c1 + c2 + c3;
+            (void)nh;
+            if (sp + tot > TSTK) {
+                flg = true;
+                break;
+            }
+            if (h0) { const uint32_t a = sp + (uint32_t)__popcll(b0 & lt); sid[a] = i0; skey[a] = k0; }
+            if (h1) { const uint32_t a = sp + c0 + (uint32_t)__popcll(b1 & lt); sid[a] = i1; skey[a] = k1; }
+            if (h2) { const uint32_t a = sp + c0 + c1 + (uint32_t)__popcll(b2 & lt); sid[a] = i2; skey[a] = k2; }
+            if (h3) { const uint32_t a = sp + c0 + c1 + c2 + (uint32_t)__popcll(b3 & lt); sid[a] = i3; skey[a] = k3; }
+            sp += tot;
+        }
+        if (lane == 0) {
+            uint32_t wd = key != NO_HIT ? btri : INVALID;
+            if (flg) wd ^= HIT_FLAG;
+            hitrec[r] = make_float2(key_t(key), __uint_as_float(wd));
         }
     }
 }
@@ -2162,12 +2313,15 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
 #define RTBVH_BT(L, G, C)                                                                                              \
     hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner,                 \
                        (C) && RTBVH_WIDE8 ? reinterpret_cast<const QNode*>(a.qnode8) : a.qnode, a.leaf,               \
-                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, a.park_rec, a.park_stack)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
     if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
         if (guard) RTBVH_BT(false, true, MODE == 2);
         else RTBVH_BT(false, false, MODE == 2);
+        if (!COUNT && PARK_STEPS > 0 && !RTBVH_WIDE8)   // the parked rays (k_bounce_trav PARK)
+            hipLaunchKernelGGL(k_bounce_tail, dim3(512), dim3(BLOCK), 0, s, a.qnode, a.leaf, qin, next, a.park_rec,
+                               a.park_stack, hitrec);
     } else if (a.limited) { if (guard) RTBVH_BT(true, true, false); else RTBVH_BT(true, false, false); }
     else { if (guard) RTBVH_BT(false, true, false); else RTBVH_BT(false, false, false); }
 #undef RTBVH_BT
