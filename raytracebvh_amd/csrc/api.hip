@@ -116,6 +116,8 @@ struct rtbvh_ctx {
         unsigned long long* keys = nullptr;
         uint32_t cap_T = 0, cap_tiles = 0, cap_bins = 0;
         size_t cap_px = 0;
+        uint32_t* list = nullptr;   // N > 1: the rank's leaves (TraceArgs::pb_list)
+        size_t cap_list = 0;
     } pb[MAXSPLIT];
     unsigned long long* d_counters = nullptr; // [64]: see rtbvh_get_stats
     bool traced = false;
@@ -771,6 +773,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (pkind == PrimaryKind::BINNED) {
         st = ensure_pb_capacity(c, slot, c->T, ntx * nty, (size_t)W * rows);
         if (st) return st;
+        if (nranks > 1 && c->pb[slot].cap_list < pb_list_words(c->T)) {
+            drop_graph(c);
+            HIPC(c, dalloc(c->pb[slot].list, pb_list_words(c->T)));
+            c->pb[slot].cap_list = pb_list_words(c->T);
+        }
     }
     // the trace's counters, queue counts, bounce work counters and bin counts: one launch
     ZeroList z{};
@@ -785,6 +792,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     if (pkind == PrimaryKind::BINNED) {
         z.ptr[3] = c->pb[slot].off;
         z.words[3] = (size_t)ntx * nty * PB_NZ + 1;
+        if (nranks > 1) {   // the list counters
+            z.ptr[4] = c->pb[slot].list;
+            z.words[4] = (size_t)PB_LISTS * PB_LIST_STRIDE;
+        }
+
     }
     // rtbvh_compute_bvh: the binned pass (and the zeroing before it) on the side stream, concurrent
     // with the build's crossing nodes (launch_refit_tail)
@@ -803,6 +815,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         TraceArgs ag = a;
         ag.band0 = g;
         ag.bstep = nsplit;
+        ag.pb_list = pkind == PrimaryKind::BINNED && nranks > 1 ? c->pb[g + slot].list : nullptr;
         ag.park_rec = c->d_park_rec[g + slot];
         ag.park_stack = c->d_park_stack[g + slot];
         const uint32_t b = g + slot;   // buffer set: chain g of the context stream's trace, or the slot
@@ -1083,6 +1096,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_counters);
     dfree(c->d_ovf);
     for (auto& r : c->d_redo) dfree(r);
+    for (auto& p : c->pb) dfree(p.list);
     for (auto& r : c->d_park_rec) dfree(r);
     for (auto& r : c->d_park_stack) dfree(r);
     dfree(c->d_cam);

@@ -36,7 +36,7 @@ __device__ __forceinline__ void pb_rows(const TraceArgs& a, int y0, int y1, int&
 // global atomics are one per bin and workgroup instead of one per wave and bin; in pass 2 the
 // table's returned bases and LDS cursors place every entry.  A bin the full table cannot hold takes
 // a global atomic of its own (correct either way).
-constexpr uint32_t PB_LEAVES = 1024;      // leaves per workgroup (4 per thread)
+// (PB_LEAVES, rtbvh_internal.h: leaves per workgroup, 4 per thread)
 constexpr uint32_t PB_HASH = 1024;        // LDS table slots
 constexpr uint32_t PB_EMPTY = 0xFFFFFFFFu;
 __device__ __forceinline__ int pb_slot_of(uint32_t* h_key, uint32_t key, bool insert) {
@@ -56,15 +56,31 @@ __device__ __forceinline__ void pb_bin_block(const TraceArgs& a, uint32_t bid, u
                                              uint32_t* __restrict__ cur, uint4* __restrict__ bins, uint32_t cap,
                                              uint32_t ntx) {
     __shared__ uint32_t h_key[PB_HASH], h_cnt[PB_HASH], h_base[FILL ? PB_HASH : 1];
+    // N > 1 (a.pb_list): the count pass appends the rank's leaves to one of PB_LISTS lists (count block bid to
+    // list bid % PB_LISTS: one atomic per block on its list's counter), and fill block bid takes the 1024
+    // entries at (bid / PB_LISTS) * 1024 of list bid % PB_LISTS -- blocks past a list's end return at once
+    uint32_t* const list = a.pb_list;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t lk = bid % PB_LISTS, rcap = pb_list_cap(a.T);
+    uint32_t* const lcnt = list ? list + PB_LIST_STRIDE * lk : nullptr;
+    uint32_t* const lent = list ? list + PB_LISTS * PB_LIST_STRIDE + (size_t)lk * rcap : nullptr;
+    const uint32_t nlist = FILL && list ? min(*lcnt, rcap) : 0u;
+    const uint32_t lbase = (bid / PB_LISTS) * PB_LEAVES;
+    if (FILL && list && lbase >= nlist) return;   // (uniform over the block)
     for (uint32_t i = threadIdx.x; i < PB_HASH; i += BLOCK) { h_key[i] = PB_EMPTY; h_cnt[i] = 0; }
     __syncthreads();
     constexpr uint32_t LPT = PB_LEAVES / BLOCK;
     uint4 f[LPT];
-    uint32_t zb[LPT];
+    uint32_t zb[LPT], jj[LPT];
     const float zlo = a.rootbox[6], zhi = a.rootbox[7];   // the leaves' depth range (= the root box's)
 #pragma unroll
     for (uint32_t i = 0; i < LPT; i++) {
-        const uint32_t j = bid * PB_LEAVES + i * BLOCK + threadIdx.x;
+        uint32_t j = bid * PB_LEAVES + i * BLOCK + threadIdx.x;
+        if (FILL && list) {
+            const uint32_t e = lbase + i * BLOCK + threadIdx.x;
+            j = e < nlist ? lent[e] : a.T;
+        }
+        jj[i] = j;
         f[i] = make_uint4(1, 1, 0, 0);   // empty: x0 = 1 > x1 = 0
         if (j < a.T) {
             {   // the build's footprint (pixel offsets from the frame centre) on this frame and rank
@@ -81,6 +97,30 @@ __device__ __forceinline__ void pb_bin_block(const TraceArgs& a, uint32_t bid, u
         // the depth bucket of min.z in the root box's depth range (general boxes first: they always test)
         const float u = (__uint_as_float(f[i].z) - zlo) / (zhi - zlo) * (float)PB_NZ;
         zb[i] = f[i].w ? 0u : (uint32_t)fminf(fmaxf(u, 0.f), (float)(PB_NZ - 1));   // NaN: 0
+    }
+    if (!FILL && list) {   // the rank's leaves (a footprint in its rows) appended to list lk: one atomic a block
+        __shared__ uint32_t s_wn[BLOCK / 64], s_base;
+        uint32_t mine = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < LPT; i++) mine += (f[i].x & 0xFFFFu) <= (f[i].x >> 16) ? 1u : 0u;
+        uint32_t x = mine;   // inclusive scan over the wave
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t y = __shfl_up(x, dd, 64);
+            if ((int)lane >= dd) x += y;
+        }
+        if (lane == 63) s_wn[wv] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (uint32_t k = 0; k < BLOCK / 64; k++) { const uint32_t v = s_wn[k]; s_wn[k] = t; t += v; }
+            s_base = t ? atomicAdd(lcnt, t) : 0u;
+        }
+        __syncthreads();
+        uint32_t at = s_base + s_wn[wv] + x - mine;
+#pragma unroll
+        for (uint32_t i = 0; i < LPT; i++)
+            if ((f[i].x & 0xFFFFu) <= (f[i].x >> 16)) lent[at++] = jj[i];
     }
     // the (leaf, bin) pairs of item i, visited by `body(key)`
     const auto pairs = [&](uint32_t i, auto&& body) {
@@ -112,7 +152,7 @@ __device__ __forceinline__ void pb_bin_block(const TraceArgs& a, uint32_t bid, u
     __syncthreads();
 #pragma unroll
     for (uint32_t i = 0; i < LPT; i++) {
-        const uint32_t j = bid * PB_LEAVES + i * BLOCK + threadIdx.x;
+        const uint32_t j = jj[i];
         const uint4 entry = make_uint4(f[i].x, f[i].y, f[i].z, j | (f[i].w ? LEAF_BIT : 0u));
         pairs(i, [&](uint32_t key) {
             const int sl = pb_slot_of(h_key, key, false);

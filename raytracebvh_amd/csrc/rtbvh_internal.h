@@ -145,6 +145,10 @@ struct TraceArgs {
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)
     const QNode8* qnode8;     // [2T-1] RTBVH_WIDE8 builds: 8-wide nodes (the certified bounce walk)
+    // N > 1, the binned pass's bins: the leaves whose footprint meets the rank's rows, in PB_LISTS lists (the
+    // count pass appends them, the fill pass reads only them; null at N = 1, where every leaf is read):
+    // counters PB_LIST_STRIDE words apart, then the lists, pb_list_cap(T) entries each (pb_bin.h)
+    uint32_t* pb_list;
     // the certified bounce walk's parked rays (RTBVH_PARK_STEPS, trace.hip k_bounce_tail): per buffer set,
     // PARK_CAP records and PARK_CAP x STACK4B stack entries
     struct Park* park_rec;
@@ -183,6 +187,13 @@ constexpr uint32_t REDO_BLOCKS = 512;
 // tiles (columns x compact band rows), every leaf listed in the tiles its box covers
 constexpr uint32_t PB_TILE = 32;
 constexpr uint32_t PB_NZ = 16;   // depth buckets per tile: a tile's bins are listed nearest bucket first
+constexpr uint32_t PB_LEAVES = 1024;   // the bin passes' leaves per workgroup (pb_bin.h)
+constexpr uint32_t PB_LISTS = 16, PB_LIST_STRIDE = 32;   // TraceArgs::pb_list: lists, counter spacing (words)
+// entries per list: the leaves of every PB_LISTS-th count block
+inline __host__ __device__ uint32_t pb_list_cap(uint32_t T) {
+    return ((T + PB_LEAVES - 1) / PB_LEAVES + PB_LISTS - 1) / PB_LISTS * PB_LEAVES;
+}
+inline size_t pb_list_words(uint32_t T) { return (size_t)PB_LISTS * PB_LIST_STRIDE + (size_t)PB_LISTS * pb_list_cap(T); }
 struct PrimBins {
     uint32_t* off;    // [tiles * PB_NZ + 1] leaves per (tile, depth bucket), then their offsets (exclusive
                       //   scan), [tiles * PB_NZ] the total
@@ -212,7 +223,7 @@ void launch_pb_gate(const TraceArgs& a, const PrimBins& pb, RayQ* q, uint32_t* q
                     hipStream_t s, bool reference);
 // up to N arrays of 32-bit words zeroed by one launch (null / 0 words: unused)
 struct ZeroList {
-    static constexpr int N = 4;
+    static constexpr int N = 5;
     uint32_t* ptr[N];
     size_t words[N];
 };

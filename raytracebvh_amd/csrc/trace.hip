@@ -2361,6 +2361,7 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
     if (rows == 0 || a.W == 0 || a.T == 0) return;
     const uint32_t keys = pb.ntx * pb.nty * PB_NZ;
     if (!zeroed) (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
+    if (!zeroed && a.pb_list) (void)hipMemsetAsync(a.pb_list, 0, (size_t)PB_LISTS * PB_LIST_STRIDE * sizeof(uint32_t), s);
     const dim3 lg((a.T + PB_LEAVES - 1) / PB_LEAVES);
     if (tail) launch_pb_count_top(*tail, a, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx, lg.x, s);
     else hipLaunchKernelGGL((k_pb_bin<false>), lg, dim3(BLOCK), 0, s, a, pb.off, pb.cur, pb.bins, pb.cap, pb.ntx);
