@@ -687,11 +687,13 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const uint32_t P = W * deal_rows(H, rank, nranks, c->root_share);   // max live rays of this shard
     // persistent grid of the bounce walk: 2048 blocks (8 waves/SIMD), 1024 for a shard of
     // < 4M pixels -- with frames in flight the next frame's primary blocks then share the CUs
-    // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame)
+    // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame) -- and 512 below 3M pixels once
+    // frames are in flight on caller streams (round 5, four in flight, `r05_hh`: the N = 8 rank 0.62 -> 0.60
+    // ms per frame, N = 4 1.03 -> 1.00; one frame at a time 512 is slower, 1.13 -> 1.37 ms at N = 8)
 #ifndef RTBVH_BOUNCE_GRID
 #define RTBVH_BOUNCE_GRID (256 * BOUNCE_WAVES)
 #endif
-    uint32_t tblocks = P < (1u << 22) ? 1024 : RTBVH_BOUNCE_GRID;
+    uint32_t tblocks = P < (1u << 22) ? (c->slots_used && P < (3u << 20) ? 512 : 1024) : RTBVH_BOUNCE_GRID;
     if (c->knob_bounce_blocks) tblocks = c->knob_bounce_blocks;   // tuning override (A/B runs)
     if (records) {
         if (c->cap_rec < P) {
