@@ -179,6 +179,15 @@ def cpu_model() -> str:
 NODE_FIELDS = ("parent", "child_l", "child_r", "code", "index", "bb_min", "bb_max")
 
 
+def affinity_cpus():
+    """The CPUs this process may run on (len(os.sched_getaffinity(0))): on the GPU boxes the process's share
+    of the host, next to OMP_NUM_THREADS (16 there, set by the box) -- the thread count is the box's cap."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+
+
 def cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame):
     """The oracle (C++ restatement of the reference path, oracle/) on the GPU box's host cores:
     its own BVH of the bench scene (the parity check of the tree), a single-thread trace
@@ -223,7 +232,7 @@ def cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame):
     res = {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
            "sample": f"oracle/liboracle.so orc_trace of 1 row in {step} of the same frame, on the oracle's own BVH "
                      f"of the same scene ({st['primary']} primary + {st['bounce']} bounce rays, {dt:.1f} s, 1 thread)",
-           "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": affinity_cpus()}
     # BASELINE.md's all-cores variant: the same code, OpenMP over rows, on this process's CPU
     # share, over the WHOLE frame (the parity check)
     orc.set_threads(threads)
@@ -234,6 +243,7 @@ def cpu_baseline(rt, scene, ctx, wl, W, H, gpu_frame):
     finally:
         orc.set_threads(1)
     res["openmp"] = {"value": (st2["primary"] + st2["bounce"]) / dt2 / 1e6, "unit": "Mrays/s", "cores": threads,
+                     "affinity_cpus": affinity_cpus(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
                      "sample": f"every row, {st2['primary']} primary + {st2['bounce']} bounce rays, "
                                f"{dt2:.1f} s, OpenMP over rows on {threads} threads (OMP_NUM_THREADS: the "
                                f"process's CPU share, not all {os.cpu_count()} host CPUs)"}

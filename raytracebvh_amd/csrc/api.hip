@@ -73,8 +73,6 @@ struct rtbvh_ctx {
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
     bool pseudo_ok = false;      // the built tree has its leaf pseudo-records (read by the packet walks only)
     bool qnode_ok = false;       // the built tree has its QNodes (read by the 4-wide bounce walk only)
-    bool q8_ok = false;          // RTBVH_WIDE8: the built tree has its 8-wide nodes (the certified bounce walk)
-    QNode8* d_qnode8 = nullptr;  // RTBVH_WIDE8: 8-wide nodes in slots, 2T-1
     // rtbvh_compute_bvh: the build leaves its crossing nodes (launch_refit_tail) to the frame's binned
     // pass, which runs them in its bin launches (launch_pb_bin_tail); any other first use of the tree
     // runs them first (flush_tail)
@@ -158,15 +156,15 @@ struct rtbvh_ctx {
     // set, the list of rays a pass re-traces in the reference order (their counts: d_qcount 16..31)
     uint32_t* d_redo[MAXSPLIT] = {};
     size_t cap_redo[MAXSPLIT] = {};
-    Park* d_park_rec[MAXSPLIT] = {};     // a certified trace's parked bounce rays (trace.hip k_bounce_tail)
-    uint2* d_park_stack[MAXSPLIT] = {};
     uint64_t cert_traces = 0;                         // certified traces so far
     uint32_t last_walk = 0;                           // walk flags of the last trace
     uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
     // RTBVH_FLAG_AUTO_WALK at <= AUTO_WALK_MAX_TRIS: the primary kind, the reference order's lanes or its
     // wave packets (the same frame), timed on this scene and frame size (enqueue_trace)
     uint64_t small_key = 0;
+    uint32_t small_flags = 0;     // the flags the small-scene primary kind was timed under
     bool small_packet = false;
+    hipEvent_t ev_small[2] = {};  // its timing events (created on first use, destroyed with the context)
     bool last_cert = false;                           // the last trace was certified (its re-trace counts)
     // tuning knobs of A/B runs, read once by rtbvh_create (RTBVH_BOUNCE_BLOCKS, RTBVH_OVERLAP,
     // RTBVH_SIDE_PRIORITY): a shipped context does not change its launches per frame
@@ -242,7 +240,6 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_topo, ni));
     HIPC(c, dalloc(c->d_rec, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_qnode, 2 * (size_t)n - 1));
-    if (RTBVH_WIDE8) HIPC(c, dalloc(c->d_qnode8, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_lfp, n));
     HIPC(c, dalloc(c->d_pleaf, n));
     HIPC(c, dalloc(c->d_pint, ni));
@@ -364,7 +361,6 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.xcnt = c->d_xcnt;
     a.rootbox = c->d_rootbox;
     a.qnode = c->d_qnode;
-    a.qnode8 = c->d_qnode8;
     a.lfp = c->d_lfp;
     a.zpart = c->d_zpart;
     // the leaf pseudo-records cost the build 0.64 GB of writes at 10M triangles: written when the
@@ -488,7 +484,6 @@ TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32
     a.inner = c->d_rec;
     a.leaf = c->d_leaf;
     a.qnode = c->d_qnode;
-    a.qnode8 = c->d_qnode8;
     a.rootbox = c->d_rootbox;
     a.lfp = c->d_lfp;
     a.tclip = c->d_tclip;
@@ -693,7 +688,12 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
 #ifndef RTBVH_BOUNCE_GRID
 #define RTBVH_BOUNCE_GRID (256 * BOUNCE_WAVES)
 #endif
-    uint32_t tblocks = P < (1u << 22) ? (c->slots_used && P < (3u << 20) ? 512 : 1024) : RTBVH_BOUNCE_GRID;
+    // ("in flight": this trace is on a caller stream's slot, or another slot's frame is still running --
+    // not a flag that stays set once any caller stream has traced: ADVICE r5)
+    bool inflight = slot != 0;
+    for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT && !inflight && !c->capturing; k++)
+        inflight = c->slot_busy[k] && hipEventQuery(c->ev_slot[k]) == hipErrorNotReady;
+    uint32_t tblocks = P < (1u << 22) ? (inflight && P < (3u << 20) ? 512 : 1024) : RTBVH_BOUNCE_GRID;
     if (c->knob_bounce_blocks) tblocks = c->knob_bounce_blocks;   // tuning override (A/B runs)
     if (records) {
         if (c->cap_rec < P) {
@@ -740,15 +740,6 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
         if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
     }
-    // RTBVH_WIDE8: the certified bounce walk's 8-wide nodes, once per build, from the complete tree (the
-    // fused tail completes it inside the binned pass: then right after it, below)
-    const bool need_q8 = RTBVH_WIDE8 && cert && bounces > 0 && !c->q8_ok;
-    if (need_q8 && !fuse_tail) {
-        launch_qnodes8(build_args(c), c->stream);
-        c->q8_ok = true;
-        if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
-        if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
-    }
     if (!c->pseudo_ok && (pkind == PrimaryKind::PACKET_REFERENCE || pkind == PrimaryKind::PACKET_NEAREST ||
                           pkind == PrimaryKind::PACKET_WIDE)) {
         // a packet walk over a tree built without the leaf pseudo-records (the context's walks took
@@ -760,11 +751,6 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
     }
     // a certified trace's re-trace list (one chain: buffer set `slot`; counts at d_qcount 16 + pass)
-    if (cert && bounces > 0 && PARK_STEPS > 0 && !c->d_park_rec[slot]) {   // (fixed size: PARK_CAP rays)
-        drop_graph(c);
-        HIPC(c, dalloc(c->d_park_rec[slot], PARK_CAP));
-        HIPC(c, dalloc(c->d_park_stack[slot], (size_t)PARK_CAP * STACK4B));
-    }
     if (cert && c->cap_redo[slot] < P) {
         drop_graph(c);
         HIPC(c, dalloc(c->d_redo[slot], P));
@@ -818,8 +804,6 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         ag.band0 = g;
         ag.bstep = nsplit;
         ag.pb_list = pkind == PrimaryKind::BINNED && nranks > 1 ? c->pb[g + slot].list : nullptr;
-        ag.park_rec = c->d_park_rec[g + slot];
-        ag.park_stack = c->d_park_stack[g + slot];
         const uint32_t b = g + slot;   // buffer set: chain g of the context stream's trace, or the slot
         RayQ* q[2] = {b ? c->d_qs[b][0] : c->d_q[0], b ? c->d_qs[b][1] : c->d_q[1]};
         float2* hit = b ? c->d_hits[b] : c->d_hit;
@@ -838,11 +822,6 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
                 if (overlap) {
                     HIPC(c, hipEventRecord(c->ev_prim, sp));
                     HIPC(c, hipStreamWaitEvent(sg, c->ev_prim, 0));
-                }
-                if (need_q8 && fuse_tail) {   // (after the join: fuse_tail's sg is the context stream)
-                    launch_qnodes8(build_args(c), sg);
-                    c->q8_ok = true;
-                    if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, sg));
                 }
                 launch_pb_gate(ag, pb, q[0], &qc[0], count, bounces > 0, sg, cert);
             } else if (overlap) {   // (nothing traced: the zeroing still joins)
@@ -948,31 +927,32 @@ rtbvh_status enqueue_trace(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     const bool limited = c->cfg.stack_limit != 0 && c->cfg.stack_limit < (uint32_t)STACK_SIZE;
     if ((f & RTBVH_FLAG_AUTO_WALK) && !p.cert && c->built_clz64 && !limited) {
         const uint64_t key = (uint64_t)W << 48 | (uint64_t)H << 32 | c->T;
-        if (c->small_key != key && !c->capturing && s == c->stream && slot == 0 && nranks == 1) {
-            hipEvent_t ev[2] = {};
-            HIPC(c, hipEventCreate(&ev[0]));
-            HIPC(c, hipEventCreate(&ev[1]));
+        // (the first frame of a key is synchronous: it waits for its own timed passes; the key includes the
+        // walk flags, so a set_flags that changes the walks times them again)
+        const uint32_t fw = f & (WALK_FLAGS | RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_CERTIFIED | RTBVH_FLAG_SORT_BOUNCE);
+        if ((c->small_key != key || c->small_flags != fw) && !c->capturing && s == c->stream && slot == 0 &&
+            nranks == 1) {
+            hipEvent_t* ev = c->ev_small;
+            for (int k = 0; k < 2; k++)
+                if (!ev[k]) HIPC(c, hipEventCreate(&ev[k]));
             float best[2] = {INFINITY, INFINITY};
-            rtbvh_status cs = RTBVH_OK;
-            for (int round = 0; round < 2 && !cs; round++)
-                for (int k = 0; k < 2 && !cs; k++) {
+            for (int round = 0; round < 2; round++)
+                for (int k = 0; k < 2; k++) {
                     HIPC(c, hipEventRecord(ev[0], s));
-                    cs = enqueue_walks(c, W, H, 0, 0, 1, color, inten, s, 0,
-                                       p.flags | (k ? RTBVH_FLAG_PACKET_PRIMARY : 0u), false);
-                    if (cs) break;
+                    rtbvh_status cs = enqueue_walks(c, W, H, 0, 0, 1, color, inten, s, 0,
+                                                    p.flags | (k ? RTBVH_FLAG_PACKET_PRIMARY : 0u), false);
+                    if (cs) return cs;
                     HIPC(c, hipEventRecord(ev[1], s));
                     HIPC(c, hipEventSynchronize(ev[1]));
                     float ms = 0.f;
                     HIPC(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
                     best[k] = std::min(best[k], ms);
                 }
-            (void)hipEventDestroy(ev[0]);
-            (void)hipEventDestroy(ev[1]);
-            if (cs) return cs;
             c->small_packet = best[1] < 0.95f * best[0];
             c->small_key = key;
+            c->small_flags = fw;
         }
-        if (c->small_key == key && c->small_packet) p.flags |= RTBVH_FLAG_PACKET_PRIMARY;
+        if (c->small_key == key && c->small_flags == fw && c->small_packet) p.flags |= RTBVH_FLAG_PACKET_PRIMARY;
     }
     return enqueue_walks(c, W, H, bounces, rank, nranks, color, inten, s, slot, p.flags, true, p.cert);
 }
@@ -1083,12 +1063,14 @@ void rtbvh_destroy(rtbvh_ctx* c) {
         (void)hipStreamSynchronize(c->side);
         (void)hipStreamDestroy(c->side);
     }
+    for (hipEvent_t e : c->ev_small)
+        if (e) (void)hipEventDestroy(e);
     if (c->ev_leaf) (void)hipEventDestroy(c->ev_leaf);
     if (c->ev_prim) (void)hipEventDestroy(c->ev_prim);
     for (auto& p : c->pb) { dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_qnode8); dfree(c->d_lfp);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_lfp);
     dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
@@ -1099,8 +1081,6 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_ovf);
     for (auto& r : c->d_redo) dfree(r);
     for (auto& p : c->pb) dfree(p.list);
-    for (auto& r : c->d_park_rec) dfree(r);
-    for (auto& r : c->d_park_stack) dfree(r);
     dfree(c->d_cam);
     for (auto& t : c->deals) free_deal(t);
     if (c->h_ovf) (void)hipHostFree(c->h_ovf);
@@ -1244,7 +1224,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
         c->built = true;
         c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
-        c->q8_ok = false;
         return check_launch(c, "build kernel");
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
@@ -1291,7 +1270,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, s));
     c->built = true;
     c->built_clz64 = c->cfg.delta_mode == RTBVH_DELTA_CLZ64;
-    c->q8_ok = false;
     return check_launch(c, "build kernels");
 }
 

@@ -700,99 +700,6 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes(Inner* __restrict__ rec, const
     qnode_from_records(rec, slot, __uint_as_float(inner[k].aux0), qn + slot);
 }
 
-// ---- 8-wide quantized nodes (RTBVH_WIDE8 builds; rtbvh_device.h QNode8) -------------------
-// quantize_axis over eight boxes: one grid (origin, power-of-two step) and two lo / hi words
-__device__ __forceinline__ bool quantize_axis8(const float (&lo)[8], const float (&hi)[8], float& org, float& scl,
-                                               uint32_t (&wlo)[2], uint32_t (&whi)[2]) {
-    float o = lo[0], m = hi[0];
-#pragma unroll
-    for (int c = 1; c < 8; c++) {
-        o = fminf(o, lo[c]);
-        m = fmaxf(m, hi[c]);
-    }
-    const float ext = m - o;
-    if (!(fabsf(o) <= 0x1p100f && fabsf(m) <= 0x1p100f && ext <= 0x1p100f)) return false;
-    int e = -120;
-    if (ext > 0.f) {
-        const int E = (int)((__float_as_uint(ext) >> 23) & 255u) - 127;
-        e = max(E - 8, -120);
-    }
-    while (fmaf(255.f, pow2f(e), o) < m) ++e;
-    const float s = pow2f(e), rs = pow2f(-e);
-    wlo[0] = wlo[1] = whi[0] = whi[1] = 0;
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-        uint32_t l = (uint32_t)fminf(fmaxf(floorf((lo[c] - o) * rs), 0.f), 255.f);
-        uint32_t h = (uint32_t)fminf(fmaxf(ceilf((hi[c] - o) * rs), 0.f), 255.f);
-        if (l > 0 && fmaf((float)l, s, o) > lo[c]) --l;
-        if (h < 255 && fmaf((float)h, s, o) < hi[c]) ++h;
-        wlo[c >> 2] |= l << (8 * (c & 3));
-        whi[c >> 2] |= h << (8 * (c & 3));
-    }
-    org = o;
-    scl = s;
-    return true;
-}
-// The 8-wide node of the node whose record is at `slot`: the greedy collapse of greedy_qnode_words
-// expanded six times (the largest-area internal entry among the first seven, replaced by its children),
-// from the records in global memory; E its edge bound (margin codes as qnode_words)
-__device__ void qnode8_from_records(const Inner* __restrict__ rec, uint32_t slot, float E, QNode8* dst) {
-    QEnt P[8];
-    record_kids(rec, slot, P[0], P[1]);
-    uint32_t n = 2;
-    for (int step = 0; step < 6; step++) {
-        int pick = -1;
-        float best = -1.f;
-        for (uint32_t k = 0; k < n && k < 7; k++)
-            if (!(P[k].id & LEAF_BIT)) {
-                const float ar = half_area(P[k].b);
-                if (ar > best) { best = ar; pick = (int)k; }
-            }
-        if (pick < 0) break;
-        QEnt c0, c1;
-        record_kids(rec, P[pick].slot, c0, c1);
-        P[pick] = c0;
-        P[n++] = c1;
-    }
-    float lx[8], ly[8], lz[8], hx[8], hy[8], hz[8];
-    uint32_t id[8];
-    for (uint32_t k = 0; k < 8; k++) {
-        const QEnt& e = P[k < n ? k : 0];
-        lx[k] = e.b[0]; ly[k] = e.b[1]; lz[k] = e.b[2];
-        hx[k] = e.b[3]; hy[k] = e.b[4]; hz[k] = e.b[5];
-        id[k] = k >= n ? INVALID : (e.id & LEAF_BIT) ? e.id : e.slot;
-    }
-    QNode8 q;
-    uint32_t wl[3][2], wh[3][2];
-    bool ok = quantize_axis8(lx, hx, q.a.org[0], q.a.scl[0], wl[0], wh[0]);
-    ok = quantize_axis8(ly, hy, q.a.org[1], q.a.scl[1], wl[1], wh[1]) && ok;
-    ok = quantize_axis8(lz, hz, q.a.org[2], q.a.scl[2], wl[2], wh[2]) && ok;
-    if (!ok) {
-        q.a.scl[0] = 0.f;   // the certified walk flags a ray that reaches this node
-    } else {
-        uint32_t ce, ct;
-        mt_node_codes(E, ce, ct);
-        q.a.scl[1] = __uint_as_float(__float_as_uint(q.a.scl[1]) | ce);
-        q.a.scl[2] = __uint_as_float(__float_as_uint(q.a.scl[2]) | ct);
-    }
-    for (int ax = 0; ax < 3; ax++) {
-        q.a.lo[ax] = wl[ax][0]; q.a.hi[ax] = wh[ax][0];
-        q.lo[ax] = wl[ax][1]; q.hi[ax] = wh[ax][1];
-    }
-    for (int k = 0; k < 4; k++) { q.a.id[k] = id[k]; q.id[k] = id[4 + k]; }
-    for (int k = 0; k < 6; k++) q.pad[k] = 0;
-    const float4* qs = reinterpret_cast<const float4*>(&q);
-    float4* d = reinterpret_cast<float4*>(dst);
-#pragma unroll
-    for (int k = 0; k < 8; k++) d[k] = qs[k];
-}
-__global__ __launch_bounds__(BLOCK) void k_qnodes8(BuildArgs a) {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k + 1 >= a.T) return;
-    const uint32_t slot = slot_of(a.pint[k], a.T);
-    qnode8_from_records(a.rec, slot, *node_edge(a, k), a.qnode8 + slot);
-}
-
 // The crossing nodes of refit workgroup b are xlist[b * RBLOCK, + xcnt[b]): one wave per
 // refit workgroup walks them (a few dozen typically; up to RBLOCK for a degenerate tree).
 constexpr uint32_t XWAVES = BLOCK / 64;
@@ -990,7 +897,6 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     QEnt e0, e1;
     lds_kids(i, e0, e1);
     E = __uint_as_float(s_cnt[tid] & 0x7FFFFFFFu);   // the node's edge bound (the climb's ticket)
-    if (RTBVH_WIDE8) *node_edge(a, i) = E;            // (k_qnodes8 reads it)
     greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, -1.f, qw, ent);
     }
     // Which of the block's QNodes the 4-wide walk reads: it steps from a QNode to its internal
@@ -1013,6 +919,18 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
             x = p;
         }
         s_read[tid] = mine && near ? 1u : 0u;
+    }
+    // A QNode without a grid is walked (uncertified walks, trace.hip qchildren) on its node's exact record
+    // pair: the walk steps to the node's binary grandchildren, not to its greedy entries -- so those are the
+    // entries whose QNodes it reads (a grandchild the collapse expanded past was left unwritten)
+    if (mine && qw[0].w == 0.f) {
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+            const uint32_t ch = side ? q.y : q.x;
+            const uint4 cq = (ch & LEAF_BIT) ? make_uint4(INVALID, INVALID, 0u, 0u) : s_topo[ch - base];
+            ent[2 * side] = cq.x;
+            ent[2 * side + 1] = cq.y;
+        }
     }
     bool pending = mine && RTBVH_QSKIP;   // its entries are not marked yet
     for (;;) {
@@ -1542,10 +1460,6 @@ void launch_build_small(const BuildArgs& a, hipStream_t s) {
     uint32_t* sv = const_cast<uint32_t*>(a.sorted_vals);
     if (a.delta_mode == 0) hipLaunchKernelGGL(k_build_small<0>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
     else hipLaunchKernelGGL(k_build_small<1>, dim3(1), dim3(SMALL_BLOCK), 0, s, a, sk, sv);
-}
-void launch_qnodes8(const BuildArgs& a, hipStream_t s) {
-    if (a.T < 2) return;
-    hipLaunchKernelGGL(k_qnodes8, dim3((a.T - 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, a);
 }
 void launch_qnodes(const BuildArgs& a, hipStream_t s) {
     if (a.T > 1)

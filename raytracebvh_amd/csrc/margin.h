@@ -35,11 +35,16 @@ struct MtMargin {
 };
 RTBVH_HD inline MtMargin mt_margin(float E, float L, float A) {
     MtMargin m;
-    const float K = 35.4f * MT_U * L * A * E * E;
+    const float K = 35.4f * MT_U * L * A * E * E;   // (underflow only drops terms the 1.01 covers)
     m.r1 = 1.01f * A * (K + 4.f * MT_U);
     m.r0 = 1.01f * E * (1.31f * K + 6.f * MT_U) + MT_FLOOR;
-    const float c = 28.3f * L * A * MT_U * E;   // (C): c (A t + 2 E) <= 0.2
-    m.tcap = c > 0.f ? (0.2f / c - 2.f * E) / A * 0.999f : INFINITY;
+    // (C): c (A t + 2 E) <= 0.2 with c = 28.3 L A u E; for a tiny E the product c is formed on E 2^64 and
+    // 0.2 / c scaled back (powers of two: exact), so neither c's gradual underflow nor 0.2 / c's overflow
+    // moves the range up (capped at 2^127: below the true range when that is past the float range)
+    const bool tiny = E < 0x1p-60f;
+    const float c = 28.3f * L * A * MT_U * (tiny ? E * 0x1p64f : E);
+    const float r = tiny ? fminf(0.2f / c * 0x1p64f, 0x1p127f) : 0.2f / c;
+    m.tcap = c > 0.f ? (r - 2.f * E) / A * 0.999f : INFINITY;
     if (!(E >= 0.f && E < INFINITY && m.r1 < 0.5f && m.r0 < INFINITY)) m.tcap = -1.f;   // (NaN: not covered)
     return m;
 }
@@ -67,12 +72,17 @@ RTBVH_HD inline float mt_rcp_down(float x) {
     return 1.f / x * (1.f - 0x1p-21f);
 #endif
 }
-// tcap of mt_margin(E, MT_LAMBDA, MT_A) from below, without a division (the build quantizes a node per thread)
+// tcap of mt_margin(E, MT_LAMBDA, MT_A) from below, without a division (the build quantizes a node per thread).
+// A tiny E is scaled as in mt_margin: c on E 2^64 (no gradual underflow of c, which would round it DOWN and
+// the range up), 0.2 / c scaled back and capped at 2^127 (no overflow to inf past the true range)
 RTBVH_HD inline float mt_tcap_down(float E) {
     if (!(E >= 0.f && E < INFINITY)) return -1.f;
-    const float c = 28.3f * MT_LAMBDA * MT_A * MT_U * E * (1.f + 0x1p-20f);   // >= mt_margin's c
+    const bool tiny = E < 0x1p-60f;
+    const float c = 28.3f * MT_LAMBDA * MT_A * MT_U * (tiny ? E * 0x1p64f : E) * (1.f + 0x1p-20f);   // >= mt_margin's c
     if (!(c > 0.f)) return INFINITY;
-    return (0.2f * mt_rcp_down(c) - 2.f * E * (1.f + 0x1p-20f)) * ((1.f - 0x1p-20f) / MT_A) * 0.999f;
+    const float q = 0.2f * mt_rcp_down(c);
+    const float r = tiny ? fminf(q * 0x1p64f, 0x1p127f) : q;
+    return (r - 2.f * E * (1.f + 0x1p-20f)) * ((1.f - 0x1p-20f) / MT_A) * 0.999f;
 }
 // a node's codes from the largest edge bound of its leaves (inf: a non-finite triangle below; tcap -1)
 RTBVH_HD inline void mt_node_codes(float E, uint32_t& ce, uint32_t& ct) {
@@ -106,11 +116,18 @@ RTBVH_HD inline MtNodeRho mt_node_prep(const MtNodeK& k, float E) {
 RTBVH_HD inline float mt_node_eval(const MtNodeRho& n, float t) { return fmaf(n.s, t, n.c); }
 RTBVH_HD inline float mt_node_rho(const MtNodeK& k, float E, float t) { return mt_node_eval(mt_node_prep(k, E), t); }
 
-// the global edge bound of a triangle: max(|e1|, |e2|) rounded up (inf for a non-finite triangle)
+// the global edge bound of a triangle: max(|e1|, |e2|) rounded up (inf for a non-finite triangle).  Below
+// 2^-50 a component's square can underflow (to a denormal that rounds by more than the 2^-20, or to 0): then
+// the bound is sqrt(3) max |component|, rounded up, plus the smallest denormal (E >= |e| must hold
+// for the tiniest triangles too)
 RTBVH_HD inline float mt_edge_bound(float e1x, float e1y, float e1z, float e2x, float e2y, float e2z) {
     const float a = e1x * e1x + e1y * e1y + e1z * e1z, b = e2x * e2x + e2y * e2y + e2z * e2z;
     const float m = sqrtf(fmaxf(a, b)) * (1.f + 0x1p-20f);
-    return m == m ? m : INFINITY;
+    if (m != m) return INFINITY;
+    const float mx = fmaxf(fmaxf(fmaxf(fabsf(e1x), fabsf(e1y)), fmaxf(fabsf(e1z), fabsf(e2x))),
+                           fmaxf(fabsf(e2y), fabsf(e2z)));
+    if (mx < 0x1p-50f) return mx * 1.7320510f * (1.f + 0x1p-20f) + 0x1p-149f;
+    return m;
 }
 
 // The depth key of a leaf for the orthographic primary rays (d = (0, 0, 1), so |d| = 1 and the

@@ -94,20 +94,6 @@ struct alignas(64) QNode {
     uint32_t id[4];
 };
 static_assert(sizeof(QNode) == 64, "QNode must be one 64-B record");
-// 128-byte quantized 8-wide node (RTBVH_WIDE8 builds): the greedy collapse expanded six times,
-// up to eight entries on one grid, in one 128-B line.  Words 0..15 are a QNode for entries 0..3 (the grid and
-// margin codes in words 0..5); words 16..18 / 19..21 the lo / hi bytes of entries 4..7, 22..25 their ids,
-// 26..31 zero.  An absent entry has id INVALID and repeats entry 0's box.
-struct alignas(128) QNode8 {
-    QNode a;
-    uint32_t lo[3], hi[3];
-    uint32_t id[4];
-    uint32_t pad[6];
-};
-static_assert(sizeof(QNode8) == 128, "QNode8 must be one 128-B line");
-#ifndef RTBVH_WIDE8
-#define RTBVH_WIDE8 0
-#endif
 __device__ __forceinline__ float qdecode(float org, float scl, uint32_t w, int c) {
     return fmaf((float)((w >> (8 * c)) & 255u), scl, org);   // == org + q*scl: the product is exact
 }

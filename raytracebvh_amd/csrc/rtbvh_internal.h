@@ -74,7 +74,6 @@ struct BuildArgs {
     uint4* lfp;               // [T] leaf footprints on the primary pixel grid (rtbvh_device.h leaf_footprint)
     float* zpart;             // [ZPART * refit_blocks(T)] k_refit workgroup b's leaf depth range, edge bound
     uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
-    QNode8* qnode8;           // [2T-1] RTBVH_WIDE8 builds: quantized 8-wide nodes in slots (rtbvh_device.h QNode8)
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
@@ -92,8 +91,6 @@ void launch_pseudo(const BuildArgs& a, hipStream_t s);
 uint32_t refit_blocks(uint32_t T);
 // qnode[k] of every internal node from the record pairs
 void launch_qnodes(const BuildArgs& a, hipStream_t s);
-// RTBVH_WIDE8 builds: qnode8[k] of every internal node from the records of a complete tree (node_edge set)
-void launch_qnodes8(const BuildArgs& a, hipStream_t s);
 // the whole build in one workgroup for T <= small_build_max() (sorted pairs into
 // a.sorted_keys / a.sorted_vals, which must be writable)
 uint32_t small_build_max();
@@ -144,30 +141,11 @@ struct TraceArgs {
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)
-    const QNode8* qnode8;     // [2T-1] RTBVH_WIDE8 builds: 8-wide nodes (the certified bounce walk)
     // N > 1, the binned pass's bins: the leaves whose footprint meets the rank's rows, in PB_LISTS lists (the
     // count pass appends them, the fill pass reads only them; null at N = 1, where every leaf is read):
     // counters PB_LIST_STRIDE words apart, then the lists, pb_list_cap(T) entries each (pb_bin.h)
     uint32_t* pb_list;
-    // the certified bounce walk's parked rays (RTBVH_PARK_STEPS, trace.hip k_bounce_tail): per buffer set,
-    // PARK_CAP records and PARK_CAP x STACK4B stack entries
-    struct Park* park_rec;
-    uint2* park_stack;
 };
-// a certified bounce ray parked after RTBVH_PARK_STEPS steps: its ray, stack depth, best hit so far;
-// its stack entries (node id, entry key bits) at park_stack[slot * STACK4B ...]
-struct Park {
-    uint32_t r, sp, btri, pad;
-    unsigned long long key;
-    unsigned long long pad2;
-};
-#ifndef RTBVH_PARK_STEPS
-#define RTBVH_PARK_STEPS 0   // off: A/B round 5, 64 / 128 / 256 all slower at N = 1
-#endif
-#ifndef RTBVH_PARK_CAP
-#define RTBVH_PARK_CAP 32768
-#endif
-constexpr uint32_t PARK_STEPS = RTBVH_PARK_STEPS, PARK_CAP = RTBVH_PARK_CAP;
 // primary-ray walks (trace.hip k_primary): per lane in reference order / nearest-first, wave
 // packets in reference order / nearest-first, 4-wide wave packets (axis-parallel box test)
 enum class PrimaryKind { LANE_REFERENCE, LANE_NEAREST, PACKET_REFERENCE, PACKET_NEAREST, PACKET_WIDE, BINNED };

@@ -905,9 +905,6 @@ constexpr uint32_t PB_RASTER_BLOCK = RTBVH_PB_RASTER_BLOCK;   // threads per til
 #ifndef RTBVH_PB_PROBE
 #define RTBVH_PB_PROBE 0
 #endif
-#ifndef RTBVH_PB_ROWMAJOR
-#define RTBVH_PB_ROWMAJOR 0   // the fine phase's lanes: 0 = 8x8 / 16x4 / 32x2 pixel blocks, 1 = row-major (A/B)
-#endif
 template <bool COUNT, bool CERT, uint32_t NT, class KeyAt>
 __device__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at, RayQ* __restrict__ q,
                               uint32_t* __restrict__ qcount, int emit, uint32_t* __restrict__ redo,
@@ -1044,23 +1041,12 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_bin
             const int sy0 = __builtin_amdgcn_readlane(ry0, k), sy1 = __builtin_amdgcn_readlane(ry1, k);
             const float sz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(zmin), k));
             const int lw = sx1 - sx0 + 1;
-#if RTBVH_PB_ROWMAJOR
-            // the rectangle's pixels row-major, 64 a pass: lane p of pass b is pixel b * 64 + p at
-            // (q % lw, q / lw); q / lw by a multiply-shift (q < 1024, lw <= 32: exact with the
-            // rounded-up 2^16 / lw).  A C5 leaf's ~9 x 5 pixels take one pass, not two of 16 x 4
-            const uint32_t npx = (uint32_t)(lw * (sy1 - sy0 + 1)), mg = (65536u + (uint32_t)lw - 1u) / (uint32_t)lw;
-            for (uint32_t q0 = 0; q0 < npx; q0 += 64) {
-                const uint32_t q = q0 + lane, qy = (q * mg) >> 16, qx = q - qy * (uint32_t)lw;
-                const bool ok = q < npx;
-                const uint32_t pi = (uint32_t)(((int)qy + sy0) * (int)PB_TILE + sx0 + (int)qx);
-#else
             const int cs = lw <= 8 ? 3 : lw <= 16 ? 4 : 5;   // lanes as 8x8, 16x4 or 32x2 pixels
             const int col = (int)(lane & ((1u << cs) - 1)), px = sx0 + col;
             for (int y0 = sy0; y0 <= sy1; y0 += 64 >> cs) {
                 const int y = y0 + (int)(lane >> cs);
                 const bool ok = col < lw && y <= sy1;
                 const uint32_t pi = (uint32_t)(y * (int)PB_TILE + px);
-#endif
                 const bool need = ok && (sg || sz <= __uint_as_float(s_t[2 * pb_slot(pi) + 1]));
                 const uint64_t nm = __ballot(need);
                 if (qn + (uint32_t)__popcll(nm) > PB_QCAP) flush();
@@ -1473,11 +1459,6 @@ __device__ __forceinline__ bool qbox_fast_cert(const QAxis& x, const QAxis& y, c
     key = fminf(fmaxf(fmaxf(fmaf(-rb, ainv.x, nx), fmaf(-rb, ainv.y, ny)), fmaf(-rb, ainv.z, nz)), tcn);
     return 0 <= mx && mn <= mx && key <= best;
 }
-// CERT on the exact decode for the rays the slack test cannot take (1), or those rays flagged for the
-// reference-order re-trace (0, A/B)
-#ifndef RTBVH_CERT_EXACT
-#define RTBVH_CERT_EXACT 0   // 1 measured: +0.3 ms (the walk spills a VGPR), for ~5 re-traced rays per C5 frame
-#endif
 // GUARD false: no walk-length guard (a clz64 tree has no cycles; the census of COUNT keeps it).
 // CERT (MODE 2 only): the certified walk.  Every box test's entry distance is taken on the
 // box grown by its node's margin rho_n(best) (margin.h: no hit the triangle test accepts at t <= best lies
@@ -1496,14 +1477,8 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          unsigned long long* __restrict__ overflow, int stack_limit,
-                                                          Park* __restrict__ park_rec, uint2* __restrict__ park_stack) {
+                                                          unsigned long long* __restrict__ overflow, int stack_limit) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
-    // PARK: a certified ray still walking after PARK_STEPS steps is parked (its stack to park_stack, the
-    // slot from the counter next[1]) for k_bounce_tail, which walks it one ray per wave
-    constexpr bool PARK = CERT && !COUNT && PARK_STEPS > 0 && !RTBVH_WIDE8;
-    uint32_t stp = 0;
-    constexpr bool W8 = CERT && RTBVH_WIDE8;   // the certified walk on the 8-wide nodes (qn: QNode8s)
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
     const uint32_t n = *qin_count;
@@ -1562,9 +1537,9 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
             const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
             a3 = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), 0u, 0u);
             b3 = make_uint4(__float_as_uint(q3.z), __float_as_uint(q3.w), 0u, 0u);
-            // (CERT without the exact-decode variant: a ray the slack test cannot take never steps -- it is
-            // flagged at its first step -- so every stepping ray takes this branch)
-            if (qfast || (CERT && !RTBVH_CERT_EXACT)) {
+            // (CERT: a ray the slack test cannot take never steps -- it is flagged at its first step -- so
+            // every stepping ray takes this branch)
+            if (qfast || CERT) {
                 // CERT: the node's margin rho_n(best) (0 before the first bound) and its range
                 float rr = 0.f, tcn = 0.f;
                 MtNodeRho nr{0.f, 0.f};
@@ -1588,7 +1563,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                     h2 = qbox_fast(X, Y, Z, 2, true, kbb, t2);
                     h3 = qbox_fast(X, Y, Z, 3, true, kbb, t3);
                 }
-            } else if (!CERT || !RTBVH_CERT_EXACT) {
+            } else {
     #define RTBVH_QBOX(c, t)                                                                                      \
 ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, lz, c), qdecode(ox, sx, hx, c), \
         qdecode(oy, sy, hy, c), qdecode(oz, sz, hz, c), true, kbb, t)
@@ -1597,33 +1572,6 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                 h2 = RTBVH_QBOX(2, t2);
                 h3 = RTBVH_QBOX(3, t3);
     #undef RTBVH_QBOX
-            } else {
-                // CERT, a ray the slack test cannot take (|1/d| > 2^20 or |o| > 2^90: rare): the exact decode,
-                // each decoded box grown by the node's margin rho_n(best) with outward rounding (one ulp past
-                // the rounded sum), the reference slab test on it; keys capped at the node's range, and -inf
-                // before the first bound (such an entry is never dropped on a pop)
-                const MtNodeRho nr = mt_node_prep(nk, mt_code_val(wy));
-                const float tcn = mt_code_val(wz);
-                const bool bnd = kbb < __builtin_inff();
-                const float rr = bnd ? mt_node_eval(nr, kbb) : 0.f;
-                const auto lo = [&](float D) { return rr > 0.f ? nextafterf(D - rr, -INFINITY) : D; };
-                const auto hi = [&](float D) { return rr > 0.f ? nextafterf(D + rr, INFINITY) : D; };
-    #define RTBVH_QBOXC(c, t)                                                                                     \
-ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdecode(oz, sz, lz, c)),            \
-        hi(qdecode(ox, sx, hx, c)), hi(qdecode(oy, sy, hy, c)), hi(qdecode(oz, sz, hz, c)), false, 0.f, t)
-                h0 = RTBVH_QBOXC(0, t0);
-                h1 = RTBVH_QBOXC(1, t1);
-                h2 = RTBVH_QBOXC(2, t2);
-                h3 = RTBVH_QBOXC(3, t3);
-    #undef RTBVH_QBOXC
-                t0 = bnd ? fminf(t0, tcn) : -INFINITY;
-                t1 = bnd ? fminf(t1, tcn) : -INFINITY;
-                t2 = bnd ? fminf(t2, tcn) : -INFINITY;
-                t3 = bnd ? fminf(t3, tcn) : -INFINITY;
-                h0 = h0 && t0 <= kbb;
-                h1 = h1 && t1 <= kbb;
-                h2 = h2 && t2 <= kbb;
-                h3 = h3 && t3 <= kbb;
             }
             h1 = h1 & (a3.y != INVALID);
             h3 = h3 & (b3.y != INVALID);
@@ -1693,9 +1641,8 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
                     top = INVALID;
                     node = root_slot(T);
                     guard = 2 * T + 2;
-                    stp = 0;
                     if (CERT) {   // a ray the margin does not cover ends at its first step, flagged
-                        flg = !((qfast || RTBVH_CERT_EXACT) && dot(d, d) <= MT_DD);   // (exact decode: slack-free rays)
+                        flg = !(qfast && dot(d, d) <= MT_DD);
                         if (flg) node = INVALID;
                     }
                 }
@@ -1712,24 +1659,7 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
             mixed += (lf != 0 && lf != act);
         }
         if (!has) continue;
-        bool done = false, parked = false;
-        if (PARK && ++stp == PARK_STEPS) {
-            // park: the stack and the node this step would visit (key 0: visited) go to the tail kernel
-            uint32_t slot = 0;
-            slot = atomicAdd(next + 1, 1u);
-            if (slot < PARK_CAP) {
-                uint2* st = park_stack + (size_t)slot * STACK4B;
-                for (int k = 0; k < sp; k++)
-                    st[k] = k < SW ? make_uint2(s_wid[k][tid], __float_as_uint(bf16_up(s_wt[k][tid]))) : wstack[k - SW];
-                st[sp] = make_uint2(node, 0u);
-                Park pr;
-                pr.r = r; pr.sp = (uint32_t)sp + 1; pr.btri = btri; pr.pad = 0; pr.key = key; pr.pad2 = 0;
-                park_rec[slot] = pr;
-                parked = true;
-                has = false;
-            }
-        }
-        if (parked) continue;
+        bool done = false;
         if (WIDE) {
             // A step: the QNode of an internal `node`, then one leaf test -- the nearest child when it
             // is a leaf (the next child is visited), or the leaf the step began at -- so a leaf found
@@ -1743,63 +1673,6 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
                 if (node & LEAF_BIT) {
                     L = node;
                     node = INVALID;
-                } else if (W8) {
-                    // RTBVH_WIDE8: the 8-wide node (rtbvh_device.h QNode8, one 128-B line): eight certified box
-                    // tests on one grid; the nearest hit entry next (a leaf: tested in this step), the other hit
-                    // entries pushed in slot order (no sort: DESIGN.md 6, the CPU study's +4% steps)
-                    const v4f* rr = reinterpret_cast<const v4f*>(qn) + 8 * (size_t)node;
-                    v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3], q4 = rr[4], q5 = rr[5], q6 = rr[6];
-                    pin(q0); pin(q1); pin(q2); pin(q3); pin(q4); pin(q5); pin(q6);
-                    if (COUNT) c.internal++;
-                    if (q0.w == 0.f || sp + 7 > limit) {   // no grid, or no room for seven pushes: flagged
-                        if (q0.w != 0.f) c.overflow++;
-                        flg = true;
-                        done = true;
-                        node = INVALID;
-                    } else {
-                        const float kbb = key_t(key);
-                        const uint32_t wy = __float_as_uint(q1.x), wz = __float_as_uint(q1.y);
-                        const float sy = __uint_as_float(wy & 0xFF800000u), sz = __uint_as_float(wz & 0xFF800000u);
-                        const MtNodeRho nr = mt_node_prep(nk, mt_code_val(wy));
-                        const float tcn = mt_code_val(wz);
-                        const float rr0 = kbb < __builtin_inff() ? mt_node_eval(nr, kbb) : 0.f;
-                        QAxis X = qaxis<true>(q0.x, q0.w, __float_as_uint(q1.z), __float_as_uint(q2.y), o.x, inv.x, rr0),
-                              Y = qaxis<true>(q0.y, sy, __float_as_uint(q1.w), __float_as_uint(q2.z), o.y, inv.y, rr0),
-                              Z = qaxis<true>(q0.z, sz, __float_as_uint(q2.x), __float_as_uint(q2.w), o.z, inv.z, rr0);
-                        const f3 ai = mk(fabsf(inv.x), fabsf(inv.y), fabsf(inv.z));
-                        float t[8];
-                        bool h[8];
-#pragma unroll
-                        for (int k = 0; k < 4; k++) h[k] = qbox_fast_cert(X, Y, Z, k, kbb, nk, nr, ai, tcn, t[k]);
-                        // entries 4..7: the same grid, their lo / hi words (near / far by the ray's signs)
-                        X.nw = inv.x < 0.f ? __float_as_uint(q4.w) : __float_as_uint(q4.x);
-                        X.fw = inv.x < 0.f ? __float_as_uint(q4.x) : __float_as_uint(q4.w);
-                        Y.nw = inv.y < 0.f ? __float_as_uint(q5.x) : __float_as_uint(q4.y);
-                        Y.fw = inv.y < 0.f ? __float_as_uint(q4.y) : __float_as_uint(q5.x);
-                        Z.nw = inv.z < 0.f ? __float_as_uint(q5.y) : __float_as_uint(q4.z);
-                        Z.fw = inv.z < 0.f ? __float_as_uint(q4.z) : __float_as_uint(q5.y);
-#pragma unroll
-                        for (int k = 0; k < 4; k++) h[4 + k] = qbox_fast_cert(X, Y, Z, k, kbb, nk, nr, ai, tcn, t[4 + k]);
-                        const uint32_t id[8] = {__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
-                                                __float_as_uint(q3.w), __float_as_uint(q5.z), __float_as_uint(q5.w),
-                                                __float_as_uint(q6.x), __float_as_uint(q6.y)};
-                        float km = __builtin_inff();
-                        uint32_t im = INVALID, cm = 8;
-#pragma unroll
-                        for (int k = 0; k < 8; k++) {
-                            h[k] = h[k] && id[k] != INVALID;
-                            const bool b = h[k] && (t[k] < km || im == INVALID);
-                            km = b ? t[k] : km;
-                            im = b ? id[k] : im;
-                            cm = b ? (uint32_t)k : cm;
-                        }
-#pragma unroll
-                        for (int k = 7; k >= 0; k--)
-                            if (h[k] && (uint32_t)k != cm) wpush(id[k], t[k]);
-                        const bool lf = im != INVALID && (im & LEAF_BIT);
-                        L = lf ? im : INVALID;
-                        node = lf ? INVALID : im;
-                    }
                 } else {
                     const v4f* rr = reinterpret_cast<const v4f*>(qn + node);
                     v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
@@ -1953,134 +1826,6 @@ ray_box(o, inv, lo(qdecode(ox, sx, lx, c)), lo(qdecode(oy, sy, ly, c)), lo(qdeco
                 atomicAdd(&counters[8], v[2]);
                 atomicAdd(overflow, v[2]);
             }
-        }
-    }
-}
-
-// The parked rays of a certified bounce pass (k_bounce_trav PARK: still walking after PARK_STEPS steps), one
-// ray per wave: each round the wave pops up to 64 entries off the ray's stack (LDS), every lane one -- an
-// entry past the bound is dropped, a leaf is tested, an internal node's QNode gets the walk's four certified
-// box tests and its hit entries are pushed (a wave prefix sum places them) -- and the leaves' (t, leaf) keys
-// fold into the ray's minimum.  The walk visits every entry the lane walk would (an entry is dropped only by
-// the bound, as there) and perhaps more, so its (t, leaf) minimum is the same; the certificate is checked by
-// k_bounce_shade as for every ray.  A stack past TSTK entries or a node without a grid flags the ray
-// (HIT_FLAG: re-traced in the reference order by k_bounce_redo).  A long walk's dependent steps become
-// rounds of up to 64 independent fetches.
-constexpr uint32_t TSTK = 1024;   // LDS stack entries per wave (8 KB)
-__global__ __launch_bounds__(BLOCK) void k_bounce_tail(const QNode* __restrict__ qn, const float4* __restrict__ leaf,
-                                                       const RayQ* __restrict__ qin, const uint32_t* __restrict__ next,
-                                                       const Park* __restrict__ park_rec,
-                                                       const uint2* __restrict__ park_stack,
-                                                       float2* __restrict__ hitrec) {
-    __shared__ uint32_t s_id[BLOCK / 64][TSTK];
-    __shared__ float s_key[BLOCK / 64][TSTK];
-    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    uint32_t* sid = s_id[w];
-    float* skey = s_key[w];
-    const uint32_t n = min(next[1], PARK_CAP);
-    const MtNodeK nk = mt_node_consts();
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t p = blockIdx.x * (BLOCK / 64) + w; p < n; p += gridDim.x * (BLOCK / 64)) {
-        const Park pr = park_rec[p];
-        const uint32_t r = pr.r;
-        uint32_t sp = min(pr.sp, (uint32_t)STACK4B);
-        uint64_t key = pr.key;
-        uint32_t btri = pr.btri;
-        const float4 q0r = reinterpret_cast<const float4*>(qin + r)[0];
-        const float4 q1r = reinterpret_cast<const float4*>(qin + r)[1];
-        const f3 o = mk(q0r.z, q0r.w, q1r.x), d = mk(q1r.y, q1r.z, q1r.w);
-        const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
-        const f3 ai = mk(fabsf(inv.x), fabsf(inv.y), fabsf(inv.z));
-        for (uint32_t k = lane; k < sp; k += 64) {
-            const uint2 e = park_stack[(size_t)p * STACK4B + k];
-            sid[k] = e.x;
-            skey[k] = __uint_as_float(e.y);
-        }
-        bool flg = false;
-        while (sp > 0 && !flg) {
-            const uint32_t m = min(sp, 64u);
-            sp -= m;
-            const float kbb = key_t(key);
-            const bool act = lane < m;
-            const uint32_t id = act ? sid[sp + lane] : INVALID;
-            const float ke = act ? skey[sp + lane] : INFINITY;
-            const bool live = act && ke <= kbb;
-            // a leaf: its (t, leaf) key
-            uint64_t ck = ~0ull;
-            uint32_t ctri = INVALID;
-            if (live && (id & LEAF_BIT)) {
-                const uint32_t j = id & ~LEAF_BIT;
-                const v4f* lr = reinterpret_cast<const v4f*>(leaf + 4 * (size_t)j);
-                const v4f la = lr[0], lb = lr[1], lc = lr[2];
-                const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
-                                                   mk(lb.z, lb.w, lc.x), true);
-                if (tw != -1.f) {
-                    ck = (uint64_t)__float_as_uint(tw) << 32 | j;
-                    ctri = __float_as_uint(lc.y) & ~LEAF_BIT;
-                }
-            }
-            // an internal node: its four certified box tests (k_bounce_trav's qchildren, CERT)
-            bool h0 = false, h1 = false, h2 = false, h3 = false, nogrid = false;
-            float k0 = 0.f, k1 = 0.f, k2 = 0.f, k3 = 0.f;
-            uint32_t i0 = INVALID, i1 = INVALID, i2 = INVALID, i3 = INVALID;
-            if (live && !(id & LEAF_BIT)) {
-                const v4f* rr = reinterpret_cast<const v4f*>(qn + id);
-                const v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
-                if (q0.w == 0.f) {
-                    nogrid = true;
-                } else {
-                    const uint32_t wy = __float_as_uint(q1.x), wz = __float_as_uint(q1.y);
-                    const float sy = __uint_as_float(wy & 0xFF800000u), sz = __uint_as_float(wz & 0xFF800000u);
-                    const MtNodeRho nr = mt_node_prep(nk, mt_code_val(wy));
-                    const float tcn = mt_code_val(wz);
-                    const float rr0 = kbb < __builtin_inff() ? mt_node_eval(nr, kbb) : 0.f;
-                    const QAxis X = qaxis<true>(q0.x, q0.w, __float_as_uint(q1.z), __float_as_uint(q2.y), o.x, inv.x, rr0),
-                                Y = qaxis<true>(q0.y, sy, __float_as_uint(q1.w), __float_as_uint(q2.z), o.y, inv.y, rr0),
-                                Z = qaxis<true>(q0.z, sz, __float_as_uint(q2.x), __float_as_uint(q2.w), o.z, inv.z, rr0);
-                    h0 = qbox_fast_cert(X, Y, Z, 0, kbb, nk, nr, ai, tcn, k0);
-                    h1 = qbox_fast_cert(X, Y, Z, 1, kbb, nk, nr, ai, tcn, k1);
-                    h2 = qbox_fast_cert(X, Y, Z, 2, kbb, nk, nr, ai, tcn, k2);
-                    h3 = qbox_fast_cert(X, Y, Z, 3, kbb, nk, nr, ai, tcn, k3);
-                    i0 = __float_as_uint(q3.x); i1 = __float_as_uint(q3.y);
-                    i2 = __float_as_uint(q3.z); i3 = __float_as_uint(q3.w);
-                    h1 = h1 && i1 != INVALID;
-                    h3 = h3 && i3 != INVALID;
-                }
-            }
-            if (__ballot(nogrid)) {   // (the lane walk flags these rays too)
-                flg = true;
-                break;
-            }
-            // the wave's smallest (t, leaf) key, and its triangle
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const uint64_t ok = (uint64_t)__shfl_xor((long long)ck, off, 64);
-                const uint32_t ot = (uint32_t)__shfl_xor((int)ctri, off, 64);
-                if (ok < ck) { ck = ok; ctri = ot; }
-            }
-            if (ck < key) { key = ck; btri = ctri; }
-            // the hit entries onto the stack: per child position c, the lanes with a hit in a block
-            const uint32_t nh = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
-            uint32_t tot = 0;
-            const uint64_t b0 = __ballot(h0), b1 = __ballot(h1), b2 = __ballot(h2), b3 = __ballot(h3);
-            const uint32_t c0 = (uint32_t)__popcll(b0), c1 = (uint32_t)__popcll(b1), c2 = (uint32_t)__popcll(b2),
-                           c3 = (uint32_t)__popcll(b3);
-            tot = c0 + c1 + c2 + c3;
-            (void)nh;
-            if (sp + tot > TSTK) {
-                flg = true;
-                break;
-            }
-            if (h0) { const uint32_t a = sp + (uint32_t)__popcll(b0 & lt); sid[a] = i0; skey[a] = k0; }
-            if (h1) { const uint32_t a = sp + c0 + (uint32_t)__popcll(b1 & lt); sid[a] = i1; skey[a] = k1; }
-            if (h2) { const uint32_t a = sp + c0 + c1 + (uint32_t)__popcll(b2 & lt); sid[a] = i2; skey[a] = k2; }
-            if (h3) { const uint32_t a = sp + c0 + c1 + c2 + (uint32_t)__popcll(b3 & lt); sid[a] = i3; skey[a] = k3; }
-            sp += tot;
-        }
-        if (lane == 0) {
-            uint32_t wd = key != NO_HIT ? btri : INVALID;
-            if (flg) wd ^= HIT_FLAG;
-            hitrec[r] = make_float2(key_t(key), __uint_as_float(wd));
         }
     }
 }
@@ -2311,17 +2056,13 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
                           float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, hipStream_t s) {
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
 #define RTBVH_BT(L, G, C)                                                                                              \
-    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner,                 \
-                       (C) && RTBVH_WIDE8 ? reinterpret_cast<const QNode*>(a.qnode8) : a.qnode, a.leaf,               \
-                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, a.park_rec, a.park_stack)
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
     if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
         if (guard) RTBVH_BT(false, true, MODE == 2);
         else RTBVH_BT(false, false, MODE == 2);
-        if (!COUNT && PARK_STEPS > 0 && !RTBVH_WIDE8)   // the parked rays (k_bounce_trav PARK)
-            hipLaunchKernelGGL(k_bounce_tail, dim3(512), dim3(BLOCK), 0, s, a.qnode, a.leaf, qin, next, a.park_rec,
-                               a.park_stack, hitrec);
     } else if (a.limited) { if (guard) RTBVH_BT(true, true, false); else RTBVH_BT(true, false, false); }
     else { if (guard) RTBVH_BT(false, true, false); else RTBVH_BT(false, false, false); }
 #undef RTBVH_BT

@@ -533,7 +533,33 @@ def test_wide_view_records_match_binary_tree():
             assert rec[15] == gen
 
 
-@pytest.mark.parametrize("scene", ["synthetic", "general boxes", "Test"])
+def _tiny_scene(seed=5):
+    """Triangles at every scale down to the denormals (for the identity camera: clip space = object space):
+    groups of a synthetic scene scaled by 2^0, 2^-40, 2^-70, 2^-100, 2^-118, 2^-126, 2^-135 -- edge bounds whose
+    squares underflow and whose margin constant c is denormal (margin.h mt_edge_bound / mt_tcap_down)."""
+    base = rt.synthetic(7000, seed=seed, half_extent=(1.0, 1.0, 1.0))
+    v = base.vertices.copy()
+    T = base.num_tris
+    scales = np.float32(2.0) ** np.array([0, -40, -70, -100, -118, -126, -135], np.float32)
+    tri_scale = scales[np.arange(T) % len(scales)]
+    idx = base.indices.reshape(-1, 3)
+    for k in range(3):   # (each vertex belongs to one triangle in the synthetic scenes)
+        v[idx[:, k], :3] = v[idx[:, k], :3] * tri_scale[:, None]
+    return rt.Scene(v, base.indices, base.mat_indices, base.materials)
+
+
+def _edge_bound_np(e1, e2):
+    """margin.h mt_edge_bound in numpy float32 (the device's operation order)."""
+    sq = lambda e: (e[:, 0] * e[:, 0] + e[:, 1] * e[:, 1]) + e[:, 2] * e[:, 2]
+    with np.errstate(invalid="ignore", under="ignore"):
+        m = np.sqrt(np.maximum(sq(e1), sq(e2))) * np.float32(1 + 2.0 ** -20)
+        mx = np.max(np.abs(np.concatenate([e1, e2], 1)), axis=1)
+        tiny = (mx * np.float32(1.7320510)) * np.float32(1 + 2.0 ** -20) + np.float32(2.0 ** -149)
+    out = np.where(mx < np.float32(2.0 ** -50), tiny, m)
+    return np.where(np.isnan(m), np.float32(np.inf), out).astype(np.float32)
+
+
+@pytest.mark.parametrize("scene", ["synthetic", "general boxes", "Test", "tiny triangles"])
 def test_qnodes_contain_the_exact_boxes(scene):
     """Quantized node of internal node k (rtbvh_device.h QNode) at k's slot: power-of-two grid
     steps, the entries of the largest-area greedy collapse (build.hip greedy_qnode: from k's
@@ -549,12 +575,16 @@ def test_qnodes_contain_the_exact_boxes(scene):
         s = rt.synthetic(20_000, seed=7, half_extent=(30, 30, 20))
     elif scene == "general boxes":
         s = _general_box_scene()
+    elif scene == "tiny triangles":
+        s = _tiny_scene()
     else:
         d = load_scene_fixture("Test")
         s = rt.Scene(d["vertices"], d["indices"], d["mat_indices"], d["material_blob"])
+    cam = (np.eye(4, dtype=np.float32), np.eye(4, dtype=np.float32)) if scene == "tiny triangles" \
+        else rt.camera_reference(320, 240)
     with rt.Context(device=0) as c:
         c.set_scene(s)
-        c.set_camera(*rt.camera_reference(320, 240))
+        c.set_camera(*cam)
         c.build()
         nodes = c.read_bvh()
         q = c.read_qnodes()
@@ -629,15 +659,17 @@ def test_qnodes_contain_the_exact_boxes(scene):
     assert ((reach < top) | (half < np.float32(2.0 ** -120)))[read].all(), "grid step not minimal"
     # the margin codes: E_k = max over node k's leaves of margin.h mt_edge_bound on the clip-space
     # triangle (rtbvh_device.h xform_point's operation order, no FMA: numpy float32), rounded up
-    wvp = rt.camera_reference(320, 240)[0].reshape(4, 4)
+    wvp = cam[0].reshape(4, 4)
     P = s.vertices[:, :3].astype(np.float32)
-    clip = ((P[:, 0:1] * wvp[0] + P[:, 1:2] * wvp[1]) + P[:, 2:3] * wvp[2]) + wvp[3]
+    with np.errstate(under="ignore"):
+        clip = ((P[:, 0:1] * wvp[0] + P[:, 1:2] * wvp[1]) + P[:, 2:3] * wvp[2]) + wvp[3]
     tri = clip[s.indices.reshape(-1, 3), :3]
     e1, e2 = tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]
-    sq = lambda e: (e[:, 0] * e[:, 0] + e[:, 1] * e[:, 1]) + e[:, 2] * e[:, 2]
-    with np.errstate(invalid="ignore"):
-        eb = np.sqrt(np.maximum(sq(e1), sq(e2))) * np.float32(1 + 2.0 ** -20)
-    eb = np.where(np.isnan(eb), np.float32(np.inf), eb).astype(np.float32)
+    eb = _edge_bound_np(e1, e2)
+    if scene == "tiny triangles":   # the bound is >= the exact 2-norm at every scale
+        n64 = lambda e: np.sqrt((e.astype(np.float64) ** 2).sum(1))
+        assert (eb.astype(np.float64) >= np.maximum(n64(e1), n64(e2))).all()
+        assert (eb < 2.0 ** -100).sum() > 500
     leaf_e = eb[nodes["index"][:T] // 3]
     node_e = np.zeros(T - 1, np.float32)
     order = []   # internal nodes, children before parents
@@ -655,12 +687,15 @@ def test_qnodes_contain_the_exact_boxes(scene):
     np.testing.assert_array_equal(codes_e[read], want_e[read])
     eq = (codes_e[read] << 16).view(np.float32).astype(np.float64)
     tcn = (codes_t[read] << 16).view(np.float32).astype(np.float64)
-    c = 28.3 * 100.01 * (1 + 2.0 ** -18) * 2.0 ** -24 * eq   # margin.h mt_margin's condition (C)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        tcap = np.where(np.isfinite(eq), (0.2 / c - 2 * eq) / (1 + 2.0 ** -18) * 0.999, -1.0)
-    assert ((tcn <= tcap * (1 + 1e-5)) | ((tcn == -1) & (tcap < 0))).all()
-    big = tcap >= 1   # (the 16-bit code truncates: within 2^-8)
-    assert (tcn[big] >= 0.99 * tcap[big]).all()
+    # the device's range (margin.h mt_tcap_down: the hardware reciprocal) against condition (C) in exact
+    # arithmetic (float64; no allowance on the unsafe side): c (A t + 2 E) <= 0.2 for every t <= tcn; a
+    # negative range covers no t
+    c = 28.3 * 100.01 * (1 + 2.0 ** -18) * 2.0 ** -24 * eq
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        tcap = np.where(np.isfinite(eq), (0.2 / c - 2 * eq) / (1 + 2.0 ** -18), -1.0)
+    assert np.where(tcap >= 0, tcn <= tcap, tcn < 0).all()
+    big = (tcap >= 1) & (tcap < 2.0 ** 127)   # (the 16-bit code truncates: within 2^-8; 0.999 of mt_margin)
+    assert (tcn[big] >= 0.99 * 0.999 * tcap[big]).all()
 
 
 def _general_box(lo, hi):
@@ -1494,6 +1529,59 @@ def test_nodes_without_a_grid_trace_their_exact_records(mode):
     ofb, _, ost = orc.trace(_oscene(s), nodes, wvp, wv, W, H, 2)
     np.testing.assert_array_equal(fb, ofb)
     assert st["bounce_rays"] == ost["bounce"] > 0 and sum(st["hits"]) == ost["hits"]
+
+
+def _huge_scene(seed=9, T=8000):
+    """A synthetic scene of T triangles, 400 of them huge (spanning about +-1e31 in x, centred among the
+    others): the nodes above them sit deep in the tree and have corners past 2^100, so their QNodes carry no
+    grid and the uncertified 4-wide bounce walk steps through their exact records to their grandchildren."""
+    base = rt.synthetic(T, seed=seed, half_extent=(30, 30, 20))
+    v = base.vertices.copy()
+    rng = np.random.default_rng(seed)
+    idx = base.indices.reshape(-1, 3)
+    for t in rng.choice(T, 400, replace=False):
+        y, z = rng.uniform(-25, 25), rng.uniform(-15, 15)
+        v[idx[t, 0], :3] = (-1e31 * rng.uniform(0.5, 2), y, z)
+        v[idx[t, 1], :3] = (1e31 * rng.uniform(0.5, 2), y + rng.uniform(0.1, 2), z)
+        v[idx[t, 2], :3] = (rng.uniform(-5, 5), y, z + rng.uniform(0.1, 2))
+    return rt.Scene(v, base.indices, base.mat_indices, base.materials)
+
+
+@pytest.mark.parametrize("mode", ["nearest+packet+wide", "binned+wide+refill"])
+def test_deep_nodes_without_a_grid_after_another_build(mode):
+    """k_refit writes only the QNodes a 4-wide walk reads; under a QNode without a grid the walk
+    reads its node's binary grandchildren's QNodes (not the greedy entries), so those must be written too --
+    else the walk reads what an earlier build of the same context left there.  The context first builds and
+    traces another scene of the same size, then the scene with deep grid-less nodes: its frame (two bounces)
+    is the oracle's."""
+    s0 = rt.synthetic(8000, seed=17, half_extent=(30, 30, 20))
+    s = _huge_scene()
+    W, H = 320, 240
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=TRACE_MODES[mode] | rt.FLAG_MULTI_KERNEL_BUILD) as c:
+        c.set_scene(s0)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 2)
+        c.set_scene(s)
+        c.compute_bvh(W, H, 2)
+        fb = c.read_framebuffer()
+        nodes, q = c.read_bvh(), c.read_qnodes()
+    T = s.num_tris
+    par, cl = nodes["parent"], nodes["child_l"]
+    depth = np.zeros(2 * T - 1, np.int32)
+    for x in range(T + 1, 2 * T - 1):   # each internal node's depth below the root
+        d, y = 0, x
+        while y != T:
+            y, d = par[y], d + 1
+        depth[x] = d
+    slots = {}
+    for x in range(T + 1, 2 * T - 1):
+        p = par[x] - T
+        slots[x] = 2 * p + (0 if cl[par[x]] == x else 1)
+    nogrid_deep = [x for x in slots if depth[x] >= 6 and q[slots[x], 3].view(np.float32) == 0]
+    assert len(nogrid_deep) >= 20   # grid-less nodes well below the top
+    ofb, _, _ = orc.trace(_oscene(s), nodes, wvp, wv, W, H, 2)
+    np.testing.assert_array_equal(fb, ofb)
 
 
 def test_packet_walk_after_a_build_without_pseudo_records():

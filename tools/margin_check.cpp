@@ -373,6 +373,41 @@ int main(int argc, char** argv) {
         ++s.node_checked;
         if (m.tcap >= 0.f ? !(tc <= m.tcap) : !(tc < 0.f)) ++s.node_viol;
     }
+    // ... and both ranges against condition (C) in exact arithmetic (long double), over every edge bound from
+    // the smallest denormal to 2^6 (2^-8 steps of the exponent): the tiny ones, whose c underflows and whose
+    // 0.2 / c overflows in float, included; with the code the walk decodes (mt_node_codes) as well
+    for (int k = -149 * 256; k <= 6 * 256; k++) {
+        const float E = (float)std::exp2((double)k / 256.0);
+        if (!(E > 0.f)) continue;
+        const long double c = 28.3L * 100.01L * (1.0L + 0x1p-18L) * 0x1p-24L * (long double)E;
+        const long double real = (0.2L / c - 2.0L * E) / (1.0L + 0x1p-18L);
+        const MtMargin m = mt_margin(E, MT_LAMBDA, MT_A);
+        const float tc = mt_tcap_down(E);
+        uint32_t ce, ct;
+        mt_node_codes(E, ce, ct);
+        const float Ec = mt_code_val(ce), tn = mt_code_val(ct);
+        const long double cc = 28.3L * 100.01L * (1.0L + 0x1p-18L) * 0x1p-24L * (long double)Ec;
+        const long double realc = (0.2L / cc - 2.0L * Ec) / (1.0L + 0x1p-18L);
+        s.node_checked += 3;
+        // (a negative range covers no t: any negative value says the same)
+        const auto ok = [](float v, long double r) { return r >= 0 ? (long double)v <= r : v < 0.f; };
+        if (!ok(tc, real)) ++s.node_viol;
+        if (!ok(m.tcap, real)) ++s.node_viol;
+        if (!(Ec >= E && ok(tn, realc))) ++s.node_viol;
+    }
+    // the edge bound against the exact 2-norm of random edges at every scale down to the denormals
+    for (int k = 0; k < 200000; k++) {
+        const int ex = -149 + (int)(rng.next() % 200);
+        float e[6];
+        long double n1 = 0, n2 = 0;
+        for (int q = 0; q < 6; q++) {
+            e[q] = (float)(std::ldexp(rng.u01() - 0.5, ex + 1));
+            (q < 3 ? n1 : n2) += (long double)e[q] * e[q];
+        }
+        const float E = mt_edge_bound(e[0], e[1], e[2], e[3], e[4], e[5]);
+        ++s.node_checked;
+        if (!((long double)E >= std::sqrt(std::max(n1, n2)))) ++s.node_viol;
+    }
     printf("{\"tests\": %ld, \"accepted\": %ld, \"dist_checked\": %ld, \"dist_violations\": %ld, "
            "\"dist_violations_tight\": %ld, \"walk_checked\": %ld, \"walk_violations\": %ld, \"zkey_checked\": %ld, "
            "\"zkey_violations\": %ld, \"uncovered\": %ld, \"max_ratio\": %.6g, \"max_ratio_tight\": %.6g, "
