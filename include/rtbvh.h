@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RTBVH_ABI_VERSION 7
+#define RTBVH_ABI_VERSION 8
 
 typedef enum {
     RTBVH_OK = 0,
@@ -218,11 +218,15 @@ typedef struct {
      * pass [0] and those that passed the tile's 8 x 8-block bound test [1] (one leaf-record fetch each) */
     uint64_t bin_entries[2];
     /* RTBVH_FLAG_AUTO_WALK, last trace: the rays re-traced in the reference order because their certificate
-     * failed, of the primary pass [0] and of the bounce passes [1] */
+     * failed, of the primary pass [0] and of the bounce passes [1] (deferred rays included) */
     uint64_t redo_rays[2];
     /* RTBVH_FLAG_COUNT_VISITS with RTBVH_FLAG_REFILL_BOUNCE, last trace: the longest bounce walk, as its
      * loop iterations << 32 | the pixel (framebuffer index) of its ray */
     uint64_t trav_longest;
+    /* RTBVH_FLAG_AUTO_WALK, last trace (ABI 8): of redo_rays[1], the bounce rays the certified walk's margin does
+     * not cover (a direction component under 2^-20, |d| off unit, |o| > 2^90), deferred at their first step and
+     * walked in the reference order by the walk's drained waves or the re-trace kernel */
+    uint64_t redo_deferred;
 } rtbvh_stats;
 typedef struct rtbvh_ctx rtbvh_ctx;
 

@@ -82,7 +82,7 @@ class Stats(ctypes.Structure):
                 ("walk_state", ctypes.c_uint32), ("packet_steps", ctypes.c_uint64 * 2),
                 ("cert_traces", ctypes.c_uint64), ("redo_total", ctypes.c_uint64),
                 ("bin_entries", ctypes.c_uint64 * 2), ("redo_rays", ctypes.c_uint64 * 2),
-                ("trav_longest", ctypes.c_uint64)]
+                ("trav_longest", ctypes.c_uint64), ("redo_deferred", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         d = {}

@@ -156,6 +156,8 @@ struct rtbvh_ctx {
     // set, the list of rays a pass re-traces in the reference order (their counts: d_qcount 16..31)
     uint32_t* d_redo[MAXSPLIT] = {};
     size_t cap_redo[MAXSPLIT] = {};
+    uint32_t* d_defer[MAXSPLIT] = {};   // the certified bounce walk's deferred rays (trace.hip DEFER_*), kept clean
+    size_t cap_defer[MAXSPLIT] = {};
     uint64_t cert_traces = 0;                         // certified traces so far
     uint32_t last_walk = 0;                           // walk flags of the last trace
     uint32_t last_walk_state = 0;                     // rtbvh_stats.walk_state of the last trace
@@ -751,6 +753,17 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (s != c->stream) HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
     }
     // a certified trace's re-trace list (one chain: buffer set `slot`; counts at d_qcount 16 + pass)
+    if (cert && bounces > 0 && c->cap_defer[slot] < P) {   // (zeroed once: its readers clear what they take)
+        drop_graph(c);
+        dfree(c->d_defer[slot]);
+        HIPC(c, dalloc(c->d_defer[slot], P));
+        HIPC(c, hipMemsetAsync(c->d_defer[slot], 0, sizeof(uint32_t) * P, c->stream));
+        if (s != c->stream) {
+            if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
+            HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+        }
+        c->cap_defer[slot] = P;
+    }
     if (cert && c->cap_redo[slot] < P) {
         drop_graph(c);
         HIPC(c, dalloc(c->d_redo[slot], P));
@@ -840,10 +853,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             }
             if (refill) {
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[3], sg));
-                launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, wk.bounce, hit,
-                                       nx + (size_t)NEXT_SEGS * NEXT_STRIDE * b, tblocks, sg, cert);
+                uint32_t* nxb = nx + (size_t)NEXT_SEGS * NEXT_STRIDE * b;
+                launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, wk.bounce, hit, nxb, tblocks, sg, cert,
+                                       c->d_defer[slot]);
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[4], sg));
-                const Redo rd{c->d_redo[slot], &qc[17 + b]};
+                const Redo rd{c->d_redo[slot], &qc[17 + b], c->d_defer[slot], nxb};
                 launch_bounce_shade(ag, q[b & 1], &qc[b], hit, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
                                     Pg, sg, cert ? &rd : nullptr);
             } else
@@ -1080,6 +1094,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_counters);
     dfree(c->d_ovf);
     for (auto& r : c->d_redo) dfree(r);
+    for (auto& r : c->d_defer) dfree(r);
     for (auto& p : c->pb) dfree(p.list);
     dfree(c->d_cam);
     for (auto& t : c->deals) free_deal(t);
@@ -1816,6 +1831,14 @@ rtbvh_status rtbvh_get_stats(rtbvh_ctx* c, rtbvh_stats* out) {
         HIPC(c, hipMemcpy(q, c->d_qcount + 32 * c->last_slot, sizeof(q), hipMemcpyDeviceToHost));
         out->redo_rays[0] = q[16];
         for (uint32_t k = 0; k < c->bounces && k < 15; k++) out->redo_rays[1] += q[17 + k];
+        // ... and the bounce walks' deferred rays (walked in the reference order by the walk or k_bounce_redo)
+        for (uint32_t k = 0; k < c->bounces && k < 15; k++) {
+            uint32_t nd = 0;
+            HIPC(c, hipMemcpy(&nd, c->d_next + (size_t)NEXT_WORDS * c->last_slot + (size_t)NEXT_SEGS * NEXT_STRIDE * k +
+                                       DEFER_COUNT, sizeof(nd), hipMemcpyDeviceToHost));
+            out->redo_rays[1] += nd;
+            out->redo_deferred += nd;
+        }
     }
     out->redo_total = out->redo_rays[0] + out->redo_rays[1];
     return RTBVH_OK;

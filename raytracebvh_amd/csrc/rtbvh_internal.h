@@ -156,9 +156,13 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
 // A certified trace's re-trace list: the rays of one pass whose certificate failed, and their
 // count (zeroed before the pass); the pass's re-trace kernel (reference order) runs over them, REDO_BLOCKS
 // workgroups striding over the count on the device
+// The certified bounce walk's deferred rays (trace.hip DEFER_*): a clean list of P words per buffer set (readers
+// clear what they take) and the pass's work-counter words (its claim and count); null outside bounce passes
 struct Redo {
     uint32_t* list;
     uint32_t* count;
+    uint32_t* defer = nullptr;
+    const uint32_t* dnext = nullptr;
 };
 constexpr uint32_t REDO_BLOCKS = 512;
 // binned primary rays (trace.hip k_primary_binned): the rank's frame in PB_TILE x PB_TILE screen
@@ -218,12 +222,15 @@ void launch_bounce(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_coun
 constexpr uint32_t NEXT_SEGS = RTBVH_NEXT_SEGS;
 constexpr uint32_t NEXT_STRIDE = 32;                          // one 128-B line per counter
 constexpr uint32_t NEXT_WORDS = 16 * NEXT_SEGS * NEXT_STRIDE;  // per buffer set: bounce passes 0..15
+// the certified walk's deferred rays (trace.hip): claim and count words in the pass's first counter line
+constexpr uint32_t DEFER_CLAIM = 1, DEFER_COUNT = 2;
+constexpr uint32_t DEFER_VALID = 0x80000000u;
 // cert: the certified 4-wide walk (WIDE_QUANTIZED, no stack limit, a clz64 tree), whose hit records flag
 // the rays it cannot vouch for; the shading with a Redo checks each hit's certificate and re-traces
 // the flagged rays in the reference order
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
-                            hipStream_t s, bool cert = false);
+                            hipStream_t s, bool cert = false, uint32_t* defer = nullptr);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s,
                          const Redo* redo = nullptr);

@@ -1468,6 +1468,25 @@ __device__ __forceinline__ bool qbox_fast_cert(const QAxis& x, const QAxis& y, c
 // all triangles the reference could test.  A ray the bound does not cover -- a slack-test-free ray
 // (qnode_fast_ray), |d| off unit, a node without a grid, a stack overflow -- is flagged in its hit record
 // (HIT_FLAG) for the reference-order re-trace (k_bounce_redo).
+// The deferred rays of a certified bounce pass (the rays its margin does not cover: |1/d| > 2^20, |o| > 2^90,
+// |d| off unit).  The walk lists them at claim time in the pass's defer list -- entry k at defer[k] with
+// DEFER_VALID set, k from the counter next[DEFER_COUNT] -- and writes a "deferred" hit record (t = -inf, flagged:
+// k_bounce_shade skips it).  Drained waves claim entries through next[DEFER_CLAIM] and walk them in the
+// reference order; k_bounce_redo takes the rest.  Readers clear the entries they take.
+// a deferred ray's reference-order walk: its hit record, "exact" (t negated; a miss -inf with id INVALID)
+template <bool COUNT>
+__device__ __forceinline__ float2 defer_walk(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
+                                             uint32_t T, const RayQ* e, Counts& c) {
+    const float4 q0 = reinterpret_cast<const float4*>(e)[0], q1 = reinterpret_cast<const float4*>(e)[1];
+    const f3 o = mk(q0.z, q0.w, q1.x), d = mk(q1.y, q1.z, q1.w);
+    const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    float best;
+    uint32_t bl;
+    const bool h = traverse<COUNT, false>(inner, leaf, T, o, d, inv, STACK_SIZE, best, bl, c);
+    const uint32_t tri = h ? __float_as_uint(leaf[4 * (size_t)bl + 2].y) & ~LEAF_BIT : INVALID;
+    return make_float2(h ? -best : -__builtin_inff(), __uint_as_float(tri));
+}
+
 template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
@@ -1477,7 +1496,8 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           const uint32_t* __restrict__ perm,
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
-                                                          unsigned long long* __restrict__ overflow, int stack_limit) {
+                                                          unsigned long long* __restrict__ overflow, int stack_limit,
+                                                          uint32_t* __restrict__ defer) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
@@ -1641,9 +1661,15 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     top = INVALID;
                     node = root_slot(T);
                     guard = 2 * T + 2;
-                    if (CERT) {   // a ray the margin does not cover ends at its first step, flagged
+                    if (CERT) {   // a ray the margin does not cover is deferred (DEFER_* below)
                         flg = !(qfast && dot(d, d) <= MT_DD);
-                        if (flg) node = INVALID;
+                        if (flg) {
+                            const uint32_t k = atomicAdd(next + DEFER_COUNT, 1u);
+                            __hip_atomic_store(defer + k, r | DEFER_VALID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            hitrec[r] = make_float2(-__builtin_inff(), __uint_as_float(INVALID ^ HIT_FLAG));
+                            has = false;
+                            flg = false;
+                        }
                     }
                 }
             }
@@ -1808,6 +1834,42 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             }
         }
     }
+    if (CERT) {
+        // The deferred rays (the slack test cannot take them): once its part of the queue is drained, the wave
+        // claims them -- up to 64 at a time, lane k the k-th -- and walks each in the reference order (the
+        // exact findCollision DFS); the hit record says "exact" (t negated), so k_bounce_shade shades it
+        // without a certificate.  A deferred ray no wave claims here (appended after the waves looked)
+        // is re-traced by k_bounce_redo.  The walks' tail hides these few long reference-order walks.
+        for (;;) {
+            uint32_t base = 0, m = 0;
+            if (lane == 0) {
+                uint32_t v = __hip_atomic_load(next + DEFER_CLAIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (;;) {
+                    const uint32_t nd = __hip_atomic_load(next + DEFER_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v >= nd) break;
+                    const uint32_t want = min(nd - v, 64u);
+                    if (__hip_atomic_compare_exchange_strong(next + DEFER_CLAIM, &v, v + want, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        base = v;
+                        m = want;
+                        break;
+                    }
+                }
+            }
+            base = __builtin_amdgcn_readfirstlane(base);
+            m = __builtin_amdgcn_readfirstlane(m);
+            if (m == 0) break;
+            if (lane < m) {
+                // (the appending lane stores its entry right after its count add: wait for it)
+                uint32_t e;
+                do {
+                    e = __hip_atomic_load(defer + base + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } while (!(e & DEFER_VALID));
+                defer[base + lane] = 0u;   // (the list is clean for the next pass)
+                hitrec[e & ~DEFER_VALID] = defer_walk<COUNT>(inner, leaf, T, qin + (e & ~DEFER_VALID), c);
+            }
+        }
+    }
     if (COUNT || __ballot(c.overflow != 0)) {
         unsigned long long v[3] = {c.internal, c.leaf, c.overflow};
 #pragma unroll
@@ -1898,17 +1960,22 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
     RayQ e;
     if (i < n) {
         e = qin[i];
-        const float2 h2 = hitrec[i];
+        float2 h2 = hitrec[i];
         uint32_t tri = __float_as_uint(h2.y);
+        bool skip = false;
         if (CERT) {
             flagged = hit_flagged(tri);
             tri = (tri & LEAF_BIT) ? INVALID : tri & ~HIT_FLAG;
-            if (!flagged && tri != INVALID) {
+            if (signbit(h2.x)) {   // the walk's deferred rays (trace.hip DEFER_*): walked in the reference order
+                skip = flagged;    //   by the walk's drained waves (exact: shaded as is), or by k_bounce_redo
+                flagged = false;
+                h2.x = -h2.x;
+            } else if (!flagged && tri != INVALID) {
                 const f3 d = mk(e.dx, e.dy, e.dz);
                 flagged = !leaf_certified(a, tri, mk(e.ox, e.oy, e.oz), mk(1.f / d.x, 1.f / d.y, 1.f / d.z), h2.x);
             }
         }
-        if (!flagged) live = bounce_apply(a, e, tri, h2.x, hits, tex);
+        if (!flagged && !skip) live = bounce_apply(a, e, tri, h2.x, hits, tex);
     }
     if (CERT) {
         const uint32_t slot = wave_append(flagged, redo_count);
@@ -1925,13 +1992,18 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
 // The reference-order re-trace of the rays a certified bounce pass flagged (redo: queue indices): the
 // exact findCollision DFS (traverse, reference order), then the shading as k_bounce_shade.  A fixed grid
 // over the count on the device (a captured frame replays it as it is).
+// Then the walk's deferred rays no drained wave claimed (trace.hip DEFER_*: entries [next[DEFER_CLAIM],
+// next[DEFER_COUNT]) of the defer list, cleared as they are read) come first in the index space.
 template <bool COUNT>
 __global__ __launch_bounds__(BLOCK) void k_bounce_redo(TraceArgs a, const RayQ* __restrict__ qin,
                                                        const uint32_t* __restrict__ redo,
                                                        const uint32_t* __restrict__ redo_count,
                                                        RayQ* __restrict__ qout, uint32_t* __restrict__ qout_count,
-                                                       int emit) {
-    const uint32_t n = *redo_count;
+                                                       int emit, uint32_t* __restrict__ defer,
+                                                       const uint32_t* __restrict__ dnext) {
+    const uint32_t d0 = defer ? min(dnext[DEFER_CLAIM], dnext[DEFER_COUNT]) : 0u;
+    const uint32_t nd = defer ? dnext[DEFER_COUNT] - d0 : 0u;
+    const uint32_t n = nd + *redo_count;
     Counts c = {0, 0, 0, 0, 0};
     uint32_t hits = 0, tex = 0;
     for (uint32_t base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
@@ -1939,7 +2011,14 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_redo(TraceArgs a, const RayQ* 
         bool live = false;
         RayQ e;
         if (i < n) {
-            e = qin[redo[i]];
+            uint32_t r;
+            if (i < nd) {
+                r = defer[d0 + i] & ~DEFER_VALID;
+                defer[d0 + i] = 0u;
+            } else {
+                r = redo[i - nd];
+            }
+            e = qin[r];
             const f3 o = mk(e.ox, e.oy, e.oz), d = mk(e.dx, e.dy, e.dz);
             const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
             float best;
@@ -2053,11 +2132,11 @@ void launch_primary_c(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count,
 
 template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                          float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, hipStream_t s) {
+                          float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, uint32_t* defer, hipStream_t s) {
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
 #define RTBVH_BT(L, G, C)                                                                                              \
     hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
-                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim)
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, defer)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
     if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
@@ -2180,9 +2259,9 @@ void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, 
 
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
-                            hipStream_t s, bool cert) {
+                            hipStream_t s, bool cert, uint32_t* defer) {
     if (blocks == 0) blocks = 2048;
-#define RTBVH_TRAV(C, M) launch_bounce_trav_t<C, M>(a, qin, qin_count, perm, hitrec, next, blocks, cert, s)
+#define RTBVH_TRAV(C, M) launch_bounce_trav_t<C, M>(a, qin, qin_count, perm, hitrec, next, blocks, cert, defer, s)
     switch (walk) {
         case BounceWalk::NEAREST: if (count) RTBVH_TRAV(true, 1); else RTBVH_TRAV(false, 1); break;
         case BounceWalk::WIDE_QUANTIZED: if (count) RTBVH_TRAV(true, 2); else RTBVH_TRAV(false, 2); break;
@@ -2204,11 +2283,11 @@ void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qi
     if (count) { if (redo) RTBVH_BS(true, true); else RTBVH_BS(true, false); }
     else { if (redo) RTBVH_BS(false, true); else RTBVH_BS(false, false); }
 #undef RTBVH_BS
-    if (redo) {   // the flagged rays, in the reference order
+    if (redo) {   // the flagged rays (and the walk's deferred rays left over), in the reference order
         if (count) hipLaunchKernelGGL((k_bounce_redo<true>), dim3(REDO_BLOCKS), dim3(BLOCK), 0, s, a, qin, rl, rc, qout,
-                                      qout_count, (int)emit);
+                                      qout_count, (int)emit, redo->defer, redo->dnext);
         else hipLaunchKernelGGL((k_bounce_redo<false>), dim3(REDO_BLOCKS), dim3(BLOCK), 0, s, a, qin, rl, rc, qout,
-                                qout_count, (int)emit);
+                                qout_count, (int)emit, redo->defer, redo->dnext);
     }
 }
 

@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     L = rt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.rtbvh_abi_version() == 7
+    assert L.rtbvh_abi_version() == 8
 
 
 def test_layout_sizes():
