@@ -648,6 +648,10 @@ __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_l
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// the set lanes of mask below this lane (v_mbcnt: no 64-bit lane mask held in VGPRs)
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
 // wave-aggregated append: one atomic per wave, lanes keep their order
 __device__ __forceinline__ uint32_t wave_append(bool active, uint32_t* counter) {
     const uint64_t mask = __ballot(active);
@@ -656,9 +660,8 @@ __device__ __forceinline__ uint32_t wave_append(bool active, uint32_t* counter) 
     const int leader = __ffsll((unsigned long long)mask) - 1;
     uint32_t base = 0;
     if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader, 64);
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    return base + (uint32_t)__popcll(mask & lt);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    return base + lane_rank(mask);
 }
 
 // counters: [base] internal visits, [base+1] leaf visits, [base+2] hits (base 2 primary,
@@ -694,8 +697,14 @@ __device__ __forceinline__ void flush_counts(const TraceArgs& a, const Counts& c
 // RayTraceLaunch.hlsl:40-86 for one pixel of the frame, from its closest hit (phit: sorted leaf bl
 // at distance best): colour, intensity, the RayPresent records, and the reflection ray in e
 // (returns whether it is live, i.e. traced by RayTraceReflection.hlsl:17-18)
+// REC false: a trace without RayPresent records (a.refl_rec, a.refr_rec null; the binned pass's shading then
+// holds its registers at 8 waves per SIMD)
+// qdst: where a live ray goes, when the caller knows it before the shading (the binned pass: no RayQ held
+// across the shading)
+template <bool REC = true>
 __device__ __forceinline__ bool primary_pixel(const TraceArgs& a, size_t out, f3 o, f3 d, bool phit, float best,
-                                              uint32_t bl, uint32_t& hits, uint32_t& tex, RayQ& e) {
+                                              uint32_t bl, uint32_t& hits, uint32_t& tex, RayQ& e,
+                                              RayQ* qdst = nullptr) {
     float4 color;
     float intensity = 0.f;
     bool live = false;
@@ -713,13 +722,14 @@ __device__ __forceinline__ bool primary_pixel(const TraceArgs& a, size_t out, f3
             e.ox = ro.x; e.oy = ro.y; e.oz = ro.z;
             e.dx = rd.x; e.dy = rd.y; e.dz = rd.z;
             live = true;
+            if (qdst) *qdst = e;
         }
-        if (a.refl_rec) {   // :48-67 (the ray is set only when the intensity is not 0)
+        if (REC && a.refl_rec) {   // :48-67 (the ray is set only when the intensity is not 0)
             const bool rr = intensity != 0;
             put_record(a.refl_rec, out, intensity, rr, rr ? add(h.hitp, mul(h.nrm, .001f)) : o,
                        rr ? normalize(reflect(d, h.nrm)) : d, color);
         }
-        if (a.refr_rec) {   // :70-80, REFRACTION_DECAY 1
+        if (REC && a.refr_rec) {   // :70-80, REFRACTION_DECAY 1
             const float ri = (1.f - h.alpha) * 1;
             const bool rr = ri != 0;
             put_record(a.refr_rec, out, ri, rr, rr ? sub(h.hitp, mul(h.nrm, .001f)) : o,
@@ -728,8 +738,8 @@ __device__ __forceinline__ bool primary_pixel(const TraceArgs& a, size_t out, f3
         }
     } else {
         color = make_float4(.5f, .5f, .5f, 1.f);   // getBackground, :85-86
-        if (a.refl_rec) put_record(a.refl_rec, out, 0.f, false, o, d, color);   // clearRayPresent
-        if (a.refr_rec) put_record(a.refr_rec, out, 0.f, false, o, d, color);
+        if (REC && a.refl_rec) put_record(a.refl_rec, out, 0.f, false, o, d, color);   // clearRayPresent
+        if (REC && a.refr_rec) put_record(a.refr_rec, out, 0.f, false, o, d, color);
     }
     a.color[out] = color;
     if (a.intensity) a.intensity[out] = intensity;
@@ -905,7 +915,7 @@ constexpr uint32_t PB_RASTER_BLOCK = RTBVH_PB_RASTER_BLOCK;   // threads per til
 #ifndef RTBVH_PB_PROBE
 #define RTBVH_PB_PROBE 0
 #endif
-template <bool COUNT, bool CERT, uint32_t NT, class KeyAt>
+template <bool COUNT, bool CERT, uint32_t NT, bool REC, class KeyAt>
 __device__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at, RayQ* __restrict__ q,
                               uint32_t* __restrict__ qcount, int emit, uint32_t* __restrict__ redo,
                               uint32_t* __restrict__ redo_count, uint32_t* s_cnt, uint64_t* s_mask, uint32_t& s_base);
@@ -919,7 +929,7 @@ __device__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at,
 #define RTBVH_PB_WAVES 8   // k_primary_binned's launch bounds: 8 waves per SIMD with 37 VGPRs spilled beat
                                    // 6 (16 spilled) and 5 (none) -- primary pass 0.87-0.89 / 0.91-0.93 / 0.98 ms
 #endif
-template <bool COUNT, bool CERT = false, bool FUSE = false>
+template <bool COUNT, bool CERT = false, bool FUSE = false, bool REC = true>
 __global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
                                                              const uint4* __restrict__ bins, uint32_t cap,
                                                              uint32_t ntx, uint32_t rows,
@@ -1050,7 +1060,7 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_bin
                 const bool need = ok && (sg || sz <= __uint_as_float(s_t[2 * pb_slot(pi) + 1]));
                 const uint64_t nm = __ballot(need);
                 if (qn + (uint32_t)__popcll(nm) > PB_QCAP) flush();
-                if (need) sq[qn + (uint32_t)__popcll(nm & ((1ull << lane) - 1))] = (uint32_t)k << 10 | pi;
+                if (need) sq[qn + lane_rank(nm)] = (uint32_t)k << 10 | pi;
                 qn += (uint32_t)__popcll(nm);
             }
         }
@@ -1082,7 +1092,7 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_bin
         __shared__ uint32_t s_cnt[(PB_TILE / 8) * (PB_TILE / 8)];
         __shared__ uint64_t s_mask[2 * (PB_TILE / 8) * (PB_TILE / 8)];
         __shared__ uint32_t s_base;
-        pb_shade_tile<COUNT, CERT, PB_RASTER_BLOCK>(
+        pb_shade_tile<COUNT, CERT, PB_RASTER_BLOCK, REC>(
             a, rows, [&](uint32_t crow, uint32_t x) { return s_key[(crow - C0) * PB_KS + (x - X0)]; }, q, qcount, emit,
             redo, redo_count, s_cnt, s_mask, s_base);
     } else {
@@ -1123,7 +1133,7 @@ constexpr uint32_t PB_SHADE_BLOCK = RTBVH_PB_SHADE_BLOCK;
 // turn; a first pass counts each one's live rays (and certificates) into LDS, the tile claims its queue
 // range, then a second pass shades them (no per-sub-tile registers held across the claim).
 // (Inlined: out of line, A/B round 5, the fused binned pass took 1.07 ms against 0.86.)
-template <bool COUNT, bool CERT, uint32_t NT, class KeyAt>
+template <bool COUNT, bool CERT, uint32_t NT, bool REC, class KeyAt>
 __device__ __forceinline__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at, RayQ* __restrict__ q,
                                               uint32_t* __restrict__ qcount, int emit, uint32_t* __restrict__ redo,
                                               uint32_t* __restrict__ redo_count, uint32_t* s_cnt, uint64_t* s_mask,
@@ -1132,7 +1142,8 @@ __device__ __forceinline__ void pb_shade_tile(const TraceArgs& a, uint32_t rows,
     const uint32_t X0 = blockIdx.x * PB_TILE, C0 = blockIdx.y * PB_TILE;
     constexpr uint32_t NST = (PB_TILE / 8) * (PB_TILE / 8) / (NT / 64);   // sub-tiles per wave
     constexpr uint32_t NSUB = (PB_TILE / 8) * (PB_TILE / 8);
-    const float hw = (float)(a.W >> 1), hh = (float)(a.H >> 1);
+    const float hw = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint((float)(a.W >> 1))));
+    const float hh = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint((float)(a.H >> 1))));
     const auto pixel = [&](uint32_t i, uint32_t& x, uint32_t& crow) {
         const uint32_t st = w + i * (NT / 64);
         x = X0 + (st % (PB_TILE / 8)) * 8 + (lane & 7u);
@@ -1178,13 +1189,20 @@ __device__ __forceinline__ void pb_shade_tile(const TraceArgs& a, uint32_t rows,
         s_base = run && emit ? atomicAdd(qcount, run) : 0u;
     }
     __syncthreads();
+    const uint32_t sbase = (uint32_t)__builtin_amdgcn_readfirstlane(s_base);
     uint32_t hits = 0, tex = 0;
 #pragma unroll 1
     for (uint32_t i = 0; i < NST; i++) {
         uint32_t x, crow;
         const bool valid = pixel(i, x, crow);
         const uint32_t st = w + i * (NT / 64);
-        const uint64_t livem = s_mask[st], flagm = CERT ? s_mask[NSUB + st] : 0ull;
+        // (wave-uniform: into SGPRs, so the shading below keeps its VGPRs)
+        const auto uni64 = [](uint64_t v) {
+            return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
+        };
+        const uint64_t livem = uni64(s_mask[st]), flagm = CERT ? uni64(s_mask[NSUB + st]) : 0ull;
+        const uint32_t qb = sbase + (uint32_t)__builtin_amdgcn_readfirstlane(s_cnt[st]);
         const bool flag = CERT && ((flagm >> lane) & 1u);
         if (CERT && flagm) {   // (rare) the re-trace list, one atomic per wave
             const uint32_t slot = wave_append(flag, redo_count);
@@ -1196,11 +1214,13 @@ __device__ __forceinline__ void pb_shade_tile(const TraceArgs& a, uint32_t rows,
             const bool phit = key != NO_HIT;
             uint32_t h1 = 0, t1 = 0;
             RayQ e;
-            const bool live = primary_pixel(a, (size_t)crow * a.W + x, o, mk(0.f, 0.f, 1.f), phit,
-                                            phit ? key_t(key) : 0.f, phit ? (uint32_t)key : 0u, h1, t1, e);
+            // (the live rays were counted above: this lane's queue entry is known before the shading)
+            RayQ* dst = emit && ((livem >> lane) & 1u) ? q + qb + lane_rank(livem)
+                                                        : nullptr;
+            (void)primary_pixel<REC>(a, (size_t)crow * a.W + x, o, mk(0.f, 0.f, 1.f), phit, phit ? key_t(key) : 0.f,
+                                     phit ? (uint32_t)key : 0u, h1, t1, e, dst);
             hits += h1;
             tex += t1;
-            if (emit && live) q[s_base + s_cnt[st] + (uint32_t)__popcll(livem & ((1ull << lane) - 1))] = e;
         }
     }
     if (COUNT) {
@@ -1219,7 +1239,7 @@ __global__ __launch_bounds__(PB_SHADE_BLOCK, 8) void k_pb_shade(TraceArgs a, con
     __shared__ uint32_t s_base;
     const uint32_t tile = blockIdx.y * ntx + blockIdx.x;
     if (off[(tile + 1) * PB_NZ] > cap) return;
-    pb_shade_tile<COUNT, CERT, PB_SHADE_BLOCK>(
+    pb_shade_tile<COUNT, CERT, PB_SHADE_BLOCK, true>(
         a, rows, [&](uint32_t crow, uint32_t x) { return keys[(size_t)crow * a.W + x]; }, q, qcount, emit, redo,
         redo_count, s_cnt, s_mask, s_base);
 }
@@ -1642,8 +1662,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             base = __builtin_amdgcn_readfirstlane(base);
             if (base + nidle >= len && ++kseg == NEXT_SEGS) drained = true;   // segment (and the last) used up
             if (!has) {
-                const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-                const uint32_t p = base + (uint32_t)__popcll(idle & lt);
+                const uint32_t p = base + lane_rank(idle);
                 if (p < len) {
                     r = perm ? perm[s0 + p] : s0 + p;
                     const float4 q0 = reinterpret_cast<const float4*>(qin + r)[0];
@@ -2192,9 +2211,16 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
     const dim3 grid(pb.ntx, pb.nty);
     uint32_t* rl = redo ? redo->list : nullptr;
     uint32_t* rc = redo ? redo->count : nullptr;
+    const bool rec = a.refl_rec || a.refr_rec;
 #define RTBVH_PBR(C, R, F)                                                                                          \
-    hipLaunchKernelGGL((k_primary_binned<C, R, F>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off, pb.bins, pb.cap,    \
-                       pb.ntx, rows, pb.keys, q, qcount, (int)emit, rl, rc)
+    do {                                                                                                            \
+        if (rec || !(F))                                                                                            \
+            hipLaunchKernelGGL((k_primary_binned<C, R, F, true>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off,     \
+                               pb.bins, pb.cap, pb.ntx, rows, pb.keys, q, qcount, (int)emit, rl, rc);               \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_primary_binned<C, R, F, false>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off,    \
+                               pb.bins, pb.cap, pb.ntx, rows, pb.keys, q, qcount, (int)emit, rl, rc);               \
+    } while (0)
 #define RTBVH_PBS(C, R)                                                                                              \
     hipLaunchKernelGGL((k_pb_shade<C, R>), grid, dim3(PB_SHADE_BLOCK), 0, s, a, pb.off, pb.cap, pb.ntx, rows, pb.keys, q, \
                        qcount, (int)emit, rl, rc)
