@@ -1493,6 +1493,9 @@ __device__ __forceinline__ bool qbox_fast_cert(const QAxis& x, const QAxis& y, c
 // DEFER_VALID set, k from the counter next[DEFER_COUNT] -- and writes a "deferred" hit record (t = -inf, flagged:
 // k_bounce_shade skips it).  Drained waves claim entries through next[DEFER_CLAIM] and walk them in the
 // reference order; k_bounce_redo takes the rest.  Readers clear the entries they take.
+#ifndef RTBVH_DEFER_INWALK
+#define RTBVH_DEFER_INWALK 1   // (0, A/B: every deferred ray to k_bounce_redo)
+#endif
 // a deferred ray's reference-order walk: its hit record, "exact" (t negated; a miss -inf with id INVALID)
 template <bool COUNT>
 __device__ __forceinline__ float2 defer_walk(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
@@ -1683,9 +1686,11 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     if (CERT) {   // a ray the margin does not cover is deferred (DEFER_* below)
                         flg = !(qfast && dot(d, d) <= MT_DD);
                         if (flg) {
-                            const uint32_t k = atomicAdd(next + DEFER_COUNT, 1u);
-                            __hip_atomic_store(defer + k, r | DEFER_VALID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            // the "deferred" record first, then the entry with release order: a wave that takes
+                            // the entry (acquire) writes the walk's record after this one, never under it
                             hitrec[r] = make_float2(-__builtin_inff(), __uint_as_float(INVALID ^ HIT_FLAG));
+                            const uint32_t k = atomicAdd(next + DEFER_COUNT, 1u);
+                            __hip_atomic_store(defer + k, r | DEFER_VALID, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                             has = false;
                             flg = false;
                         }
@@ -1853,7 +1858,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             }
         }
     }
-    if (CERT) {
+    if (CERT && RTBVH_DEFER_INWALK) {
         // The deferred rays (the slack test cannot take them): once its part of the queue is drained, the wave
         // claims them -- up to 64 at a time, lane k the k-th -- and walks each in the reference order (the
         // exact findCollision DFS); the hit record says "exact" (t negated), so k_bounce_shade shades it
@@ -1882,7 +1887,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                 // (the appending lane stores its entry right after its count add: wait for it)
                 uint32_t e;
                 do {
-                    e = __hip_atomic_load(defer + base + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    e = __hip_atomic_load(defer + base + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 } while (!(e & DEFER_VALID));
                 defer[base + lane] = 0u;   // (the list is clean for the next pass)
                 hitrec[e & ~DEFER_VALID] = defer_walk<COUNT>(inner, leaf, T, qin + (e & ~DEFER_VALID), c);
