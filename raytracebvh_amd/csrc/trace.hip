@@ -1510,6 +1510,52 @@ __device__ __forceinline__ float2 defer_walk(const Inner* __restrict__ inner, co
     return make_float2(h ? -best : -__builtin_inff(), __uint_as_float(tri));
 }
 
+// One wave takes deferred rays -- up to 64 at a time, lane k the k-th -- and walks each in the reference order,
+// until the list holds none it has not taken
+template <bool COUNT>
+__device__ __forceinline__ void defer_walk_all(uint32_t* __restrict__ next, uint32_t* __restrict__ defer,
+                                               const Inner* __restrict__ inner, const float4* __restrict__ leaf,
+                                               uint32_t T, const RayQ* __restrict__ qin, float2* __restrict__ hitrec,
+                                               Counts& c) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (;;) {
+        uint32_t base = 0, m = 0;
+        if (lane == 0) {
+            uint32_t v = __hip_atomic_load(next + DEFER_CLAIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (;;) {
+                const uint32_t nd = __hip_atomic_load(next + DEFER_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v >= nd) break;
+                const uint32_t want = min(nd - v, 64u);
+                if (__hip_atomic_compare_exchange_strong(next + DEFER_CLAIM, &v, v + want, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    base = v;
+                    m = want;
+                    break;
+                }
+            }
+        }
+        base = __builtin_amdgcn_readfirstlane(base);
+        m = __builtin_amdgcn_readfirstlane(m);
+        if (m == 0) return;
+        if (lane < m) {
+            // (the appending lane stores its entry right after its count add: wait for it)
+            uint32_t e;
+            do {
+                e = __hip_atomic_load(defer + base + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            } while (!(e & DEFER_VALID));
+            defer[base + lane] = 0u;   // (the list is clean for the next pass)
+            hitrec[e & ~DEFER_VALID] = defer_walk<COUNT>(inner, leaf, T, qin + (e & ~DEFER_VALID), c);
+        }
+    }
+}
+// the deferral workers: wave 0 of the first DEFER_WORKERS workgroups (one per XCD) walks the deferred rays as they
+// come, from the start of the pass -- beside the walk, not after it -- and leaves once every queue segment is
+// claimed and the list is empty (a ray deferred after that goes to the drained waves or k_bounce_redo)
+#ifndef RTBVH_DEFER_WORKERS
+#define RTBVH_DEFER_WORKERS 8
+#endif
+constexpr uint32_t DEFER_WORKERS = RTBVH_DEFER_WORKERS;
+
 template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
@@ -1528,6 +1574,34 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     if (n == 0) return;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0, 0, 0};
+    if (CERT && DEFER_WORKERS && blockIdx.x < DEFER_WORKERS && gridDim.x > 2 * DEFER_WORKERS && threadIdx.x < 64) {
+        for (;;) {
+            defer_walk_all<COUNT>(next, defer, inner, leaf, T, qin, hitrec, c);
+            // every segment claimed (lane k: segment k's counter past its length): no ray left to defer but
+            // those being claimed right now
+            bool used = true;
+            for (uint32_t seg = lane; seg < NEXT_SEGS; seg += 64) {
+                const uint32_t s0 = (uint32_t)((uint64_t)n * seg / NEXT_SEGS);
+                const uint32_t len = (uint32_t)((uint64_t)n * (seg + 1) / NEXT_SEGS) - s0;
+                used = used && __hip_atomic_load(next + NEXT_STRIDE * seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= len;
+            }
+            if (__ballot(!used) == 0) break;
+            __builtin_amdgcn_s_sleep(64);
+        }
+        defer_walk_all<COUNT>(next, defer, inner, leaf, T, qin, hitrec, c);
+        if (COUNT) {
+            unsigned long long v[2] = {c.internal, c.leaf};
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+            if (lane == 0) {
+                atomicAdd(&counters[5], v[0]);
+                atomicAdd(&counters[6], v[1]);
+            }
+        }
+        return;
+    }
     bool has = false, hit = false, qfast = false;
     uint32_t r = 0, node = 0, top = INVALID, bl = 0, guard = 0;
     uint32_t btri = 0;       // triangle of the best hit (leaf record word 9): the hit record's id
@@ -1859,40 +1933,11 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
         }
     }
     if (CERT && RTBVH_DEFER_INWALK) {
-        // The deferred rays (the slack test cannot take them): once its part of the queue is drained, the wave
-        // claims them -- up to 64 at a time, lane k the k-th -- and walks each in the reference order (the
-        // exact findCollision DFS); the hit record says "exact" (t negated), so k_bounce_shade shades it
-        // without a certificate.  A deferred ray no wave claims here (appended after the waves looked)
-        // is re-traced by k_bounce_redo.  The walks' tail hides these few long reference-order walks.
-        for (;;) {
-            uint32_t base = 0, m = 0;
-            if (lane == 0) {
-                uint32_t v = __hip_atomic_load(next + DEFER_CLAIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (;;) {
-                    const uint32_t nd = __hip_atomic_load(next + DEFER_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (v >= nd) break;
-                    const uint32_t want = min(nd - v, 64u);
-                    if (__hip_atomic_compare_exchange_strong(next + DEFER_CLAIM, &v, v + want, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        base = v;
-                        m = want;
-                        break;
-                    }
-                }
-            }
-            base = __builtin_amdgcn_readfirstlane(base);
-            m = __builtin_amdgcn_readfirstlane(m);
-            if (m == 0) break;
-            if (lane < m) {
-                // (the appending lane stores its entry right after its count add: wait for it)
-                uint32_t e;
-                do {
-                    e = __hip_atomic_load(defer + base + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                } while (!(e & DEFER_VALID));
-                defer[base + lane] = 0u;   // (the list is clean for the next pass)
-                hitrec[e & ~DEFER_VALID] = defer_walk<COUNT>(inner, leaf, T, qin + (e & ~DEFER_VALID), c);
-            }
-        }
+        // The deferred rays (the slack test cannot take them) the workers above have not taken yet: once its part
+        // of the queue is drained, the wave walks them in the reference order; the hit record says "exact" (t
+        // negated), so k_bounce_shade shades it without a certificate.  A deferred ray no wave takes here
+        // (appended after the waves looked) is re-traced by k_bounce_redo.
+        defer_walk_all<COUNT>(next, defer, inner, leaf, T, qin, hitrec, c);
     }
     if (COUNT || __ballot(c.overflow != 0)) {
         unsigned long long v[3] = {c.internal, c.leaf, c.overflow};
