@@ -9,7 +9,9 @@ export TMPDIR=/tmp
 T=${TAG:-r06_x}
 S=",${STEPS:-tests,oneframe,bench},"
 if [[ $S == *,tests,* ]]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/${T}_gpu_tests.log 2>&1
+  KARGS=()
+  if [ -n "${PYTEST_K:-}" ]; then KARGS=(-k "$PYTEST_K"); fi
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${KARGS[@]}" > gpurun_out/${T}_gpu_tests.log 2>&1
   rc=$?
   tail -3 gpurun_out/${T}_gpu_tests.log
   if [ $rc -ne 0 ]; then echo "TESTS rc=$rc: stop"; grep -E "^(FAILED|E  )" gpurun_out/${T}_gpu_tests.log | head -30; exit 1; fi
