@@ -48,7 +48,33 @@ constexpr int WMAX = 8;
 struct QNodeE {
     uint32_t e[WMAX];
     int n;
+    float qb[WMAX][6];   // QUANT=1: the entries' boxes decoded from the node's 8-bit grid (build.hip quantize_axis)
 };
+// build.hip quantize_axis over n boxes: the decoded corners (origin + q * step, one rounding) that contain them
+static float pow2f_(int e) { uint32_t u = (uint32_t)(e + 127) << 23; float f; memcpy(&f, &u, 4); return f; }
+static void quantize(QNodeE& q, const Node* N) {
+    for (int a = 0; a < 3; a++) {
+        float o = INFINITY, m = -INFINITY;
+        for (int k = 0; k < q.n; k++) { o = std::min(o, N[q.e[k]].bmin[a]); m = std::max(m, N[q.e[k]].bmax[a]); }
+        const float ext = m - o;
+        int e = -120;
+        if (ext > 0.f) {
+            uint32_t u; memcpy(&u, &ext, 4);
+            e = std::max((int)((u >> 23) & 255u) - 127 - 8, -120);
+        }
+        while (std::fma(255.f, pow2f_(e), o) < m) ++e;
+        const float sc = pow2f_(e), rs = pow2f_(-e);
+        for (int k = 0; k < q.n; k++) {
+            const float lo = N[q.e[k]].bmin[a], hi = N[q.e[k]].bmax[a];
+            uint32_t l = (uint32_t)std::min(std::max(std::floor((lo - o) * rs), 0.f), 255.f);
+            uint32_t h = (uint32_t)std::min(std::max(std::ceil((hi - o) * rs), 0.f), 255.f);
+            if (l > 0 && std::fma((float)l, sc, o) > lo) --l;
+            if (h < 255 && std::fma((float)h, sc, o) < hi) ++h;
+            q.qb[k][a] = std::fma((float)l, sc, o);
+            q.qb[k][3 + a] = std::fma((float)h, sc, o);
+        }
+    }
+}
 
 // the ray / box slab test (entry distance, hit)
 static bool slab(const float o[3], const float inv[3], const Node& b, float best, float& tn) {
@@ -61,6 +87,11 @@ static bool slab(const float o[3], const float inv[3], const Node& b, float best
     }
     tn = t0;
     return t0 <= t1;
+}
+static bool slab6(const float o[3], const float inv[3], const float* b, float best, float& tn) {
+    Node n;
+    for (int a = 0; a < 3; a++) { n.bmin[a] = b[a]; n.bmax[a] = b[3 + a]; }
+    return slab(o, inv, n, best, tn);
 }
 // Moller-Trumbore as the kernels (EPSILON 0.01 on the determinant)
 static float tri_hit(const float o[3], const float d[3], const float* v) {
@@ -256,6 +287,16 @@ int main(int argc, char** argv) {
     }
     // greedy collapse (build.hip greedy_qnode_words)
     std::vector<QNodeE> greedy(NN), sah(NN);
+    // LEAFRUN=1: the leaf entries of a node must be one run of consecutive sorted leaves (a 64-B 6-wide node
+    // addresses them by the run's first leaf and a mask): an expansion that would break the run is skipped
+    const bool leafrun = getenv("LEAFRUN") != nullptr;
+    const bool quant = getenv("QUANT") != nullptr;
+    auto run_ok = [&](const uint32_t* E, int n) {
+        uint32_t lo = ~0u, hi = 0, c = 0;
+        for (int k = 0; k < n; k++)
+            if (E[k] < T) { lo = std::min(lo, E[k]); hi = std::max(hi, E[k]); ++c; }
+        return c == 0 || hi - lo + 1 == c;
+    };
     for (uint32_t x : order) {
         uint32_t E[WMAX] = {N[x].child_l, N[x].child_r};
         int n = 2;
@@ -265,7 +306,17 @@ int main(int argc, char** argv) {
             for (int k = 0; k < n && k < W - 1; k++)
                 if (!leaf(E[k])) {
                     const double ar = half_area(N[E[k]]);
-                    if (ar > best) { best = ar; pick = k; }
+                    if (ar > best) {
+                        if (leafrun) {   // the expansion keeps the leaf run
+                            uint32_t F[WMAX];
+                            memcpy(F, E, sizeof F);
+                            F[k] = N[E[k]].child_l;
+                            F[n] = N[E[k]].child_r;
+                            if (!run_ok(F, n + 1)) continue;
+                        }
+                        best = ar;
+                        pick = k;
+                    }
                 }
             if (pick < 0) break;
             const uint32_t sel = E[pick];
@@ -276,6 +327,7 @@ int main(int argc, char** argv) {
         QNodeE& q = greedy[x];
         q.n = n;
         for (int k = 0; k < WMAX; k++) q.e[k] = k < n ? E[k] : 0;
+        if (quant) quantize(q, N);
     }
     // SAH-optimal cuts: D[x][j], j = 1..4
     const double INF = 1e300;
@@ -404,7 +456,9 @@ int main(int argc, char** argv) {
                     int nh = 0;
                     for (int k = 0; k < Q[node].n; k++) {
                         float tn;
-                        if (slab(o, inv, N[Q[node].e[k]], best, tn)) hit[nh++] = {Q[node].e[k], tn};
+                        const bool h = quant ? slab6(o, inv, Q[node].qb[k], best, tn)
+                                             : slab(o, inv, N[Q[node].e[k]], best, tn);
+                        if (h) hit[nh++] = {Q[node].e[k], tn};
                     }
                     if (order == 0) {
                         std::stable_sort(hit, hit + nh, [](auto& a, auto& b) { return a.second < b.second; });
@@ -447,10 +501,11 @@ int main(int argc, char** argv) {
         for (int order = 0; order < 2; order++) {
             double sS, sV, sL;
             steps_walk(greedy, order, sS, sV, sL);
-            printf("{\"T\": %u, \"rays\": %zu, \"width\": %d, \"order\": \"%s\", \"steps\": %.4f, \"qnode_visits\": %.4f, "
-                   "\"leaf_tests\": %.4f, \"steps_past_13_20_32_entries\": [%.4f, %.4f, %.4f], \"pushes\": %.4f}\n", T, R, W,
-                   order ? "nearest, slot order" : "sorted", sS, sV, sL, (double)deep[0] / R, (double)deep[1] / R,
-                   (double)deep[2] / R, (double)deep[3] / R);
+            printf("{\"T\": %u, \"rays\": %zu, \"width\": %d, \"leafrun\": %d, \"quant\": %d, \"order\": \"%s\", "
+                   "\"steps\": %.4f, \"qnode_visits\": %.4f, \"leaf_tests\": %.4f, \"fetches\": %.4f, "
+                   "\"steps_past_13_20_32_entries\": [%.4f, %.4f, %.4f], \"pushes\": %.4f}\n", T, R, W, (int)leafrun,
+                   (int)quant, order ? "nearest, slot order" : "sorted", sS, sV, sL, sV + sL, (double)deep[0] / R,
+                   (double)deep[1] / R, (double)deep[2] / R, (double)deep[3] / R);
         }
         return 0;
     }
