@@ -726,19 +726,30 @@ def main():
         if world == 1 and not args.no_extras and args.workload == "c5":
             # C4: 10M synthetic (seed 0x5EED0004, +-50) build only; C3: Test.obj 1080p primary+1 bounce
             c4 = rt.synthetic(10_000_000, seed=0x5EED0004, half_extent=(50.0, 50.0, 50.0))
-            with rt.Context(device=local, flags=rt.FLAG_TIMING) as c:
-                c.set_scene(c4)
-                c.set_camera(*rt.camera_reference(1920, 1080))
-                c.build()
-                c.reset_stats()
-                for _ in range(args.build_iters):
-                    c.build(sync=False)
-                c.synchronize()
-                s4 = c.stats()
+
+            def c4_build(flags):
+                with rt.Context(device=local, flags=rt.FLAG_TIMING | flags) as c:
+                    c.set_scene(c4)
+                    c.set_camera(*rt.camera_reference(1920, 1080))
+                    c.build()
+                    c.reset_stats()
+                    for _ in range(args.build_iters):
+                        c.build(sync=False)
+                    c.synchronize()
+                    return c.stats()
+            # the drop-in's configuration (RTBVH_FLAG_AUTO_WALK: the certified walks at this size, whose build
+            # writes node boxes instead of node records), and the API's default (reference-order walks: records)
+            s4 = c4_build(rt.FLAG_AUTO_WALK)
+            s4d = c4_build(0)
             extras["c4_build"] = {"mtris_s": round(10_000_000 / (s4["ms_build"] * 1e-3) / 1e6, 1),
                                   "ms": round(s4["ms_build"], 4),
                                   "achieved_gbs": round(S_BUILD_PER_TRI * 1e7 / (s4["ms_build"] * 1e-3) / 1e9, 1),
-                                  "stages_ms": [round(x, 4) for x in s4["ms_stage"][:5]]}
+                                  "stages_ms": [round(x, 4) for x in s4["ms_stage"][:5]],
+                                  "flags": "RTBVH_FLAG_AUTO_WALK (the drop-in's: node boxes, no node records)",
+                                  "default_walks": {"ms": round(s4d["ms_build"], 4),
+                                                    "mtris_s": round(10_000_000 / (s4d["ms_build"] * 1e-3) / 1e6, 1),
+                                                    "stages_ms": [round(x, 4) for x in s4d["ms_stage"][:5]],
+                                                    "flags": "none (reference-order walks: node records)"}}
             del c4
             # C3 (Test.obj, primary + 1 bounce) and C2 (Image_Test.obj, primary only): the
             # reference rebuilds and traces every frame (Graphics.cpp:56), so build + trace

@@ -72,6 +72,12 @@ struct rtbvh_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
     bool pseudo_ok = false;      // the built tree has its leaf pseudo-records (read by the packet walks only)
+    // the built tree's node records (the binary and packet walks') and node boxes (a certified trace's
+    // reference-order re-traces): a certified-only context's build writes the boxes alone (records_skipped),
+    // any other build the records alone; the other form is derived on first use (ensure_records / ensure_nbox)
+    bool rec_ok = false, nbox_ok = false;
+    bool build_nbox = false;     // the last build wrote node boxes, not records
+    float* d_nbox = nullptr;     // [6 (T-1)] internal node boxes
     bool qnode_ok = false;       // the built tree has its QNodes (read by the 4-wide bounce walk only)
     // rtbvh_compute_bvh: the build leaves its crossing nodes (launch_refit_tail) to the frame's binned
     // pass, which runs them in its bin launches (launch_pb_bin_tail); any other first use of the tree
@@ -171,7 +177,7 @@ struct rtbvh_ctx {
     // tuning knobs of A/B runs, read once by rtbvh_create (RTBVH_BOUNCE_BLOCKS, RTBVH_OVERLAP,
     // RTBVH_SIDE_PRIORITY): a shipped context does not change its launches per frame
     uint32_t knob_bounce_blocks = 0;
-    bool knob_overlap = false, knob_side_priority = true;
+    bool knob_overlap = false, knob_side_priority = true, knob_keep_records = false;
     // the band deal of band traces (rtbvh_set_band_deal): rank 0's weight in 1/16 of another rank's
     uint32_t root_share = 16;
     struct DealTab {   // a weighted deal's device table: every rank's bands, then slots[b] = r << 24 | pos
@@ -241,6 +247,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_inner, ni));
     HIPC(c, dalloc(c->d_topo, ni));
     HIPC(c, dalloc(c->d_rec, 2 * (size_t)n - 1));
+    HIPC(c, dalloc(c->d_nbox, 6 * (size_t)ni));
     HIPC(c, dalloc(c->d_qnode, 2 * (size_t)n - 1));
     HIPC(c, dalloc(c->d_lfp, n));
     HIPC(c, dalloc(c->d_pleaf, n));
@@ -371,6 +378,15 @@ BuildArgs build_args(rtbvh_ctx* c) {
     const uint32_t f = c->cfg.flags;
     a.pseudo = (f & RTBVH_FLAG_PACKET_PRIMARY) &&
                !(f & (RTBVH_FLAG_BINNED_PRIMARY | RTBVH_FLAG_AUTO_WALK | RTBVH_FLAG_CERTIFIED));
+    // the last build's outputs: node records, or (a certified-only context's) node boxes instead
+    a.rec_on = c->build_nbox ? 0u : 1u;
+    a.nbox = c->build_nbox ? c->d_nbox : nullptr;
+    return a;
+}
+// the same, with the node-box array for a kernel that reads (or writes) it
+BuildArgs build_args_nbox(rtbvh_ctx* c) {
+    BuildArgs a = build_args(c);
+    a.nbox = c->d_nbox;
     return a;
 }
 
@@ -484,6 +500,9 @@ rtbvh_status get_deal(rtbvh_ctx* c, uint32_t H, uint32_t nranks, const rtbvh_ctx
 TraceArgs trace_args(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks, float4* color, float* inten) {
     TraceArgs a{};
     a.inner = c->d_rec;
+    a.topo = c->d_topo;
+    a.nbox = c->d_nbox;
+    a.nb = false;
     a.leaf = c->d_leaf;
     a.qnode = c->d_qnode;
     a.rootbox = c->d_rootbox;
@@ -531,6 +550,45 @@ constexpr uint32_t WALK_FLAGS = RTBVH_FLAG_NEAREST_FIRST | RTBVH_FLAG_PACKET_PRI
                                 RTBVH_FLAG_WIDE_BVH | RTBVH_FLAG_BINNED_PRIMARY;
 bool auto_checked(const rtbvh_ctx* c) {
     return (c->cfg.flags & RTBVH_FLAG_AUTO_WALK) && c->T > AUTO_WALK_MAX_TRIS;
+}
+// A certified-only context -- RTBVH_FLAG_CERTIFIED, or AUTO_WALK on a scene past AUTO_WALK_MAX_TRIS, on a clz64
+// tree with no stack limit (plan_trace) -- traces with walks that read no node record: the binned primary pass
+// (leaf footprints and records), the certified 4-wide bounce walk (QNodes; a node without a grid flags the ray),
+// and reference-order re-traces of the few flagged rays on the topology and node boxes (trace.hip traverse_nb).
+// Its multi-kernel build writes the 24-B node boxes instead of the 64-B node records (C4
+// refit stage 0.94 -> 0.81 ms without them); records are derived if another walk needs them (ensure_records).
+// RTBVH_KEEP_RECORDS=1 (A/B): write the records anyway.
+bool records_skipped(const rtbvh_ctx* c);
+rtbvh_status ensure_records(rtbvh_ctx* c, hipStream_t s) {
+    if (c->rec_ok || !c->built) return RTBVH_OK;
+    launch_records(build_args_nbox(c), c->stream);
+    HIPC(c, hipGetLastError());
+    c->rec_ok = true;
+    if (s != c->stream) {
+        if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
+        HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+    }
+    return RTBVH_OK;
+}
+bool records_skipped(const rtbvh_ctx* c) {
+    const uint32_t f = c->cfg.flags;
+    const bool limited = c->cfg.stack_limit != 0 && c->cfg.stack_limit < (uint32_t)STACK_SIZE;
+    const bool small = c->T <= small_build_max() && !(f & RTBVH_FLAG_MULTI_KERNEL_BUILD);   // (k_build_small: records)
+    return !small && !c->knob_keep_records && ((f & RTBVH_FLAG_CERTIFIED) || auto_checked(c)) &&
+           c->cfg.delta_mode == RTBVH_DELTA_CLZ64 && !limited;
+}
+rtbvh_status ensure_nbox(rtbvh_ctx* c, hipStream_t s) {
+    if (c->nbox_ok || !c->built) return RTBVH_OK;
+    BuildArgs a = build_args_nbox(c);
+    a.rec_on = 1;
+    launch_nbox(a, c->stream);
+    HIPC(c, hipGetLastError());
+    c->nbox_ok = true;
+    if (s != c->stream) {
+        if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
+        HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
+    }
+    return RTBVH_OK;
 }
 struct Walks {
     PrimaryKind primary;
@@ -723,7 +781,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
                                   ? (cert ? PrimaryKind::LANE_REFERENCE : PrimaryKind::PACKET_WIDE)
                                   : wk.primary;
     if (sort || my_bands < nsplit || slot || c->slots_used || binned) nsplit = 1;
-    const bool fuse_tail = tail.pending && pkind == PrimaryKind::BINNED && s == c->stream && slot == 0 && rows > 0;
+    // the walks' node data: a certified trace's re-traces walk the node boxes (a.nb), every other walk the node
+    // records; a build writes one of the two, the other is derived here from the complete tree (after the tail)
+    const bool need_conv = cert ? !c->nbox_ok : !c->rec_ok;
+    const bool fuse_tail = tail.pending && pkind == PrimaryKind::BINNED && s == c->stream && slot == 0 && rows > 0 &&
+                           !need_conv;
     if (!fuse_tail && tail.pending) {   // before any walk reads the tree
         tail.run();
         if (s != c->stream) {   // (a caller stream: ordered after it like after the build)
@@ -731,6 +793,11 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
         }
     }
+    if (need_conv) {
+        st = cert ? ensure_nbox(c, s) : ensure_records(c, s);
+        if (st) return st;
+    }
+    a.nb = cert;
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
@@ -1049,6 +1116,7 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
     if (const char* e = getenv("RTBVH_BOUNCE_BLOCKS")) c->knob_bounce_blocks = (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("RTBVH_OVERLAP")) c->knob_overlap = atoi(e) != 0;
     if (const char* e = getenv("RTBVH_SIDE_PRIORITY")) c->knob_side_priority = atoi(e) != 0;
+    if (const char* e = getenv("RTBVH_KEEP_RECORDS")) c->knob_keep_records = atoi(e) != 0;
     *out = c;
     return RTBVH_OK;
 }
@@ -1084,7 +1152,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     for (auto& p : c->pb) { dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_qnode); dfree(c->d_lfp);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_nbox); dfree(c->d_qnode); dfree(c->d_lfp);
     dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
@@ -1227,6 +1295,11 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         a.sorted_keys = c->d_ka;
         a.sorted_vals = c->d_va;
         a.pseudo = 1;   // (the one-workgroup build writes them anyway)
+        a.rec_on = 1;   // (and the node records)
+        a.nbox = nullptr;
+        c->build_nbox = false;
+        c->rec_ok = true;
+        c->nbox_ok = false;
         launch_build_small(a, s);
         // the QNodes only for walks that read them (the 4-wide bounce walk; enqueue_walks otherwise)
         c->qnode_ok = (c->cfg.flags & (RTBVH_FLAG_WIDE_BVH | RTBVH_FLAG_CERTIFIED)) != 0 || auto_checked(c);
@@ -1242,6 +1315,12 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
         return check_launch(c, "build kernel");
     }
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
+    // a certified-only context's build: node boxes instead of node records (records_skipped)
+    c->build_nbox = records_skipped(c);
+    c->rec_ok = !c->build_nbox;
+    c->nbox_ok = c->build_nbox;
+    a.rec_on = c->build_nbox ? 0u : 1u;
+    a.nbox = c->build_nbox ? c->d_nbox : nullptr;
     if (c->T <= small_sort_max() && !(c->cfg.flags & RTBVH_FLAG_MULTI_KERNEL_BUILD)) {
         // the Morton pass and the sort in one workgroup (build.hip k_morton_sort_small; stage "morton")
         c->sorted = SortResult{c->d_ka, c->d_va};
@@ -1700,6 +1779,8 @@ rtbvh_status rtbvh_read_wide(rtbvh_ctx* c, uint32_t* out, uint64_t capacity) {
     const size_t total = c->T > 1 ? 2 * (size_t)(c->T - 1) : 0;
     if (capacity < total) return fail(c, RTBVH_ERR_INVALID_ARG, "read_wide: capacity < 2(n-1)");
     HIPC(c, hipSetDevice(c->cfg.device));
+    rtbvh_status rs = ensure_records(c, c->stream);   // (a certified-only build wrote node boxes instead)
+    if (rs) return rs;
     if (!c->pseudo_ok) {   // a build that wrote no leaf pseudo-records (binned / AUTO walks): now
         launch_pseudo(build_args(c), c->stream);
         c->pseudo_ok = true;
@@ -1919,6 +2000,8 @@ rtbvh_status rtbvh_build_from_codes(rtbvh_ctx* c, const uint32_t* sorted_codes, 
     a.sorted_keys = c->d_ka;
     a.sorted_vals = nullptr;
     a.leaf = nullptr;
+    a.rec_on = 1;   // (its QNodes and export read the records)
+    a.nbox = nullptr;
     launch_from_codes(a, d_boxes, c->stream);
     launch_export(a, d_out, c->stream);
     st = check_launch(c, "build_from_codes kernels");
@@ -1929,6 +2012,8 @@ rtbvh_status rtbvh_build_from_codes(rtbvh_ctx* c, const uint32_t* sorted_codes, 
     if (st) return st;
     HIPC(c, e);
     c->built = false;   // the scene's BVH buffers were reused
+    c->build_nbox = false;
+    c->rec_ok = c->nbox_ok = false;
     return RTBVH_OK;
 }
 

@@ -440,17 +440,44 @@ __device__ __forceinline__ void store_leaf_record(Inner* rec, uint32_t p, uint32
     store_pseudo_record(rec + 2 * (size_t)p + side, leaf_id, lo, hi);
 }
 
+// The node boxes of a build without records (BuildArgs::nbox, rtbvh_internal.h): internal node k's box, min xyz
+// then max xyz, 24 B at nbox + 6 k (three 8-B stores: consecutive nodes' threads write consecutive bytes)
+__device__ __forceinline__ void st_nbox(float* nbox, uint32_t k, f3 lo, f3 hi) {
+    float2* d = reinterpret_cast<float2*>(nbox + 6 * (size_t)k);
+    d[0] = make_float2(lo.x, lo.y);
+    d[1] = make_float2(lo.z, hi.x);
+    d[2] = make_float2(hi.y, hi.z);
+}
+__device__ __forceinline__ void ld_nbox(const float* nbox, uint32_t k, float (&b)[6]) {
+    const float2* d = reinterpret_cast<const float2*>(nbox + 6 * (size_t)k);
+    const float2 x = d[0], y = d[1], z = d[2];
+    b[0] = x.x; b[1] = x.y; b[2] = y.x; b[3] = y.y; b[4] = z.x; b[5] = z.y;
+}
+// the box of child c (internal node, or LEAF_BIT | j: its leaf record's words 10..15)
+__device__ __forceinline__ void child_box(const BuildArgs& a, uint32_t c, float (&b)[6]) {
+    if (c & LEAF_BIT) {
+        const float4* r = a.leaf + 4 * (size_t)(c & ~LEAF_BIT);
+        const float4 w2 = r[2], w3 = r[3];
+        b[0] = w2.z; b[1] = w2.w; b[2] = w3.x; b[3] = w3.y; b[4] = w3.z; b[5] = w3.w;
+    } else {
+        ld_nbox(a.nbox, c, b);
+    }
+}
+
 // A node of the climb is complete: its record (both children's boxes) at its slot, the
 // pseudo-records of its leaf children; returns its box, the union in (childL, childR)
 // order as the reference's min(L.bbMin, R.bbMin).
 __device__ __forceinline__ void complete_node(const BuildArgs& a, uint32_t p, uint32_t e, f3 l0, f3 l1, f3 r0, f3 r1,
                                               f3& lo, f3& hi) {
     const uint4 ids = a.topo[p];
-    store_record(a.rec + slot_of(e, a.T), l0, l1, r0, r1, ids.x, ids.y, p);
-    if (a.pseudo && (ids.x & LEAF_BIT)) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
-    if (a.pseudo && (ids.y & LEAF_BIT)) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
+    if (a.rec_on) {
+        store_record(a.rec + slot_of(e, a.T), l0, l1, r0, r1, ids.x, ids.y, p);
+        if (a.pseudo && (ids.x & LEAF_BIT)) store_leaf_record(a.rec, p, 0, ids.x, l0, l1);
+        if (a.pseudo && (ids.y & LEAF_BIT)) store_leaf_record(a.rec, p, 1, ids.y, r0, r1);
+    }
     lo = vmin(l0, r0);
     hi = vmax(l1, r1);
+    if (a.nbox) st_nbox(a.nbox, p, lo, hi);
     if (e == INVALID) {
         a.rootbox[0] = lo.x; a.rootbox[1] = lo.y; a.rootbox[2] = lo.z;
         a.rootbox[3] = hi.x; a.rootbox[4] = hi.y; a.rootbox[5] = hi.z;
@@ -669,6 +696,16 @@ __device__ __forceinline__ void record_kids(const Inner* __restrict__ rec, uint3
     c0.b[0] = w0.x; c0.b[1] = w0.y; c0.b[2] = w2.x; c0.b[3] = w0.z; c0.b[4] = w0.w; c0.b[5] = w2.y;
     c1.b[0] = w1.x; c1.b[1] = w1.y; c1.b[2] = w2.z; c1.b[3] = w1.z; c1.b[4] = w1.w; c1.b[5] = w2.w;
 }
+// the same from the topology and the node boxes (a build without records): the children of internal node k
+__device__ __forceinline__ void nbox_kids(const BuildArgs& a, uint32_t k, QEnt& c0, QEnt& c1) {
+    const uint4 t = a.topo[k];
+    c0.id = t.x;
+    c1.id = t.y;
+    c0.slot = 2 * k;
+    c1.slot = 2 * k + 1;
+    child_box(a, t.x, c0.b);
+    child_box(a, t.y, c1.b);
+}
 // the QNode of the node whose record is at `slot`, from the records (crossing nodes, small builds);
 // E: the largest edge bound below it (node_edge); PSEUDO_NOGRID: a QNode without a grid gets its
 // node's leaf pseudo-records (the bounce walk reads that node's exact record pair, trace.hip
@@ -717,9 +754,49 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
     for_crossing(a, [&](uint32_t k) {
         const uint32_t slot = slot_of(a.pint[k], a.T);
         const float E = *node_edge(a, k);
-        if (a.pseudo) qnode_from_records<false>(a.rec, slot, E, a.qnode + slot);
-        else qnode_from_records<true>(a.rec, slot, E, a.qnode + slot);
+        if (!a.rec_on) {   // no records: the topology and the node boxes (no pseudo-records either)
+            QEnt e0, e1;
+            nbox_kids(a, k, e0, e1);
+            float4 w[4];
+            uint32_t ent[4];
+            greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { nbox_kids(a, e.id, c0, c1); }, E, w,
+                               ent);
+            store4(a.qnode + slot, w);
+        } else if (a.pseudo) {
+            qnode_from_records<false>(a.rec, slot, E, a.qnode + slot);
+        } else {
+            qnode_from_records<true>(a.rec, slot, E, a.qnode + slot);
+        }
     });
+}
+
+// The node records (rtbvh_device.h) of a build that wrote none (a certified-only context's, api.hip), on demand:
+// node k's at its slot from the topology and the node boxes, and the leaf pseudo-records of a node whose QNode
+// has no grid (the uncertified 4-wide walk reads that node's exact records) -- the words k_refit writes
+__global__ __launch_bounds__(BLOCK) void k_records(BuildArgs a) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k + 1 >= a.T) return;
+    const uint4 t = a.topo[k];
+    float l[6], r[6];
+    child_box(a, t.x, l);
+    child_box(a, t.y, r);
+    const f3 l0 = mk(l[0], l[1], l[2]), l1 = mk(l[3], l[4], l[5]), r0 = mk(r[0], r[1], r[2]), r1 = mk(r[3], r[4], r[5]);
+    const uint32_t slot = slot_of(a.pint[k], a.T);
+    store_record(a.rec + slot, l0, l1, r0, r1, t.x, t.y, k);
+    if (a.qnode && reinterpret_cast<const float4*>(a.qnode + slot)[0].w == 0.f) {
+        if (t.x & LEAF_BIT) store_leaf_record(a.rec, k, 0, t.x, l0, l1);
+        if (t.y & LEAF_BIT) store_leaf_record(a.rec, k, 1, t.y, r0, r1);
+    }
+}
+// ... and the node boxes of a build that wrote only records (from each node's record: its children's union)
+__global__ __launch_bounds__(BLOCK) void k_nbox(BuildArgs a) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k + 1 >= a.T) return;
+    const Inner* r = a.rec + slot_of(a.pint[k], a.T);
+    float l[6], q[6];
+    record_box(r, 0, l);
+    record_box(r, 1, q);
+    st_nbox(a.nbox, k, vmin(mk(l[0], l[1], l[2]), mk(q[0], q[1], q[2])), vmax(mk(l[3], l[4], l[5]), mk(q[3], q[4], q[5])));
 }
 
 // Refit (BVHConstructP2.hlsl:8-37) fused with the leaf records and the node outputs.  One
@@ -881,6 +958,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     r0 = mk(R[0], R[1], R[2]); r1 = mk(R[3], R[4], R[5]);
     slot = slot_of(s_pint[tid], T);
     record_words(l0, l1, r0, r1, q.x, q.y, i, rw);
+    if (a.nbox) st_nbox(a.nbox, i, vmin(l0, r0), vmax(l1, r1));   // (its own box; node-indexed: coalesced)
     // the QNode: its entries' boxes are in LDS (an in-block node's subtree is in the block)
     const auto lds_kids = [&](uint32_t x, QEnt& c0, QEnt& c1) {   // children of in-block node x
         const uint4 xq = s_topo[x - base];
@@ -967,12 +1045,13 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     const uint32_t w0 = 2 * base;
     const bool rin = mine && slot - w0 < 2 * RBLOCK;
     if (mine && !rin) {
-        store4(a.rec + slot, rw);
+        if (a.rec_on) store4(a.rec + slot, rw);
         if (rd) store4(a.qnode + slot, qw);
     }
     const uint32_t nslots = 2 * T - 1;
 #pragma unroll
-    for (uint32_t kind = 0; kind < 2; kind++) {   // 0: records and pseudo-records, 1: QNodes
+    for (uint32_t kind = 0; kind < 2; kind++) {   // 0: records and pseudo-records (unless none: a.rec_on), 1: QNodes
+        if (kind == 0 && !a.rec_on) continue;
         float4* dst = kind ? reinterpret_cast<float4*>(a.qnode) : reinterpret_cast<float4*>(a.rec);
 #pragma unroll 1
         for (uint32_t r = 0; r < 2 * RBLOCK; r += STAGE) {
@@ -1420,7 +1499,8 @@ __global__ __launch_bounds__(BLOCK) void k_export(BuildArgs a, RefNode* __restri
         for (int k = 0; k < 6; k++) box[k] = a.rootbox[k];
     } else {
         o.parent = (e >> 1) + T;
-        record_box(a.rec + slot_of(a.pint[e >> 1], T), e & 1u, box);   // from the parent's record
+        if (a.rec_on) record_box(a.rec + slot_of(a.pint[e >> 1], T), e & 1u, box);   // from the parent's record
+        else child_box(a, r < T ? LEAF_BIT | r : r - T, box);                          // (or the node boxes)
     }
     for (int k = 0; k < 3; k++) { o.bb_min[k] = box[k]; o.bb_max[k] = box[3 + k]; }
     out[r] = o;
@@ -1534,6 +1614,12 @@ void launch_pseudo(const BuildArgs& a, hipStream_t s) {
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     launch_refit_leaves(a, s);
     launch_refit_tail(a, s);
+}
+void launch_records(const BuildArgs& a, hipStream_t s) {
+    if (a.T > 1) hipLaunchKernelGGL(k_records, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a);
+}
+void launch_nbox(const BuildArgs& a, hipStream_t s) {
+    if (a.T > 1) hipLaunchKernelGGL(k_nbox, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a);
 }
 void launch_export(const BuildArgs& a, void* out, hipStream_t s) {
     hipLaunchKernelGGL(k_export, dim3(blocks_for(2 * (size_t)a.T - 1)), dim3(BLOCK), 0, s, a, (RefNode*)out);

@@ -74,6 +74,9 @@ struct BuildArgs {
     uint4* lfp;               // [T] leaf footprints on the primary pixel grid (rtbvh_device.h leaf_footprint)
     float* zpart;             // [ZPART * refit_blocks(T)] k_refit workgroup b's leaf depth range, edge bound
     uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
+    uint32_t rec_on;          // write the node records (rec; a certified-only context's build writes none: api.hip)
+    float* nbox;              // [6 (T-1)] or null: internal node k's box (min xyz, max xyz) -- what the certified
+                              //   walks' reference-order re-traces and the crossing nodes' QNodes read without records
 };
 void launch_bounds(const BuildArgs& a, hipStream_t s);
 void launch_morton(const BuildArgs& a, hipStream_t s);
@@ -99,6 +102,10 @@ void launch_build_small(const BuildArgs& a, hipStream_t s);
 // a.sorted_keys / a.sorted_vals, which must be writable); the multi-kernel build's later stages follow
 uint32_t small_sort_max();
 void launch_morton_sort_small(const BuildArgs& a, hipStream_t s);
+// the node records from the topology and the node boxes (a build that wrote none), and the node boxes from the
+// records (one that wrote only records)
+void launch_records(const BuildArgs& a, hipStream_t s);
+void launch_nbox(const BuildArgs& a, hipStream_t s);
 // reference-layout export (44-B Node), 2T-1 entries
 void launch_export(const BuildArgs& a, void* out_nodes, hipStream_t s);
 // Karras + refit from given sorted codes and leaf boxes (n x 6 floats, device)
@@ -107,6 +114,11 @@ void launch_from_codes(const BuildArgs& a, const float* leaf_boxes, hipStream_t 
 // ---- trace (trace.hip) ------------------------------------------------------
 struct TraceArgs {
     const Inner* inner;       // node records in slots (BuildArgs::rec); the 4-wide walks read the same array
+    // a certified trace's reference-order re-traces walk the topology and the node boxes instead (the context's
+    // build may have written no records): nb set, topo = BuildArgs::topo, nbox = BuildArgs::nbox
+    const uint4* topo;
+    const float* nbox;
+    bool nb;
     const float4* leaf;       // [4T] sorted leaf records (see build.hip)
     const float4* tclip;      // [3T] clip-space triangles in triangle order (hit shading)
     const float* verts;       // rtbvh_vertex AoS, 8 floats each

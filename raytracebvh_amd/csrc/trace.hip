@@ -179,6 +179,92 @@ __device__ __forceinline__ bool traverse(const Inner* __restrict__ inner, const 
     return hit;
 }
 
+// traverse<COUNT, false> (findCollision, the reference order) on the topology and the node boxes, for a build that
+// wrote no node records (api.hip: a certified-only context's): at internal node k its children from topo[k], their
+// boxes from nbox (internal) or the leaf record (words 10..15), the same slab test in the same operations -- the same
+// visits, in the same order, and the same hit.  Two dependent fetches a step instead of one: the certified walks'
+// few re-traced rays only.
+__device__ __forceinline__ void nb_child_box(const float* __restrict__ nbox, const float4* __restrict__ leaf, uint32_t c,
+                                             f2v& mnxy, f2v& mxxy, float& mnz, float& mxz) {
+    if (c & LEAF_BIT) {
+        const float4* r = leaf + 4 * (size_t)(c & ~LEAF_BIT);
+        const float4 w2 = r[2], w3 = r[3];
+        mnxy = f2v{w2.z, w2.w}; mnz = w3.x; mxxy = f2v{w3.y, w3.z}; mxz = w3.w;
+    } else {
+        const float2* d = reinterpret_cast<const float2*>(nbox + 6 * (size_t)c);
+        const float2 x = d[0], y = d[1], z = d[2];
+        mnxy = f2v{x.x, x.y}; mnz = y.x; mxxy = f2v{y.y, z.x}; mxz = z.y;
+    }
+}
+template <bool COUNT>
+__device__ __forceinline__ bool traverse_nb(const uint4* __restrict__ topo, const float* __restrict__ nbox,
+                                            const float4* __restrict__ leaf, uint32_t T, f3 o, f3 d, f3 inv,
+                                            float& best, uint32_t& best_leaf, Counts& c) {
+    bool hit = false;
+    best = 0.f;
+    best_leaf = 0;
+    uint32_t stack[STACK_SIZE];
+    int sp = 0;
+    uint32_t top = INVALID;
+    uint32_t node = T > 1 ? 0u : LEAF_BIT;   // the root: internal node 0 (a one-leaf tree: the leaf)
+    uint32_t guard = 2 * T + 2;
+    do {
+        if (--guard == 0) { c.overflow++; break; }
+        if (node & LEAF_BIT) {
+            const uint32_t j = node & ~LEAF_BIT;
+            const float4* r = leaf + 4 * (size_t)j;
+            float4 a = r[0], b = r[1];
+            float e2z = r[2].x;
+            pin(a); pin(b); pin(e2z);
+            if (COUNT) c.leaf++;
+            const float t = ray_triangle(o, d, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, e2z));
+            if (t != -1.f && (!hit || t < best)) {
+                best = t;
+                best_leaf = j;
+                hit = true;
+            }
+            node = top;
+            if (--sp >= 0) top = stack[sp];
+            continue;
+        }
+        if (COUNT) c.internal++;
+        const uint4 q = topo[node];
+        const uint32_t cl = q.x, cr = q.y;
+        f2v lmn, lmx, rmn, rmx;
+        float lz0, lz1, rz0, rz1;
+        nb_child_box(nbox, leaf, cl, lmn, lmx, lz0, lz1);
+        nb_child_box(nbox, leaf, cr, rmn, rmx, rz0, rz1);
+        float tl, tr;
+        const bool lh = ray_box_xy(o, inv, lmn, lmx, lz0, lz1, hit, best, tl);
+        const bool rh = ray_box_xy(o, inv, rmn, rmx, rz0, rz1, hit, best, tr);
+        if (!lh && !rh) {
+            node = top;
+            if (--sp >= 0) top = stack[sp];
+        } else {
+            if (lh && rh) {
+                if (sp + 1 >= STACK_SIZE) {
+                    c.overflow++;
+                    node = top;
+                    if (--sp >= 0) top = stack[sp];
+                    continue;
+                }
+                stack[sp] = top;
+                sp++;
+                top = cr;
+            }
+            node = lh ? cl : cr;
+        }
+    } while (sp != -1);
+    return hit;
+}
+// the reference-order walk of a re-traced ray: on the records, or (a.nb) the topology and node boxes
+template <bool COUNT>
+__device__ __forceinline__ bool traverse_ref(const TraceArgs& a, f3 o, f3 d, f3 inv, float& best, uint32_t& bl,
+                                             Counts& c) {
+    return a.nb ? traverse_nb<COUNT>(a.topo, a.nbox, a.leaf, a.T, o, d, inv, best, bl, c)
+                : traverse<COUNT, false>(a.inner, a.leaf, a.T, o, d, inv, STACK_SIZE, best, bl, c);
+}
+
 // ---- wave-packet traversal (primary rays) -------------------------------------
 // The 64 rays of an 8x8 pixel tile are nearly parallel neighbours, so a wave walks
 // ONE node at a time with a per-node lane mask: the node record is fetched by the
@@ -519,11 +605,14 @@ __device__ __forceinline__ bool traverse_packet4(const Inner* __restrict__ inner
 // Primary walks: 0 per-lane reference order, 1 per-lane nearest-first,
 // 2 packet reference order, 3 packet nearest-first, 4 4-wide packet (axis-parallel test),
 // 5 the same without the walk-length guard (a clz64 tree has no cycles; ~6 SALU per step)
+// 6: the reference order per lane on the topology and the node boxes (a certified trace's overflowed tiles and
+// frames past the binned pass's size, on a build without node records: traverse_nb)
 template <int K> struct PrimaryWalk {
     static constexpr bool NEAREST = (K == 1 || K == 3);
-    static constexpr bool PACKET = (K >= 2);
-    static constexpr bool WIDE = (K >= 4);
+    static constexpr bool PACKET = (K >= 2 && K <= 5);
+    static constexpr bool WIDE = (K == 4 || K == 5);
     static constexpr bool GUARD = (K != 5);   // 5: the 4-wide walk on a clz64 tree (acyclic)
+    static constexpr bool NB = (K == 6);
 };
 
 struct HitInfo {
@@ -756,7 +845,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
     const int lim = LIM ? a.stack_limit : STACK_SIZE, lim4 = LIM ? a.stack_limit4 : STACK4;
     constexpr int PST = PW::WIDE ? 3 * (STACK4 + 1) : 3 * STACK_SIZE;   // per-wave packet stack words (+ sentinel)
     __shared__ uint32_t s_pst[PW::PACKET ? 4 * PST : 1];
-    __shared__ uint32_t s_lst[PW::PACKET || LANE_LSB == 0 ? 1 : LANE_LSB * BLOCK];
+    __shared__ uint32_t s_lst[PW::PACKET || PW::NB || LANE_LSB == 0 ? 1 : LANE_LSB * BLOCK];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + w * 8 + (lane & 7);
     const uint32_t k = a.band0 + blockIdx.y * a.bstep;   // the rank's k-th band
@@ -785,6 +874,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_primary(TraceArgs a, RayQ* __restr
                                                    s_pst + w * PST);
     if (valid) {
         const bool h = PW::PACKET ? phit
+                       : PW::NB   ? traverse_nb<COUNT>(a.topo, a.nbox, a.leaf, a.T, o, d, inv, best, bl, c)
                                   : traverse<COUNT, PW::NEAREST, PW::PACKET ? 0 : LANE_LSB>(a.inner, a.leaf, a.T, o, d, inv, lim,
                                                                                            best, bl, c, s_lst + threadIdx.x);
         live = primary_pixel(a, out, o, d, h, best, bl, hits, tex, e);
@@ -1266,7 +1356,7 @@ __global__ __launch_bounds__(BLOCK) void k_primary_redo(TraceArgs a, const uint3
             const f3 o = mk(((float)x - hw) / 4.f, ((float)pb_image_row(a, crow) - hh) / 4.f, 0.f);
             float best;
             uint32_t bl, h1 = 0, t1 = 0;
-            const bool h = traverse<COUNT, false>(a.inner, a.leaf, a.T, o, d, inv, STACK_SIZE, best, bl, c);
+            const bool h = traverse_ref<COUNT>(a, o, d, inv, best, bl, c);
             live = primary_pixel(a, p, o, d, h, best, bl, h1, t1, e);
             hits += h1;
             tex += t1;
@@ -1498,14 +1588,16 @@ __device__ __forceinline__ bool qbox_fast_cert(const QAxis& x, const QAxis& y, c
 #endif
 // a deferred ray's reference-order walk: its hit record, "exact" (t negated; a miss -inf with id INVALID)
 template <bool COUNT>
-__device__ __forceinline__ float2 defer_walk(const Inner* __restrict__ inner, const float4* __restrict__ leaf,
+__device__ __forceinline__ float2 defer_walk(const Inner* __restrict__ inner, const uint4* __restrict__ topo,
+                                             const float* __restrict__ nbox, const float4* __restrict__ leaf,
                                              uint32_t T, const RayQ* e, Counts& c) {
     const float4 q0 = reinterpret_cast<const float4*>(e)[0], q1 = reinterpret_cast<const float4*>(e)[1];
     const f3 o = mk(q0.z, q0.w, q1.x), d = mk(q1.y, q1.z, q1.w);
     const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
     float best;
     uint32_t bl;
-    const bool h = traverse<COUNT, false>(inner, leaf, T, o, d, inv, STACK_SIZE, best, bl, c);
+    const bool h = nbox ? traverse_nb<COUNT>(topo, nbox, leaf, T, o, d, inv, best, bl, c)
+                        : traverse<COUNT, false>(inner, leaf, T, o, d, inv, STACK_SIZE, best, bl, c);
     const uint32_t tri = h ? __float_as_uint(leaf[4 * (size_t)bl + 2].y) & ~LEAF_BIT : INVALID;
     return make_float2(h ? -best : -__builtin_inff(), __uint_as_float(tri));
 }
@@ -1514,7 +1606,8 @@ __device__ __forceinline__ float2 defer_walk(const Inner* __restrict__ inner, co
 // until the list holds none it has not taken
 template <bool COUNT>
 __device__ __forceinline__ void defer_walk_all(uint32_t* __restrict__ next, uint32_t* __restrict__ defer,
-                                               const Inner* __restrict__ inner, const float4* __restrict__ leaf,
+                                               const Inner* __restrict__ inner, const uint4* __restrict__ topo,
+                                               const float* __restrict__ nbox, const float4* __restrict__ leaf,
                                                uint32_t T, const RayQ* __restrict__ qin, float2* __restrict__ hitrec,
                                                Counts& c) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1544,7 +1637,7 @@ __device__ __forceinline__ void defer_walk_all(uint32_t* __restrict__ next, uint
                 e = __hip_atomic_load(defer + base + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             } while (!(e & DEFER_VALID));
             defer[base + lane] = 0u;   // (the list is clean for the next pass)
-            hitrec[e & ~DEFER_VALID] = defer_walk<COUNT>(inner, leaf, T, qin + (e & ~DEFER_VALID), c);
+            hitrec[e & ~DEFER_VALID] = defer_walk<COUNT>(inner, topo, nbox, leaf, T, qin + (e & ~DEFER_VALID), c);
         }
     }
 }
@@ -1566,7 +1659,8 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           float2* __restrict__ hitrec, uint32_t* __restrict__ next,
                                                           unsigned long long* __restrict__ counters,
                                                           unsigned long long* __restrict__ overflow, int stack_limit,
-                                                          uint32_t* __restrict__ defer) {
+                                                          uint32_t* __restrict__ defer, const uint4* __restrict__ topo,
+                                                          const float* __restrict__ nbox) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
@@ -1576,7 +1670,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     Counts c = {0, 0, 0, 0, 0};
     if (CERT && DEFER_WORKERS && blockIdx.x < DEFER_WORKERS && gridDim.x > 2 * DEFER_WORKERS && threadIdx.x < 64) {
         for (;;) {
-            defer_walk_all<COUNT>(next, defer, inner, leaf, T, qin, hitrec, c);
+            defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c);
             // every segment claimed (lane k: segment k's counter past its length): no ray left to defer but
             // those being claimed right now
             bool used = true;
@@ -1588,7 +1682,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
             if (__ballot(!used) == 0) break;
             __builtin_amdgcn_s_sleep(64);
         }
-        defer_walk_all<COUNT>(next, defer, inner, leaf, T, qin, hitrec, c);
+        defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c);
         if (COUNT) {
             unsigned long long v[2] = {c.internal, c.leaf};
 #pragma unroll
@@ -1937,7 +2031,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
         // of the queue is drained, the wave walks them in the reference order; the hit record says "exact" (t
         // negated), so k_bounce_shade shades it without a certificate.  A deferred ray no wave takes here
         // (appended after the waves looked) is re-traced by k_bounce_redo.
-        defer_walk_all<COUNT>(next, defer, inner, leaf, T, qin, hitrec, c);
+        defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c);
     }
     if (COUNT || __ballot(c.overflow != 0)) {
         unsigned long long v[3] = {c.internal, c.leaf, c.overflow};
@@ -2092,7 +2186,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_redo(TraceArgs a, const RayQ* 
             const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
             float best;
             uint32_t bl;
-            const bool h = traverse<COUNT, false>(a.inner, a.leaf, a.T, o, d, inv, STACK_SIZE, best, bl, c);
+            const bool h = traverse_ref<COUNT>(a, o, d, inv, best, bl, c);
             const uint32_t tri = h ? __float_as_uint(a.leaf[4 * (size_t)bl + 2].y) & ~LEAF_BIT : INVALID;
             uint32_t h1 = 0, t1 = 0;
             live = bounce_apply(a, e, tri, best, h1, t1);
@@ -2205,7 +2299,8 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
 #define RTBVH_BT(L, G, C)                                                                                              \
     hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
-                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, defer)
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, defer, a.topo,            \
+                       a.nb ? a.nbox : nullptr)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
     if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
@@ -2232,7 +2327,10 @@ void launch_primary(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count, b
             if (a.acyclic) launch_primary_c<5>(a, q, qcount, count, emit, grid, s);
             else launch_primary_c<4>(a, q, qcount, count, emit, grid, s);
             break;
-        default: launch_primary_c<0>(a, q, qcount, count, emit, grid, s); break;
+        default:   // LANE_REFERENCE: on the topology and node boxes when the trace says so (a certified one)
+            if (a.nb) launch_primary_c<6>(a, q, qcount, count, emit, grid, s);
+            else launch_primary_c<0>(a, q, qcount, count, emit, grid, s);
+            break;
     }
 }
 
