@@ -78,7 +78,6 @@ struct rtbvh_ctx {
     bool rec_ok = false, nbox_ok = false;
     bool build_nbox = false;     // the last build wrote node boxes, not records
     float* d_nbox = nullptr;     // [6 (T-1)] internal node boxes
-    uint32_t* d_gover = nullptr; // BuildArgs::gover
     bool qnode_ok = false;       // the built tree has its QNodes (read by the 4-wide bounce walk only)
     // rtbvh_compute_bvh: the build leaves its crossing nodes (launch_refit_tail) to the frame's binned
     // pass, which runs them in its bin launches (launch_pb_bin_tail); any other first use of the tree
@@ -256,7 +255,6 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_cnt, ni));
     HIPC(c, dalloc(c->d_xlist, n));
     HIPC(c, dalloc(c->d_xcnt, refit_blocks(T)));
-    HIPC(c, dalloc(c->d_gover, refit_blocks(T) / 64 + 1));
     HIPC(c, dalloc(c->d_zpart, ZPART * (size_t)refit_blocks(T)));
     HIPC(c, dalloc(c->d_bounds, BOUNDS_WORDS));
     HIPC(c, dalloc(c->d_rootbox, ROOTBOX_WORDS));
@@ -383,7 +381,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     // the last build's outputs: node records, or (a certified-only context's) node boxes instead
     a.rec_on = c->build_nbox ? 0u : 1u;
     a.nbox = c->build_nbox ? c->d_nbox : nullptr;
-    a.gover = c->knob_flat_climb ? nullptr : c->d_gover;
+    a.flat_climb = c->knob_flat_climb ? 1u : 0u;
     return a;
 }
 // the same, with the node-box array for a kernel that reads (or writes) it
@@ -1158,7 +1156,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_nbox); dfree(c->d_qnode); dfree(c->d_lfp);
     dfree(c->d_band);
-    dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_gover); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
+    dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
     dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);

@@ -1090,35 +1090,10 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
 // subtree).  Node k's thread: both children non-crossing -> k is complete, climb from it; one
 // -> arrive at k's ticket for that child (the other arrives by a climb); none -> nothing.  A
 // separate launch, so that k_refit's workgroups never wait on the global climb's latency.
-// ---- the crossing nodes in two phases (launch_refit_tail) -------------------------------------------
-// A group is RGROUP consecutive refit workgroups (GSPAN node indices); a crossing node whose leaf range lies inside
-// its group's span is "group-internal".  k_refit_group (one workgroup per group) joins the group-internal ones in
-// LDS -- the climb k_refit_top would make through device-scope tickets, level by level, becomes LDS atomics -- and
-// hands the boxes of the group's top nodes to their parents (inner[], as k_refit does); k_refit_top<true> then
-// climbs only the nodes that cross their group (C5: 4.6K of the 181K crossing nodes), a handful of levels.  A
-// group with more than GCAP crossing nodes (a degenerate tree) leaves them all to the climb (gover[g] = 1).
-constexpr uint32_t RGROUP = 64;
-constexpr uint32_t GSPAN = RGROUP * RBLOCK;
-static_assert((GSPAN & (GSPAN - 1)) == 0, "the group span is a power of two");
-constexpr uint32_t GCAP = 1024;
-constexpr uint32_t GBLOCK = 1024;
-__device__ __forceinline__ bool group_internal(uint4 topo_k, uint32_t k) {
-    const uint32_t gb = k & ~(GSPAN - 1);
-    return topo_k.z >= gb && topo_k.w < gb + GSPAN;
-}
-// a child whose box waits in its parent's hand-off (inner[]) once k_refit_group has run: a leaf, a node k_refit
-// joined, or a group-internal crossing node of a group that fit in LDS
-__device__ __forceinline__ bool child_done(const BuildArgs& a, uint32_t c) {
-    if (c & LEAF_BIT) return true;
-    const uint4 t = a.topo[c];
-    return !crossing(t, c) || (group_internal(t, c) && a.gover[c / GSPAN] == 0);
-}
-// GROUPED: after k_refit_group (children done per child_done; only the nodes that cross their group come here)
-template <bool GROUPED = false>
 __device__ __forceinline__ void refit_top_node(const BuildArgs& a, uint32_t k) {
     const uint4 q = a.topo[k];
-    const bool ncl = GROUPED ? child_done(a, q.x) : (q.x & LEAF_BIT) || !crossing(a.topo[q.x], q.x);
-    const bool ncr = GROUPED ? child_done(a, q.y) : (q.y & LEAF_BIT) || !crossing(a.topo[q.y], q.y);
+    const bool ncl = (q.x & LEAF_BIT) || !crossing(a.topo[q.x], q.x);
+    const bool ncr = (q.y & LEAF_BIT) || !crossing(a.topo[q.y], q.y);
     if (!ncl && !ncr) return;
     const float* L = a.inner[k].lmin;
     const float* R = a.inner[k].rmin;
@@ -1147,22 +1122,38 @@ __device__ __forceinline__ void refit_top_node(const BuildArgs& a, uint32_t k) {
     }
     refit_climb(lo, hi, em, e, a);
 }
-template <bool GROUPED>
 __global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
-    for_crossing(a, [&](uint32_t k) {
-        if (GROUPED && group_internal(a.topo[k], k) && a.gover[k / GSPAN] == 0) return;   // (k_refit_group's)
-        refit_top_node<GROUPED>(a, k);
-    });
+    for_crossing(a, [&](uint32_t k) { refit_top_node(a, k); });
 }
 
+// ---- the crossing nodes, grouped (launch_refit_tail) ---------------------------------------------------
+// k_refit_top's climb makes one device-scope round trip (sc1 box hand-off, ticket atomic) per level of crossing
+// nodes, ~25 levels at C5.  A group is RGROUP consecutive refit workgroups (GSPAN node indices), and a crossing
+// node whose leaf range lies inside its group's span is "group-internal" (C5: 176K of the 181K).  k_refit_group,
+// one workgroup per group, climbs the group-internal ones in LDS (slots by node index through a bitmap rank; the
+// same union order and bounds as k_refit_top), and where a climb leaves the group -- its parent crosses the group
+// -- it continues with k_refit_top's global protocol (refit_climb); the group's other crossing nodes start it as
+// k_refit_top's threads do.  The protocol's tickets take arrivals in any order, so the global climb above the
+// groups is the same, a handful of levels.  A group with more than GCAP crossing nodes (a degenerate tree) runs
+// k_refit_top's protocol for all of them.
+constexpr uint32_t RGROUP = 64;
+constexpr uint32_t GSPAN = RGROUP * RBLOCK;
+static_assert((GSPAN & (GSPAN - 1)) == 0, "the group span is a power of two");
+constexpr uint32_t GCAP = 1024;
+constexpr uint32_t GBLOCK = 1024;
+__device__ __forceinline__ bool group_internal(uint4 topo_k, uint32_t k) {
+    const uint32_t gb = k & ~(GSPAN - 1);
+    return topo_k.z >= gb && topo_k.w < gb + GSPAN;
+}
 __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
     __shared__ uint32_t s_bits[GSPAN / 32];   // the group's crossing nodes, by index
     __shared__ uint32_t s_pre[GSPAN / 32];    // their rank before each word: slot(k) = s_pre[w] + popc(bits below k)
     __shared__ uint32_t s_off[RGROUP + 1];
     __shared__ uint32_t s_sid[GCAP];          // slot -> node
+    __shared__ uint32_t s_par[GCAP];          // the node's parent link (pint)
     __shared__ float s_gbox[GCAP][2][6];
     __shared__ float s_ge[GCAP][2];
-    __shared__ uint32_t s_tk[GCAP];           // children joined (3: not group-internal, never completed here)
+    __shared__ uint32_t s_tk[GCAP];           // children in (3: not group-internal, k_refit_top's protocol)
     __shared__ uint32_t s_wsum[GBLOCK / 64];
     const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t nb = (a.T + RBLOCK - 1) / RBLOCK;
@@ -1183,20 +1174,20 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
     for (uint32_t w = tid; w < GSPAN / 32; w += GBLOCK) s_bits[w] = 0;
     __syncthreads();
     const uint32_t m = s_off[nbg];
-    if (m > GCAP) {   // (uniform) all to the global climb
-        if (tid == 0) a.gover[g] = 1;
-        return;
-    }
-    if (tid == 0) a.gover[g] = 0;
     const auto entry = [&](uint32_t e) {   // the e-th crossing node of the group (list order)
         uint32_t j = 0;
         for (uint32_t st = 32; st; st >>= 1)
             if (j + st <= nbg - 1 && s_off[j + st] <= e) j += st;
         return a.xlist[(size_t)(b0 + j) * RBLOCK + (e - s_off[j])];
     };
-    for (uint32_t e = tid; e < m; e += GBLOCK) {
-        const uint32_t k = entry(e) - gbase;
-        atomicOr(&s_bits[k >> 5], 1u << (k & 31));
+    if (m > GCAP) {   // (uniform) k_refit_top's protocol for every crossing node of the group
+        for (uint32_t e = tid; e < m; e += GBLOCK) refit_top_node(a, entry(e));
+        return;
+    }
+    uint32_t k0 = 0;
+    if (tid < m) {
+        k0 = entry(tid);
+        atomicOr(&s_bits[(k0 - gbase) >> 5], 1u << ((k0 - gbase) & 31));
     }
     __syncthreads();
     {   // the word ranks: an exclusive scan of the words' popcounts (GSPAN / 32 = GBLOCK words, one a thread)
@@ -1223,34 +1214,38 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
         const uint32_t r = k - gbase;
         return r < GSPAN && ((s_bits[r >> 5] >> (r & 31)) & 1u);
     };
-    // each node: its children, and the boxes k_refit handed over (leaves and the subtrees it joined)
-    for (uint32_t e = tid; e < m; e += GBLOCK) {
-        const uint32_t k = entry(e), sl = slot_of_k(k);
-        const uint4 t = a.topo[k];
-        s_sid[sl] = k;
+    // each node: its parent link, and the boxes k_refit handed over (leaves and the subtrees it joined)
+    static_assert(GCAP == GBLOCK, "one slot per thread");
+    bool outside = false;   // this thread's node crosses its group: k_refit_top's protocol
+    if (tid < m) {
+        const uint32_t sl = slot_of_k(k0);
+        const uint4 t = a.topo[k0];
+        s_sid[sl] = k0;
+        s_par[sl] = a.pint[k0];
         uint32_t ready = 3;
-        if (group_internal(t, k)) {
+        if (group_internal(t, k0)) {
             ready = 0;
 #pragma unroll
             for (uint32_t side = 0; side < 2; side++) {
                 const uint32_t c = side ? t.y : t.x;
                 if ((c & LEAF_BIT) || !crossing(a.topo[c], c)) {
-                    const float* hb = side ? a.inner[k].rmin : a.inner[k].lmin;
+                    const float* hb = side ? a.inner[k0].rmin : a.inner[k0].lmin;
 #pragma unroll
                     for (int q = 0; q < 6; q++) s_gbox[sl][side][q] = hb[q];
-                    s_ge[sl][side] = *hand_edge(a, k, side);
+                    s_ge[sl][side] = *hand_edge(a, k0, side);
                     ++ready;
                 }
             }
+        } else {
+            outside = true;
         }
         s_tk[sl] = ready;
     }
     __syncthreads();
-    // the climbs, from every group-internal node whose two children are in (k_refit_top's protocol on LDS)
-    // (the starting nodes are read before any climb raises a ticket: GCAP == GBLOCK, a slot per thread)
-    static_assert(GCAP == GBLOCK, "one slot per thread");
+    // the starting nodes, read before any climb raises a ticket (a slot per thread)
     const bool start = tid < m && s_tk[tid] == 2;
     __syncthreads();
+    if (outside) refit_top_node(a, k0);
     if (start) {
         uint32_t sl = tid;
         for (int level = 0; level < 2 * STACK_SIZE; level++) {   // (bounded: a CPUTests-delta tree may cycle)
@@ -1259,7 +1254,7 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
             const float* R = s_gbox[sl][1];
             const float em = fmaxf(s_ge[sl][0], s_ge[sl][1]);
             *node_edge(a, k) = em;   // (read by k_qnodes_cross, a later launch)
-            const uint32_t e = a.pint[k];
+            const uint32_t e = s_par[sl];
             f3 lo, hi;
             complete_node(a, k, e, mk(L[0], L[1], L[2]), mk(L[3], L[4], L[5]), mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]),
                           lo, hi);
@@ -1275,10 +1270,8 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
                 if (old != 1) break;   // the sibling is still to come
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 sl = sp;
-            } else {   // the parent crosses the group: its hand-off, as k_refit's (k_refit_top<true> follows)
-                float* hb = side ? a.inner[p].rmin : a.inner[p].lmin;
-                hb[0] = lo.x; hb[1] = lo.y; hb[2] = lo.z; hb[3] = hi.x; hb[4] = hi.y; hb[5] = hi.z;
-                *hand_edge(a, p, side) = em;
+            } else {   // the parent crosses the group: k_refit_top's global climb from here
+                refit_climb(lo, hi, em, e, a);
                 break;
             }
         }
@@ -1295,7 +1288,7 @@ __global__ __launch_bounds__(BLOCK) void k_pb_count_top(BuildArgs b, TraceArgs a
                                                         uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
                                                         uint4* __restrict__ bins, uint32_t cap, uint32_t ntx) {
     if (blockIdx.x < ntail) {
-        for_crossing(b, [&](uint32_t k) { refit_top_node<false>(b, k); }, blockIdx.x);
+        for_crossing(b, [&](uint32_t k) { refit_top_node(b, k); }, blockIdx.x);
         return;
     }
     pb_bin_block<false>(a, blockIdx.x - ntail, off, cur, bins, cap, ntx);
@@ -1754,13 +1747,9 @@ void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, 
 }
 void launch_refit_tail(const BuildArgs& a, hipStream_t s) {
     const uint32_t nb = refit_blocks(a.T);
-    if (a.T > RBLOCK) {   // the crossing nodes: climbed (in LDS per group, then across groups), then quantized
-        if (a.gover) {
-            hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, a);
-            hipLaunchKernelGGL(k_refit_top<true>, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
-        } else {
-            hipLaunchKernelGGL(k_refit_top<false>, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
-        }
+    if (a.T > RBLOCK) {   // the crossing nodes: climbed (in LDS within a group, then across), then quantized
+        if (a.flat_climb) hipLaunchKernelGGL(k_refit_top, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
+        else hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, a);
         hipLaunchKernelGGL(k_qnodes_cross, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
     }
 }

@@ -75,8 +75,7 @@ struct BuildArgs {
     float* zpart;             // [ZPART * refit_blocks(T)] k_refit workgroup b's leaf depth range, edge bound
     uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
     uint32_t rec_on;          // write the node records (rec; a certified-only context's build writes none: api.hip)
-    uint32_t* gover;          // [refit_blocks(T) / 64 + 1] or null: launch_refit_tail's groups that left their crossing
-                              //   nodes to the global climb (build.hip k_refit_group); null: one global climb
+    uint32_t flat_climb;      // launch_refit_tail: k_refit_top's one global climb instead of k_refit_group's (A/B)
     float* nbox;              // [6 (T-1)] or null: internal node k's box (min xyz, max xyz) -- what the certified
                               //   walks' reference-order re-traces and the crossing nodes' QNodes read without records
 };
