@@ -59,6 +59,7 @@ struct rtbvh_ctx {
     size_t cap_rec = 0, rec_P = 0;           // record capacity; pixels of the last records trace
     uint32_t *d_pleaf = nullptr, *d_pint = nullptr, *d_cnt = nullptr;
     uint32_t *d_xlist = nullptr, *d_xcnt = nullptr;   // refit: crossing nodes per workgroup
+    uint32_t* d_qlate = nullptr;                        // BuildArgs::qlate
     unsigned long long* d_ovf = nullptr;     // stack overflows + guard trips of every trace (never reset)
     unsigned long long* h_ovf = nullptr;     // pinned: a snapshot of *d_ovf copied at the end of each trace,
                                              //   one word per slot; ovf_seen: the value last reported
@@ -254,6 +255,7 @@ rtbvh_status ensure_build_capacity(rtbvh_ctx* c, uint32_t T) {
     HIPC(c, dalloc(c->d_pint, ni));
     HIPC(c, dalloc(c->d_cnt, ni));
     HIPC(c, dalloc(c->d_xlist, n));
+    HIPC(c, dalloc(c->d_qlate, n + 1));
     HIPC(c, dalloc(c->d_xcnt, refit_blocks(T)));
     HIPC(c, dalloc(c->d_zpart, ZPART * (size_t)refit_blocks(T)));
     HIPC(c, dalloc(c->d_bounds, BOUNDS_WORDS));
@@ -367,6 +369,7 @@ BuildArgs build_args(rtbvh_ctx* c) {
     a.pint = c->d_pint;
     a.refit_cnt = c->d_cnt;
     a.xlist = c->d_xlist;
+    a.qlate = c->d_qlate;
     a.xcnt = c->d_xcnt;
     a.rootbox = c->d_rootbox;
     a.qnode = c->d_qnode;
@@ -1156,7 +1159,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
     dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_nbox); dfree(c->d_qnode); dfree(c->d_lfp);
     dfree(c->d_band);
-    dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
+    dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_qlate); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
     dfree(c->d_bkin); dfree(c->d_bvin); dfree(c->d_bka); dfree(c->d_bva); dfree(c->d_bkb); dfree(c->d_bvb);
     dfree(c->d_bscratch); dfree(c->d_refl_rec); dfree(c->d_refr_rec);

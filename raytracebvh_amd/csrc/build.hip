@@ -750,24 +750,30 @@ __device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f, uint32_t
 // QNodes of the nodes whose leaf range crosses a refit workgroup (k_refit quantizes the
 // others): a scan of the 16-B topology records, the pair loads for the crossing ones only.
 // (A list appended by the climbing threads serialised on its one counter: ~88 adds per us.)
+// the QNode of crossing node k at its slot, from the node boxes or the records (k_qnodes_cross, k_qnodes_late)
+__device__ __forceinline__ void qnode_cross(const BuildArgs& a, uint32_t k) {
+    const uint32_t slot = slot_of(a.pint[k], a.T);
+    const float E = *node_edge(a, k);
+    if (!a.rec_on) {   // no records: the topology and the node boxes (no pseudo-records either)
+        QEnt e0, e1;
+        nbox_kids(a, k, e0, e1);
+        float4 w[4];
+        uint32_t ent[4];
+        greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { nbox_kids(a, e.id, c0, c1); }, E, w, ent);
+        store4(a.qnode + slot, w);
+    } else if (a.pseudo) {
+        qnode_from_records<false>(a.rec, slot, E, a.qnode + slot);
+    } else {
+        qnode_from_records<true>(a.rec, slot, E, a.qnode + slot);
+    }
+}
 __global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
-    for_crossing(a, [&](uint32_t k) {
-        const uint32_t slot = slot_of(a.pint[k], a.T);
-        const float E = *node_edge(a, k);
-        if (!a.rec_on) {   // no records: the topology and the node boxes (no pseudo-records either)
-            QEnt e0, e1;
-            nbox_kids(a, k, e0, e1);
-            float4 w[4];
-            uint32_t ent[4];
-            greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { nbox_kids(a, e.id, c0, c1); }, E, w,
-                               ent);
-            store4(a.qnode + slot, w);
-        } else if (a.pseudo) {
-            qnode_from_records<false>(a.rec, slot, E, a.qnode + slot);
-        } else {
-            qnode_from_records<true>(a.rec, slot, E, a.qnode + slot);
-        }
-    });
+    for_crossing(a, [&](uint32_t k) { qnode_cross(a, k); });
+}
+// the QNodes of the crossing nodes k_refit_group listed: qlate[1, 1 + qlate[0]), one a thread
+__global__ __launch_bounds__(BLOCK) void k_qnodes_late(BuildArgs a) {
+    const uint32_t n = a.qlate[0];
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) qnode_cross(a, a.qlate[1 + j]);
 }
 
 // The node records (rtbvh_device.h) of a build that wrote none (a certified-only context's, api.hip), on demand:
@@ -833,6 +839,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     const uint32_t end = base + RBLOCK;
     s_cnt[tid] = 0;
     if (tid == 0) s_xn = 0;
+    if (i == 0 && a.qlate) a.qlate[0] = 0;   // (k_refit_group's list of crossing nodes)
     if (i + 1 < T) {   // coalesced, so the in-block climb makes no dependent global loads
         s_topo[tid] = a.topo[i];
         s_pint[tid] = a.pint[i];
@@ -1180,13 +1187,24 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
             if (j + st <= nbg - 1 && s_off[j + st] <= e) j += st;
         return a.xlist[(size_t)(b0 + j) * RBLOCK + (e - s_off[j])];
     };
+    // the group's crossing nodes, listed densely for k_qnodes_late (k_qnodes_cross's wave per refit workgroup
+    // runs ~9 of 64 lanes)
+    __shared__ uint32_t s_lbase;
+    if (tid == 0) s_lbase = atomicAdd(&a.qlate[0], m);
+    __syncthreads();
+    const uint32_t lbase = 1 + s_lbase;
     if (m > GCAP) {   // (uniform) k_refit_top's protocol for every crossing node of the group
-        for (uint32_t e = tid; e < m; e += GBLOCK) refit_top_node(a, entry(e));
+        for (uint32_t e = tid; e < m; e += GBLOCK) {
+            const uint32_t k = entry(e);
+            a.qlate[lbase + e] = k;
+            refit_top_node(a, k);
+        }
         return;
     }
     uint32_t k0 = 0;
     if (tid < m) {
         k0 = entry(tid);
+        a.qlate[lbase + tid] = k0;
         atomicOr(&s_bits[(k0 - gbase) >> 5], 1u << ((k0 - gbase) & 31));
     }
     __syncthreads();
@@ -1748,9 +1766,13 @@ void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, 
 void launch_refit_tail(const BuildArgs& a, hipStream_t s) {
     const uint32_t nb = refit_blocks(a.T);
     if (a.T > RBLOCK) {   // the crossing nodes: climbed (in LDS within a group, then across), then quantized
-        if (a.flat_climb) hipLaunchKernelGGL(k_refit_top, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
-        else hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, a);
-        hipLaunchKernelGGL(k_qnodes_cross, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
+        if (a.flat_climb || !a.qlate) {
+            hipLaunchKernelGGL(k_refit_top, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
+            hipLaunchKernelGGL(k_qnodes_cross, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, a);
+            hipLaunchKernelGGL(k_qnodes_late, dim3(min(1024u, (nb + 15) / 16)), dim3(BLOCK), 0, s, a);
+        }
     }
 }
 // leaf j's pseudo-record from its leaf record's box (the bytes k_refit<true> writes)

@@ -75,6 +75,7 @@ struct BuildArgs {
     float* zpart;             // [ZPART * refit_blocks(T)] k_refit workgroup b's leaf depth range, edge bound
     uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
     uint32_t rec_on;          // write the node records (rec; a certified-only context's build writes none: api.hip)
+    uint32_t* qlate;          // [T] or null: k_refit_group's crossing nodes whose QNodes k_qnodes_late builds (count at 0)
     uint32_t flat_climb;      // launch_refit_tail: k_refit_top's one global climb instead of k_refit_group's (A/B)
     float* nbox;              // [6 (T-1)] or null: internal node k's box (min xyz, max xyz) -- what the certified
                               //   walks' reference-order re-traces and the crossing nodes' QNodes read without records
