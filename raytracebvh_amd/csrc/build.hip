@@ -992,7 +992,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     // greedy collapse expands them) no QNode is written.
     uint32_t* s_read = s_cnt;   // (the edge bounds were read above)
     __syncthreads();
-    if (!RTBVH_QSKIP) {   // (A/B: every QNode written)
+    if (!RTBVH_QSKIP || a.qall) {   // (every QNode written: A/B, or a context whose six-wide tree reads them all)
         s_read[tid] = mine ? 1u : 0u;
     } else {
         bool near = false;
@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
             ent[2 * side + 1] = cq.y;
         }
     }
-    bool pending = mine && RTBVH_QSKIP;   // its entries are not marked yet
+    bool pending = mine && RTBVH_QSKIP && !a.qall;   // its entries are not marked yet
     for (;;) {
         __syncthreads();
         bool changed = false;
@@ -1293,6 +1293,164 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
                 break;
             }
         }
+    }
+}
+
+// ---- the six-wide walk-only tree (RTBVH_W6, an A/B knob of certified contexts) -----------------
+// Item p of w6 (64 B): a node -- words 0-2 the grid origin, 3 the step exponents ex | ey << 8 | ez << 16 (all 0: no
+// grid, the certified walk flags the ray), 4 the margin codes (margin.h: ce | ct << 16), 5 k: its n entries are
+// items 6k .. 6k+n-1, 6-11 the lo / hi bytes of entries 0-3 per axis (x lo, x hi, y lo, y hi, z lo, z hi), 12-14
+// entries 4-5 per axis {lo4, lo5, hi4, hi5}, 15 the entries' leaf mask | n << 8 -- or a leaf: words 0-9 of its leaf
+// record (v0, e1, e2, the triangle word) and 10 its sorted index j.  The root node is item 6(T-1).  Node k's
+// entries: its two children, the largest-area internal entry among the first five expanded into its children,
+// four times (greedy_qnode_words's rule, six wide).  This first form builds it after the build, from the
+// topology, the node boxes and the QNodes' margin codes (all of them written: RTBVH_QSKIP=0): w6s[k] holds node
+// k's item, and every node copies its entries' items into its six slots.
+struct W6E {
+    uint32_t id;
+    float b[6];
+};
+__device__ __forceinline__ void w6_sel(W6E& d, const W6E& s, bool take) {
+    d.id = take ? s.id : d.id;
+#pragma unroll
+    for (int q = 0; q < 6; q++) d.b[q] = take ? s.b[q] : d.b[q];
+}
+__device__ __forceinline__ void w6_entries(const BuildArgs& a, uint32_t k, W6E (&E)[6], uint32_t& n) {
+    const uint4 t = a.topo[k];
+    E[0].id = t.x;
+    child_box(a, t.x, E[0].b);
+    E[1].id = t.y;
+    child_box(a, t.y, E[1].b);
+#pragma unroll
+    for (int m = 2; m < 6; m++) E[m] = E[0];
+    n = 2;
+#pragma unroll
+    for (int step = 0; step < 4; step++) {
+        int pick = -1;
+        float best = -1.f;
+#pragma unroll
+        for (int m = 0; m < 5; m++) {
+            if ((uint32_t)m < n && !(E[m].id & LEAF_BIT)) {
+                const float ar = half_area(E[m].b);
+                if (ar > best) { best = ar; pick = m; }
+            }
+        }
+        if (pick < 0) break;
+        W6E sel = E[0];
+#pragma unroll
+        for (int m = 1; m < 5; m++) w6_sel(sel, E[m], m == pick);
+        const uint4 st = a.topo[sel.id];
+        W6E c0, c1;
+        c0.id = st.x;
+        child_box(a, st.x, c0.b);
+        c1.id = st.y;
+        child_box(a, st.y, c1.b);
+#pragma unroll
+        for (int m = 0; m < 5; m++) w6_sel(E[m], c0, m == pick);
+#pragma unroll
+        for (int m = 2; m < 6; m++) w6_sel(E[m], c1, (uint32_t)m == n);
+        ++n;
+    }
+}
+// one axis of a six-entry grid (quantize_axis, six boxes; the absent ones repeat entry 0): the exponent byte
+// (0: no finite frame) and the bytes
+__device__ __forceinline__ uint32_t w6_axis(const float (&lo)[6], const float (&hi)[6], float& org, uint32_t (&bl)[6],
+                                            uint32_t (&bh)[6]) {
+    float o = lo[0], m = hi[0];
+#pragma unroll
+    for (int c = 1; c < 6; c++) {
+        o = fminf(o, lo[c]);
+        m = fmaxf(m, hi[c]);
+    }
+    const float ext = m - o;
+    org = o;
+    if (!(fabsf(o) <= 0x1p100f && fabsf(m) <= 0x1p100f && ext <= 0x1p100f)) return 0u;
+    int e = -120;
+    if (ext > 0.f) {
+        const int E = (int)((__float_as_uint(ext) >> 23) & 255u) - 127;
+        e = max(E - 8, -120);
+    }
+    while (fmaf(255.f, pow2f(e), o) < m) ++e;
+    const float sc = pow2f(e), rs = pow2f(-e);
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+        uint32_t l = (uint32_t)fminf(fmaxf(floorf((lo[c] - o) * rs), 0.f), 255.f);
+        uint32_t h = (uint32_t)fminf(fmaxf(ceilf((hi[c] - o) * rs), 0.f), 255.f);
+        if (l > 0 && fmaf((float)l, sc, o) > lo[c]) --l;
+        if (h < 255 && fmaf((float)h, sc, o) < hi[c]) ++h;
+        bl[c] = l;
+        bh[c] = h;
+    }
+    return (uint32_t)(e + 127);
+}
+__global__ __launch_bounds__(BLOCK) void k_w6_stage(BuildArgs a, uint4* __restrict__ w6s) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k + 1 >= a.T) return;
+    W6E E[6];
+    uint32_t n;
+    w6_entries(a, k, E, n);
+    uint32_t w[16];
+    uint32_t ex = 0, lmask = 0;
+    bool grid = true;
+#pragma unroll
+    for (int ax = 0; ax < 3; ax++) {
+        float lo[6], hi[6], org;
+        uint32_t bl[6], bh[6];
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+            lo[c] = E[c].b[ax];
+            hi[c] = E[c].b[3 + ax];
+        }
+        const uint32_t eb = w6_axis(lo, hi, org, bl, bh);
+        grid = grid && eb != 0u;
+        ex |= eb << (8 * ax);
+        w[ax] = __float_as_uint(org);
+        w[6 + 2 * ax] = bl[0] | bl[1] << 8 | bl[2] << 16 | bl[3] << 24;
+        w[7 + 2 * ax] = bh[0] | bh[1] << 8 | bh[2] << 16 | bh[3] << 24;
+        w[12 + ax] = bl[4] | bl[5] << 8 | bh[4] << 16 | bh[5] << 24;
+    }
+    // the margin codes of node k's QNode (scl[1], scl[2] low 16 bits; none without a grid)
+    const uint4 qw = reinterpret_cast<const uint4*>(a.qnode + slot_of(a.pint[k], a.T))[1];
+    const bool qgrid = __uint_as_float(reinterpret_cast<const uint4*>(a.qnode + slot_of(a.pint[k], a.T))[0].w) != 0.f;
+    w[3] = grid && qgrid ? ex : 0u;
+    w[4] = (qw.x & 0xFFFFu) | (qw.y & 0xFFFFu) << 16;
+    w[5] = k;
+#pragma unroll
+    for (int m = 0; m < 6; m++) lmask |= ((uint32_t)m < n && (E[m].id & LEAF_BIT)) ? 1u << m : 0u;
+    w[15] = lmask | n << 8;
+    uint4* d = w6s + 4 * (size_t)k;
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    d[2] = make_uint4(w[8], w[9], w[10], w[11]);
+    d[3] = make_uint4(w[12], w[13], w[14], w[15]);
+}
+__global__ __launch_bounds__(BLOCK) void k_w6_fill(BuildArgs a, const uint4* __restrict__ w6s, uint4* __restrict__ w6) {
+    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k + 1 >= a.T) return;
+    W6E E[6];
+    uint32_t n;
+    w6_entries(a, k, E, n);
+#pragma unroll
+    for (int m = 0; m < 6; m++) {
+        if ((uint32_t)m >= n) break;
+        uint4* d = w6 + 4 * (6 * (size_t)k + m);
+        const uint32_t id = E[m].id;
+        if (id & LEAF_BIT) {
+            const uint32_t j = id & ~LEAF_BIT;
+            const uint4* r = reinterpret_cast<const uint4*>(a.leaf + 4 * (size_t)j);
+            const uint4 r0 = r[0], r1 = r[1], r2 = r[2];
+            d[0] = r0;
+            d[1] = r1;
+            d[2] = make_uint4(r2.x, r2.y, j, 0u);
+            d[3] = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            const uint4* src = w6s + 4 * (size_t)id;
+            d[0] = src[0]; d[1] = src[1]; d[2] = src[2]; d[3] = src[3];
+        }
+    }
+    if (k == 0) {   // the root (Karras node 0)
+        uint4* d = w6 + 4 * (6 * (size_t)(a.T - 1));
+        d[0] = w6s[0]; d[1] = w6s[1]; d[2] = w6s[2]; d[3] = w6s[3];
     }
 }
 
@@ -1789,6 +1947,11 @@ void launch_pseudo(const BuildArgs& a, hipStream_t s) {
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     launch_refit_leaves(a, s);
     launch_refit_tail(a, s);
+}
+void launch_w6(const BuildArgs& a, uint4* w6s, uint4* w6, hipStream_t s) {
+    if (a.T <= 1) return;
+    hipLaunchKernelGGL(k_w6_stage, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a, w6s);
+    hipLaunchKernelGGL(k_w6_fill, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a, (const uint4*)w6s, w6);
 }
 void launch_records(const BuildArgs& a, hipStream_t s) {
     if (a.T > 1) hipLaunchKernelGGL(k_records, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a);
