@@ -1469,6 +1469,19 @@ __global__ __launch_bounds__(BLOCK) void k_pb_count_top(BuildArgs b, TraceArgs a
     }
     pb_bin_block<false>(a, blockIdx.x - ntail, off, cur, bins, cap, ntx);
 }
+// ... and after k_refit_group (the grouped climb, its own launch): blocks [0, nlate) quantize the crossing nodes it
+// listed (k_qnodes_late's work) beside the count.  (8 waves per SIMD, the QNode blocks spilling: 89 us against 98 at
+// the QNode code's 84 VGPRs, 5 waves; k_refit_group + this 162 us against k_pb_count_top + k_qnodes_cross 194, r06_o)
+__global__ __launch_bounds__(BLOCK, 8) void k_pb_count_late(BuildArgs b, TraceArgs a, uint32_t nlate,
+                                                         uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                                                         uint4* __restrict__ bins, uint32_t cap, uint32_t ntx) {
+    if (blockIdx.x < nlate) {
+        const uint32_t n = b.qlate[0];
+        for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < n; j += nlate * BLOCK) qnode_cross(b, b.qlate[1 + j]);
+        return;
+    }
+    pb_bin_block<false>(a, blockIdx.x - nlate, off, cur, bins, cap, ntx);
+}
 
 __global__ __launch_bounds__(BLOCK) void k_refit_boxes(BuildArgs a, const float* __restrict__ boxes) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1917,6 +1930,13 @@ void launch_refit_leaves(const BuildArgs& a, hipStream_t s) {
 void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, uint32_t* cur, uint4* bins, uint32_t cap,
                          uint32_t ntx, uint32_t leaf_blocks, hipStream_t s) {
     const uint32_t nb = refit_blocks(b.T);
+    if (!b.flat_climb && b.qlate) {   // the grouped climb first, then its list's QNodes beside the count
+        const uint32_t nlate = b.T > RBLOCK ? min(1024u, (nb + 15) / 16) : 0u;
+        if (nlate) hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, b);
+        hipLaunchKernelGGL(k_pb_count_late, dim3(nlate + leaf_blocks), dim3(BLOCK), 0, s, b, a, nlate, off, cur, bins, cap,
+                           ntx);
+        return;
+    }
     const uint32_t ntail = b.T > RBLOCK ? (nb + XWAVES - 1) / XWAVES : 0u;
     hipLaunchKernelGGL(k_pb_count_top, dim3(ntail + leaf_blocks), dim3(BLOCK), 0, s, b, a, ntail, off, cur, bins, cap, ntx);
     if (ntail) hipLaunchKernelGGL(k_qnodes_cross, dim3(ntail), dim3(BLOCK), 0, s, b);
