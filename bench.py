@@ -162,8 +162,9 @@ def build_pmc(workload, mode):
 
 # the build's kernels and their launches per build (the 30-bit sort: 4 passes of 8-bit digits);
 # the mesh box (k_bounds) is computed once per scene by rtbvh_set_scene
+# (the crossing nodes: k_refit_group + k_qnodes_late since round 6; k_refit_top + k_qnodes_cross in older profiles)
 BUILD_KERNELS = {"k_morton": 1, "k_upsweep": 4, "k_scan_rows": 4, "k_downsweep": 4, "k_karras": 1, "k_refit": 1, "k_zrange": 1,
-                 "k_refit_top": 1, "k_qnodes_cross": 1}
+                 "k_refit_group": 1, "k_qnodes_late": 1, "k_refit_top": 1, "k_qnodes_cross": 1}
 
 
 def cpu_model() -> str:
