@@ -68,7 +68,7 @@ struct rtbvh_ctx {
     float* d_rootbox = nullptr;
     float* d_zpart = nullptr;
     // rtbvh_compute_bvh: the binned primary pass of the frame starts on `side` once the build's
-    // leaves are written (ev_leaf, between k_zrange and k_refit_top) and joins the context stream
+    // leaves are written (ev_leaf, between k_zrange and k_refit_group) and joins the context stream
     // (ev_prim) before the walk of its overflowed tiles, which reads the whole BVH
     hipStream_t side = nullptr;
     hipEvent_t ev_leaf = nullptr, ev_prim = nullptr;
@@ -77,10 +77,6 @@ struct rtbvh_ctx {
     // reference-order re-traces): a certified-only context's build writes the boxes alone (records_skipped),
     // any other build the records alone; the other form is derived on first use (ensure_records / ensure_nbox)
     bool rec_ok = false, nbox_ok = false;
-    // RTBVH_W6=1 (A/B): the certified bounce walk on the six-wide tree (build.hip launch_w6), built on first use
-    bool w6_ok = false;
-    uint4 *d_w6s = nullptr, *d_w6 = nullptr;
-    uint32_t cap_w6 = 0;
     bool build_nbox = false;     // the last build wrote node boxes, not records
     float* d_nbox = nullptr;     // [6 (T-1)] internal node boxes
     bool qnode_ok = false;       // the built tree has its QNodes (read by the 4-wide bounce walk only)
@@ -182,7 +178,7 @@ struct rtbvh_ctx {
     // tuning knobs of A/B runs, read once by rtbvh_create (RTBVH_BOUNCE_BLOCKS, RTBVH_OVERLAP,
     // RTBVH_SIDE_PRIORITY): a shipped context does not change its launches per frame
     uint32_t knob_bounce_blocks = 0;
-    bool knob_overlap = false, knob_side_priority = true, knob_keep_records = false, knob_flat_climb = false, knob_w6 = false;
+    bool knob_overlap = false, knob_side_priority = true, knob_keep_records = false;
     // the band deal of band traces (rtbvh_set_band_deal): rank 0's weight in 1/16 of another rank's
     uint32_t root_share = 16;
     struct DealTab {   // a weighted deal's device table: every rank's bands, then slots[b] = r << 24 | pos
@@ -388,8 +384,6 @@ BuildArgs build_args(rtbvh_ctx* c) {
     // the last build's outputs: node records, or (a certified-only context's) node boxes instead
     a.rec_on = c->build_nbox ? 0u : 1u;
     a.nbox = c->build_nbox ? c->d_nbox : nullptr;
-    a.flat_climb = c->knob_flat_climb ? 1u : 0u;
-    a.qall = c->knob_w6 ? 1u : 0u;
     return a;
 }
 // the same, with the node-box array for a kernel that reads (or writes) it
@@ -793,11 +787,8 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     // the walks' node data: a certified trace's re-traces walk the node boxes (a.nb), every other walk the node
     // records; a build writes one of the two, the other is derived here from the complete tree (after the tail)
     const bool need_conv = cert ? !c->nbox_ok : !c->rec_ok;
-    // RTBVH_W6: the six-wide tree is built from the complete tree (after the tail) on first use
-    const bool w6_want = cert && c->knob_w6 && c->qnode_ok && c->T > 2048 && c->T < (1u << 28) && bounces > 0 &&
-                         !(c->capturing && c->cap_w6 < c->T);
     const bool fuse_tail = tail.pending && pkind == PrimaryKind::BINNED && s == c->stream && slot == 0 && rows > 0 &&
-                           !need_conv && !(w6_want && !c->w6_ok);
+                           !need_conv;
     if (!fuse_tail && tail.pending) {   // before any walk reads the tree
         tail.run();
         if (s != c->stream) {   // (a caller stream: ordered after it like after the build)
@@ -810,25 +801,6 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
         if (st) return st;
     }
     a.nb = cert;
-    a.w6 = nullptr;
-    if (w6_want) {
-        if (!c->w6_ok) {
-            if (c->cap_w6 < c->T) {
-                drop_graph(c);
-                HIPC(c, dalloc(c->d_w6s, 4 * (size_t)c->T));
-                HIPC(c, dalloc(c->d_w6, 4 * (6 * (size_t)c->T - 5)));
-                c->cap_w6 = c->T;
-            }
-            launch_w6(build_args_nbox(c), c->d_w6s, c->d_w6, c->stream);
-            HIPC(c, hipGetLastError());
-            c->w6_ok = true;
-            if (s != c->stream) {
-                if (!c->capturing) HIPC(c, hipEventRecord(c->ev_built, c->stream));
-                HIPC(c, hipStreamWaitEvent(s, c->ev_built, 0));
-            }
-        }
-        a.w6 = c->d_w6;
-    }
     const uint32_t Pg = nsplit == 1 ? P : W * 8 * ((my_bands + nsplit - 1) / nsplit);   // max live rays per chain
     st = ensure_split_capacity(c, slot ? slot + 1 : nsplit, Pg);
     if (st) return st;
@@ -1148,8 +1120,6 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
     if (const char* e = getenv("RTBVH_OVERLAP")) c->knob_overlap = atoi(e) != 0;
     if (const char* e = getenv("RTBVH_SIDE_PRIORITY")) c->knob_side_priority = atoi(e) != 0;
     if (const char* e = getenv("RTBVH_KEEP_RECORDS")) c->knob_keep_records = atoi(e) != 0;
-    if (const char* e = getenv("RTBVH_W6")) c->knob_w6 = atoi(e) != 0;
-    if (const char* e = getenv("RTBVH_FLAT_CLIMB")) c->knob_flat_climb = atoi(e) != 0;   // (A/B: one global climb)
     *out = c;
     return RTBVH_OK;
 }
@@ -1185,7 +1155,7 @@ void rtbvh_destroy(rtbvh_ctx* c) {
     for (auto& p : c->pb) { dfree(p.off); dfree(p.cur); dfree(p.bins); dfree(p.sums); dfree(p.keys); }
     dfree(c->d_opos); dfree(c->d_verts); dfree(c->d_idx); dfree(c->d_matidx); dfree(c->d_mats);
     dfree(c->d_codes); dfree(c->d_ids); dfree(c->d_ka); dfree(c->d_va); dfree(c->d_kb); dfree(c->d_vb);
-    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_nbox); dfree(c->d_w6s); dfree(c->d_w6); dfree(c->d_qnode); dfree(c->d_lfp);
+    dfree(c->d_sort_scratch); dfree(c->d_tclip); dfree(c->d_leaf); dfree(c->d_inner); dfree(c->d_topo); dfree(c->d_rec); dfree(c->d_nbox); dfree(c->d_qnode); dfree(c->d_lfp);
     dfree(c->d_band);
     dfree(c->d_pleaf); dfree(c->d_pint); dfree(c->d_cnt); dfree(c->d_xlist); dfree(c->d_qlate); dfree(c->d_xcnt); dfree(c->d_bounds); dfree(c->d_rootbox); dfree(c->d_zpart);
     dfree(c->d_color); dfree(c->d_intensity); dfree(c->d_q[0]); dfree(c->d_q[1]); dfree(c->d_qcount); dfree(c->d_next); dfree(c->d_hit);
@@ -1350,7 +1320,6 @@ rtbvh_status rtbvh_build_async(rtbvh_ctx* c) {
     if (timing) HIPC(c, hipEventRecord(ev[1], s));   // (the mesh box is the scene's: rtbvh_set_scene)
     // a certified-only context's build: node boxes instead of node records (records_skipped)
     c->build_nbox = records_skipped(c);
-    c->w6_ok = false;
     c->rec_ok = !c->build_nbox;
     c->nbox_ok = c->build_nbox;
     a.rec_on = c->build_nbox ? 0u : 1u;

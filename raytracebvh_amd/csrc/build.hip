@@ -32,8 +32,12 @@ constexpr uint32_t BLOCK = 256;
 #define RTBVH_REFIT_BLOCK 512
 #endif
 // leaves (and node indices) per k_refit workgroup: the nodes whose leaf range lies inside
-// one join in LDS; the others ("crossing") climb in k_refit_top
+// one join in LDS; the others ("crossing") climb in k_refit_group
 constexpr uint32_t RBLOCK = RTBVH_REFIT_BLOCK;
+#ifndef RTBVH_REFIT_PROBE
+#define RTBVH_REFIT_PROBE 0   // A/B probe builds (-DRTBVH_AB_BUILD): 1 no QNode computed, 3 no phase-4 stores,
+                              // 4 no leaf-record stores, 5 no leaf margin / footprint (wrong trees: timing only)
+#endif
 #ifndef RTBVH_QSKIP
 #define RTBVH_QSKIP 1   // k_refit writes only the QNodes the 4-wide walk reads (0: all, A/B)
 #endif
@@ -485,7 +489,7 @@ __device__ __forceinline__ void complete_node(const BuildArgs& a, uint32_t p, ui
 }
 
 // The largest leaf edge bound below a node (margin.h: its QNode's margin codes).  Where a QNode is
-// built from the records (k_qnodes_cross, k_qnodes) it is read from inner[k].aux0, written by
+// built from the records (k_qnodes_late, k_qnodes) it is read from inner[k].aux0, written by
 // whoever completes node k outside k_refit's in-block climb (refit_climb, refit_top_node,
 // k_build_small); inner[p].child_l / child_r carry a child's bound through the climb's hand-off,
 // beside its box (the hand-off uses no other word of inner[p]).
@@ -506,7 +510,7 @@ __device__ __forceinline__ float ld_edge_sc1(const float* src) {
 // The global climb, for the nodes whose leaf range crosses a refit workgroup: from a complete
 // node (box lo, hi, edge bound em; e = its parent link) upward, the child box and bound handed
 // over through inner[p] (sc1) and a per-node ticket; the second arriver completes p and goes on.
-// k_qnodes_cross quantizes these nodes afterwards.
+// k_qnodes_late quantizes these nodes afterwards.
 __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, float em, uint32_t e, const BuildArgs& a) {
     // a clz64 tree is at most 64 levels deep; the bound only stops a CPUTests-delta
     // tree with a parent cycle from spinning forever
@@ -521,7 +525,7 @@ __device__ __forceinline__ void refit_climb(f3 lo, f3 hi, float em, uint32_t e, 
         f3 smin, smax;
         ld_box_sc1(side ? a.inner[p].lmin : a.inner[p].rmin, smin, smax);
         em = fmaxf(em, ld_edge_sc1(hand_edge(a, p, side ^ 1u)));
-        *node_edge(a, p) = em;   // (read by k_qnodes_cross / k_qnodes, later launches)
+        *node_edge(a, p) = em;   // (read by k_qnodes_late / k_qnodes, later launches)
         e = a.pint[p];
         if (side) complete_node(a, p, e, smin, smax, lo, hi, lo, hi);
         else      complete_node(a, p, e, lo, hi, smin, smax, lo, hi);
@@ -737,20 +741,7 @@ __global__ __launch_bounds__(BLOCK) void k_qnodes(Inner* __restrict__ rec, const
     qnode_from_records(rec, slot, __uint_as_float(inner[k].aux0), qn + slot);
 }
 
-// The crossing nodes of refit workgroup b are xlist[b * RBLOCK, + xcnt[b]): one wave per
-// refit workgroup walks them (a few dozen typically; up to RBLOCK for a degenerate tree).
-constexpr uint32_t XWAVES = BLOCK / 64;
-template <class F>
-__device__ __forceinline__ void for_crossing(const BuildArgs& a, F&& f, uint32_t bid = blockIdx.x) {
-    const uint32_t b = bid * XWAVES + (threadIdx.x >> 6);
-    if (b * RBLOCK >= a.T) return;
-    const uint32_t n = a.xcnt[b];
-    for (uint32_t j = threadIdx.x & 63u; j < n; j += 64) f(a.xlist[b * RBLOCK + j]);
-}
-// QNodes of the nodes whose leaf range crosses a refit workgroup (k_refit quantizes the
-// others): a scan of the 16-B topology records, the pair loads for the crossing ones only.
-// (A list appended by the climbing threads serialised on its one counter: ~88 adds per us.)
-// the QNode of crossing node k at its slot, from the node boxes or the records (k_qnodes_cross, k_qnodes_late)
+// the QNode of crossing node k at its slot, from the node boxes or the records (k_qnodes_late, k_pb_count_late)
 __device__ __forceinline__ void qnode_cross(const BuildArgs& a, uint32_t k) {
     const uint32_t slot = slot_of(a.pint[k], a.T);
     const float E = *node_edge(a, k);
@@ -766,9 +757,6 @@ __device__ __forceinline__ void qnode_cross(const BuildArgs& a, uint32_t k) {
     } else {
         qnode_from_records<true>(a.rec, slot, E, a.qnode + slot);
     }
-}
-__global__ __launch_bounds__(BLOCK) void k_qnodes_cross(BuildArgs a) {
-    for_crossing(a, [&](uint32_t k) { qnode_cross(a, k); });
 }
 // the QNodes of the crossing nodes k_refit_group listed: qlate[1, 1 + qlate[0]), one a thread
 __global__ __launch_bounds__(BLOCK) void k_qnodes_late(BuildArgs a) {
@@ -852,11 +840,15 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
         if (i < T) {
             leaf_record_words(a, i, lo, hi, r);
             float zkey;
+#if RTBVH_REFIT_PROBE == 5   // (A/B probe builds only: cost of the leaf's margin and footprint)
+            zkey = lo.z;
+#else
             leaf_margin(r, lo.z, hi.z, emax, zkey);
             a.lfp[i] = leaf_footprint(lo, hi, zkey);
+#endif
         }
         const uint32_t w0 = base + (tid & ~63u);   // this wave's first leaf
-        staged_records(a.leaf + 4 * (size_t)w0, T > w0 ? min(64u, T - w0) : 0u, r,
+        if (RTBVH_REFIT_PROBE != 4) staged_records(a.leaf + 4 * (size_t)w0, T > w0 ? min(64u, T - w0) : 0u, r,
                        reinterpret_cast<float4*>(&s_box[0][0][0]) + 128 * (tid >> 6));
     }
     if (i < T) {
@@ -906,7 +898,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
             q3 = s_topo[p - base];   // ids, leaf range
             cross = !(q3.z >= base && q3.w < end);
         }
-        if (cross) {   // k_refit_top takes it from here (kernel boundary: plain stores)
+        if (cross) {   // k_refit_group takes it from here (kernel boundary: plain stores)
             float* hb = side ? a.inner[p].rmin : a.inner[p].lmin;
             hb[0] = lo.x; hb[1] = lo.y; hb[2] = lo.z; hb[3] = hi.x; hb[4] = hi.y; hb[5] = hi.z;
             *hand_edge(a, p, side) = emax;
@@ -934,7 +926,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
         }
     }
     __syncthreads();
-    // the block's crossing nodes (k_refit_top completes them, k_qnodes_cross quantizes them):
+    // the block's crossing nodes (k_refit_group completes them, k_qnodes_late quantizes them):
     // listed at xlist[base, ...) in wave order, their tickets zeroed (no other ticket is used)
     const uint4 q = s_topo[tid];
     const bool xnode = i + 1 < T && !(q.z >= base && q.w < end);
@@ -982,17 +974,21 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     QEnt e0, e1;
     lds_kids(i, e0, e1);
     E = __uint_as_float(s_cnt[tid] & 0x7FFFFFFFu);   // the node's edge bound (the climb's ticket)
+#if RTBVH_REFIT_PROBE == 1   // (probe: no QNode computed)
+    for (int k = 0; k < 4; k++) { qw[k] = make_float4(0.f, 0.f, 0.f, 0.f); ent[k] = INVALID; }
+#else
     greedy_qnode_words(e0, e1, [&](const QEnt& e, QEnt& c0, QEnt& c1) { lds_kids(e.id, c0, c1); }, -1.f, qw, ent);
+#endif
     }
     // Which of the block's QNodes the 4-wide walk reads: it steps from a QNode to its internal
     // entries only, so a node's QNode is read iff the node is the root or an entry of a read QNode.  A QNode's
     // entries lie 1..3 levels below its node, so every node within 3 levels below a node the block does not own
-    // (the root's parent, a crossing node, whose QNode k_qnodes_cross builds) is taken as read, and the rest is
+    // (the root's parent, a crossing node, whose QNode k_qnodes_late builds) is taken as read, and the rest is
     // decided top-down inside the block, one QNode level per round.  Of the others (about two in three: the
     // greedy collapse expands them) no QNode is written.
     uint32_t* s_read = s_cnt;   // (the edge bounds were read above)
     __syncthreads();
-    if (!RTBVH_QSKIP || a.qall) {   // (every QNode written: A/B, or a context whose six-wide tree reads them all)
+    if (!RTBVH_QSKIP) {   // (A/B: every QNode written)
         s_read[tid] = mine ? 1u : 0u;
     } else {
         bool near = false;
@@ -1017,7 +1013,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
             ent[2 * side + 1] = cq.y;
         }
     }
-    bool pending = mine && RTBVH_QSKIP && !a.qall;   // its entries are not marked yet
+    bool pending = mine && RTBVH_QSKIP;   // its entries are not marked yet
     for (;;) {
         __syncthreads();
         bool changed = false;
@@ -1043,7 +1039,7 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
     // out STAGE slots at a time: the writers fill the staging buffer (over s_box, read no more)
     // and mark their slots, then the block stores the marked slots 16 B per lane, consecutive
     // lanes on consecutive bytes (a 64-B record per lane writes at ~0.6x that rate).
-    // Unmarked slots (records of crossing nodes, k_refit_top's; other blocks' records) are left
+    // Unmarked slots (records of crossing nodes, k_refit_group's; other blocks' records) are left
     // alone.
     constexpr uint32_t STAGE = RTBVH_REFIT_STAGE_SLOTS;
     static_assert(sizeof(s_box) >= 64 * STAGE, "staging fits in s_box");
@@ -1086,17 +1082,18 @@ __global__ __launch_bounds__(RBLOCK) void k_refit(BuildArgs a) {
             for (uint32_t c = tid; c < 4 * STAGE; c += RBLOCK) {
                 const uint32_t k = c >> 2;
                 if ((s_own[k >> 5] >> (k & 31)) & 1u && lo_slot + k < nslots)
-                    st_out<4>(dst + 4 * (size_t)(lo_slot + k) + (c & 3), s_stage[c]);
+                    if (RTBVH_REFIT_PROBE != 3) st_out<4>(dst + 4 * (size_t)(lo_slot + k) + (c & 3), s_stage[c]);
             }
         }
     }
 }
 
-// The crossing nodes (a few per k_refit workgroup, the top of the tree among them): k_refit
-// left the box of every non-crossing child of a crossing node in inner[node] (leaf or in-block
-// subtree).  Node k's thread: both children non-crossing -> k is complete, climb from it; one
-// -> arrive at k's ticket for that child (the other arrives by a climb); none -> nothing.  A
-// separate launch, so that k_refit's workgroups never wait on the global climb's latency.
+// The global climb of a crossing node k (a few per k_refit workgroup, the top of the tree among them;
+// k_refit_group runs it for the nodes that cross their group): k_refit left the box of every
+// non-crossing child of a crossing node in inner[node] (leaf or in-block subtree).  Both children
+// non-crossing -> k is complete, climb from it; one -> arrive at k's ticket for that child (the other
+// arrives by a climb); none -> nothing.  (Round 5 ran it for every crossing node, one wave per refit
+// workgroup, as k_refit_top: ~25 levels of device-scope round trips at C5, 0.12 ms.)
 __device__ __forceinline__ void refit_top_node(const BuildArgs& a, uint32_t k) {
     const uint4 q = a.topo[k];
     const bool ncl = (q.x & LEAF_BIT) || !crossing(a.topo[q.x], q.x);
@@ -1129,20 +1126,17 @@ __device__ __forceinline__ void refit_top_node(const BuildArgs& a, uint32_t k) {
     }
     refit_climb(lo, hi, em, e, a);
 }
-__global__ __launch_bounds__(BLOCK) void k_refit_top(BuildArgs a) {
-    for_crossing(a, [&](uint32_t k) { refit_top_node(a, k); });
-}
 
 // ---- the crossing nodes, grouped (launch_refit_tail) ---------------------------------------------------
-// k_refit_top's climb makes one device-scope round trip (sc1 box hand-off, ticket atomic) per level of crossing
+// The global climb makes one device-scope round trip (sc1 box hand-off, ticket atomic) per level of crossing
 // nodes, ~25 levels at C5.  A group is RGROUP consecutive refit workgroups (GSPAN node indices), and a crossing
 // node whose leaf range lies inside its group's span is "group-internal" (C5: 176K of the 181K).  k_refit_group,
 // one workgroup per group, climbs the group-internal ones in LDS (slots by node index through a bitmap rank; the
-// same union order and bounds as k_refit_top), and where a climb leaves the group -- its parent crosses the group
-// -- it continues with k_refit_top's global protocol (refit_climb); the group's other crossing nodes start it as
-// k_refit_top's threads do.  The protocol's tickets take arrivals in any order, so the global climb above the
-// groups is the same, a handful of levels.  A group with more than GCAP crossing nodes (a degenerate tree) runs
-// k_refit_top's protocol for all of them.
+// same union order and bounds as the global climb), and where a climb leaves the group -- its parent crosses the
+// group -- it continues with the global protocol (refit_climb); the group's other crossing nodes start it
+// (refit_top_node).  The protocol's tickets take arrivals in any order, so the global climb above the groups is the
+// same, a handful of levels.  A group with more than GCAP crossing nodes (a degenerate tree) runs the global
+// protocol for all of them.
 constexpr uint32_t RGROUP = 64;
 constexpr uint32_t GSPAN = RGROUP * RBLOCK;
 static_assert((GSPAN & (GSPAN - 1)) == 0, "the group span is a power of two");
@@ -1160,7 +1154,7 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
     __shared__ uint32_t s_par[GCAP];          // the node's parent link (pint)
     __shared__ float s_gbox[GCAP][2][6];
     __shared__ float s_ge[GCAP][2];
-    __shared__ uint32_t s_tk[GCAP];           // children in (3: not group-internal, k_refit_top's protocol)
+    __shared__ uint32_t s_tk[GCAP];           // children in (3: not group-internal, the global protocol)
     __shared__ uint32_t s_wsum[GBLOCK / 64];
     const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t nb = (a.T + RBLOCK - 1) / RBLOCK;
@@ -1187,13 +1181,13 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
             if (j + st <= nbg - 1 && s_off[j + st] <= e) j += st;
         return a.xlist[(size_t)(b0 + j) * RBLOCK + (e - s_off[j])];
     };
-    // the group's crossing nodes, listed densely for k_qnodes_late (k_qnodes_cross's wave per refit workgroup
-    // runs ~9 of 64 lanes)
+    // the group's crossing nodes, listed densely for k_qnodes_late (a wave per refit workgroup ran ~9 of 64
+    // lanes)
     __shared__ uint32_t s_lbase;
     if (tid == 0) s_lbase = atomicAdd(&a.qlate[0], m);
     __syncthreads();
     const uint32_t lbase = 1 + s_lbase;
-    if (m > GCAP) {   // (uniform) k_refit_top's protocol for every crossing node of the group
+    if (m > GCAP) {   // (uniform) the global protocol for every crossing node of the group
         for (uint32_t e = tid; e < m; e += GBLOCK) {
             const uint32_t k = entry(e);
             a.qlate[lbase + e] = k;
@@ -1234,7 +1228,7 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
     };
     // each node: its parent link, and the boxes k_refit handed over (leaves and the subtrees it joined)
     static_assert(GCAP == GBLOCK, "one slot per thread");
-    bool outside = false;   // this thread's node crosses its group: k_refit_top's protocol
+    bool outside = false;   // this thread's node crosses its group: the global protocol
     if (tid < m) {
         const uint32_t sl = slot_of_k(k0);
         const uint4 t = a.topo[k0];
@@ -1271,7 +1265,7 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
             const float* L = s_gbox[sl][0];
             const float* R = s_gbox[sl][1];
             const float em = fmaxf(s_ge[sl][0], s_ge[sl][1]);
-            *node_edge(a, k) = em;   // (read by k_qnodes_cross, a later launch)
+            *node_edge(a, k) = em;   // (read by k_qnodes_late, a later launch)
             const uint32_t e = s_par[sl];
             f3 lo, hi;
             complete_node(a, k, e, mk(L[0], L[1], L[2]), mk(L[3], L[4], L[5]), mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]),
@@ -1288,7 +1282,7 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
                 if (old != 1) break;   // the sibling is still to come
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 sl = sp;
-            } else {   // the parent crosses the group: k_refit_top's global climb from here
+            } else {   // the parent crosses the group: the global climb from here
                 refit_climb(lo, hi, em, e, a);
                 break;
             }
@@ -1296,182 +1290,13 @@ __global__ __launch_bounds__(GBLOCK) void k_refit_group(BuildArgs a) {
     }
 }
 
-// ---- the six-wide walk-only tree (RTBVH_W6, an A/B knob of certified contexts) -----------------
-// Item p of w6 (64 B): a node -- words 0-2 the grid origin, 3 the step exponents ex | ey << 8 | ez << 16 (all 0: no
-// grid, the certified walk flags the ray), 4 the margin codes (margin.h: ce | ct << 16), 5 k: its n entries are
-// items 6k .. 6k+n-1, 6-11 the lo / hi bytes of entries 0-3 per axis (x lo, x hi, y lo, y hi, z lo, z hi), 12-14
-// entries 4-5 per axis {lo4, lo5, hi4, hi5}, 15 the entries' leaf mask | n << 8 -- or a leaf: words 0-9 of its leaf
-// record (v0, e1, e2, the triangle word) and 10 its sorted index j.  The root node is item 6(T-1).  Node k's
-// entries: its two children, the largest-area internal entry among the first five expanded into its children,
-// four times (greedy_qnode_words's rule, six wide).  This first form builds it after the build, from the
-// topology, the node boxes and the QNodes' margin codes (all of them written: RTBVH_QSKIP=0): w6s[k] holds node
-// k's item, and every node copies its entries' items into its six slots.
-struct W6E {
-    uint32_t id;
-    float b[6];
-};
-__device__ __forceinline__ void w6_sel(W6E& d, const W6E& s, bool take) {
-    d.id = take ? s.id : d.id;
-#pragma unroll
-    for (int q = 0; q < 6; q++) d.b[q] = take ? s.b[q] : d.b[q];
-}
-__device__ __forceinline__ void w6_entries(const BuildArgs& a, uint32_t k, W6E (&E)[6], uint32_t& n) {
-    const uint4 t = a.topo[k];
-    E[0].id = t.x;
-    child_box(a, t.x, E[0].b);
-    E[1].id = t.y;
-    child_box(a, t.y, E[1].b);
-#pragma unroll
-    for (int m = 2; m < 6; m++) E[m] = E[0];
-    n = 2;
-#pragma unroll
-    for (int step = 0; step < 4; step++) {
-        int pick = -1;
-        float best = -1.f;
-#pragma unroll
-        for (int m = 0; m < 5; m++) {
-            if ((uint32_t)m < n && !(E[m].id & LEAF_BIT)) {
-                const float ar = half_area(E[m].b);
-                if (ar > best) { best = ar; pick = m; }
-            }
-        }
-        if (pick < 0) break;
-        W6E sel = E[0];
-#pragma unroll
-        for (int m = 1; m < 5; m++) w6_sel(sel, E[m], m == pick);
-        const uint4 st = a.topo[sel.id];
-        W6E c0, c1;
-        c0.id = st.x;
-        child_box(a, st.x, c0.b);
-        c1.id = st.y;
-        child_box(a, st.y, c1.b);
-#pragma unroll
-        for (int m = 0; m < 5; m++) w6_sel(E[m], c0, m == pick);
-#pragma unroll
-        for (int m = 2; m < 6; m++) w6_sel(E[m], c1, (uint32_t)m == n);
-        ++n;
-    }
-}
-// one axis of a six-entry grid (quantize_axis, six boxes; the absent ones repeat entry 0): the exponent byte
-// (0: no finite frame) and the bytes
-__device__ __forceinline__ uint32_t w6_axis(const float (&lo)[6], const float (&hi)[6], float& org, uint32_t (&bl)[6],
-                                            uint32_t (&bh)[6]) {
-    float o = lo[0], m = hi[0];
-#pragma unroll
-    for (int c = 1; c < 6; c++) {
-        o = fminf(o, lo[c]);
-        m = fmaxf(m, hi[c]);
-    }
-    const float ext = m - o;
-    org = o;
-    if (!(fabsf(o) <= 0x1p100f && fabsf(m) <= 0x1p100f && ext <= 0x1p100f)) return 0u;
-    int e = -120;
-    if (ext > 0.f) {
-        const int E = (int)((__float_as_uint(ext) >> 23) & 255u) - 127;
-        e = max(E - 8, -120);
-    }
-    while (fmaf(255.f, pow2f(e), o) < m) ++e;
-    const float sc = pow2f(e), rs = pow2f(-e);
-#pragma unroll
-    for (int c = 0; c < 6; c++) {
-        uint32_t l = (uint32_t)fminf(fmaxf(floorf((lo[c] - o) * rs), 0.f), 255.f);
-        uint32_t h = (uint32_t)fminf(fmaxf(ceilf((hi[c] - o) * rs), 0.f), 255.f);
-        if (l > 0 && fmaf((float)l, sc, o) > lo[c]) --l;
-        if (h < 255 && fmaf((float)h, sc, o) < hi[c]) ++h;
-        bl[c] = l;
-        bh[c] = h;
-    }
-    return (uint32_t)(e + 127);
-}
-__global__ __launch_bounds__(BLOCK) void k_w6_stage(BuildArgs a, uint4* __restrict__ w6s) {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k + 1 >= a.T) return;
-    W6E E[6];
-    uint32_t n;
-    w6_entries(a, k, E, n);
-    uint32_t w[16];
-    uint32_t ex = 0, lmask = 0;
-    bool grid = true;
-#pragma unroll
-    for (int ax = 0; ax < 3; ax++) {
-        float lo[6], hi[6], org;
-        uint32_t bl[6], bh[6];
-#pragma unroll
-        for (int c = 0; c < 6; c++) {
-            lo[c] = E[c].b[ax];
-            hi[c] = E[c].b[3 + ax];
-        }
-        const uint32_t eb = w6_axis(lo, hi, org, bl, bh);
-        grid = grid && eb != 0u;
-        ex |= eb << (8 * ax);
-        w[ax] = __float_as_uint(org);
-        w[6 + 2 * ax] = bl[0] | bl[1] << 8 | bl[2] << 16 | bl[3] << 24;
-        w[7 + 2 * ax] = bh[0] | bh[1] << 8 | bh[2] << 16 | bh[3] << 24;
-        w[12 + ax] = bl[4] | bl[5] << 8 | bh[4] << 16 | bh[5] << 24;
-    }
-    // the margin codes of node k's QNode (scl[1], scl[2] low 16 bits; none without a grid)
-    const uint4 qw = reinterpret_cast<const uint4*>(a.qnode + slot_of(a.pint[k], a.T))[1];
-    const bool qgrid = __uint_as_float(reinterpret_cast<const uint4*>(a.qnode + slot_of(a.pint[k], a.T))[0].w) != 0.f;
-    w[3] = grid && qgrid ? ex : 0u;
-    w[4] = (qw.x & 0xFFFFu) | (qw.y & 0xFFFFu) << 16;
-    w[5] = k;
-#pragma unroll
-    for (int m = 0; m < 6; m++) lmask |= ((uint32_t)m < n && (E[m].id & LEAF_BIT)) ? 1u << m : 0u;
-    w[15] = lmask | n << 8;
-    uint4* d = w6s + 4 * (size_t)k;
-    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    d[2] = make_uint4(w[8], w[9], w[10], w[11]);
-    d[3] = make_uint4(w[12], w[13], w[14], w[15]);
-}
-__global__ __launch_bounds__(BLOCK) void k_w6_fill(BuildArgs a, const uint4* __restrict__ w6s, uint4* __restrict__ w6) {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k + 1 >= a.T) return;
-    W6E E[6];
-    uint32_t n;
-    w6_entries(a, k, E, n);
-#pragma unroll
-    for (int m = 0; m < 6; m++) {
-        if ((uint32_t)m >= n) break;
-        uint4* d = w6 + 4 * (6 * (size_t)k + m);
-        const uint32_t id = E[m].id;
-        if (id & LEAF_BIT) {
-            const uint32_t j = id & ~LEAF_BIT;
-            const uint4* r = reinterpret_cast<const uint4*>(a.leaf + 4 * (size_t)j);
-            const uint4 r0 = r[0], r1 = r[1], r2 = r[2];
-            d[0] = r0;
-            d[1] = r1;
-            d[2] = make_uint4(r2.x, r2.y, j, 0u);
-            d[3] = make_uint4(0u, 0u, 0u, 0u);
-        } else {
-            const uint4* src = w6s + 4 * (size_t)id;
-            d[0] = src[0]; d[1] = src[1]; d[2] = src[2]; d[3] = src[3];
-        }
-    }
-    if (k == 0) {   // the root (Karras node 0)
-        uint4* d = w6 + 4 * (6 * (size_t)(a.T - 1));
-        d[0] = w6s[0]; d[1] = w6s[1]; d[2] = w6s[2]; d[3] = w6s[3];
-    }
-}
-
-// rtbvh_compute_bvh with the binned primary pass: the climb of the build's crossing nodes runs in
-// the launch of the pass's count pass, which reads only what k_refit wrote (leaf footprints, the depth
-// range): blocks [0, ntail) climb (k_refit_top's work), the rest count.  k_qnodes_cross follows as
-// its own launch (fused into the fill pass its 81 VGPRs held that pass to 5 waves per SIMD); the
+// rtbvh_compute_bvh with the binned primary pass: k_refit_group's listed crossing nodes are quantized in the
+// launch of the pass's count pass, which reads only what k_refit wrote (leaf footprints, the depth range); the
 // gated walk and the bounce walk, which read the whole tree, come after both.
 #include "pb_bin.h"
-__global__ __launch_bounds__(BLOCK) void k_pb_count_top(BuildArgs b, TraceArgs a, uint32_t ntail,
-                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
-                                                        uint4* __restrict__ bins, uint32_t cap, uint32_t ntx) {
-    if (blockIdx.x < ntail) {
-        for_crossing(b, [&](uint32_t k) { refit_top_node(b, k); }, blockIdx.x);
-        return;
-    }
-    pb_bin_block<false>(a, blockIdx.x - ntail, off, cur, bins, cap, ntx);
-}
-// ... and after k_refit_group (the grouped climb, its own launch): blocks [0, nlate) quantize the crossing nodes it
-// listed (k_qnodes_late's work) beside the count.  (8 waves per SIMD, the QNode blocks spilling: 89 us against 98 at
-// the QNode code's 84 VGPRs, 5 waves; k_refit_group + this 162 us against k_pb_count_top + k_qnodes_cross 194, r06_o)
+// After k_refit_group (the grouped climb, its own launch): blocks [0, nlate) quantize the crossing nodes it listed
+// (k_qnodes_late's work) beside the count.  (8 waves per SIMD, the QNode blocks spilling: 89 us against 98 at
+// the QNode code's 84 VGPRs, 5 waves; k_refit_group + this 162 us against round 5's one global climb in the count launch + its QNodes 194, r06_o)
 __global__ __launch_bounds__(BLOCK, 8) void k_pb_count_late(BuildArgs b, TraceArgs a, uint32_t nlate,
                                                          uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
                                                          uint4* __restrict__ bins, uint32_t cap, uint32_t ntx) {
@@ -1930,27 +1755,16 @@ void launch_refit_leaves(const BuildArgs& a, hipStream_t s) {
 void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, uint32_t* cur, uint4* bins, uint32_t cap,
                          uint32_t ntx, uint32_t leaf_blocks, hipStream_t s) {
     const uint32_t nb = refit_blocks(b.T);
-    if (!b.flat_climb && b.qlate) {   // the grouped climb first, then its list's QNodes beside the count
-        const uint32_t nlate = b.T > RBLOCK ? min(1024u, (nb + 15) / 16) : 0u;
-        if (nlate) hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, b);
-        hipLaunchKernelGGL(k_pb_count_late, dim3(nlate + leaf_blocks), dim3(BLOCK), 0, s, b, a, nlate, off, cur, bins, cap,
-                           ntx);
-        return;
-    }
-    const uint32_t ntail = b.T > RBLOCK ? (nb + XWAVES - 1) / XWAVES : 0u;
-    hipLaunchKernelGGL(k_pb_count_top, dim3(ntail + leaf_blocks), dim3(BLOCK), 0, s, b, a, ntail, off, cur, bins, cap, ntx);
-    if (ntail) hipLaunchKernelGGL(k_qnodes_cross, dim3(ntail), dim3(BLOCK), 0, s, b);
+    // the grouped climb first, then its list's QNodes beside the count
+    const uint32_t nlate = b.T > RBLOCK ? min(1024u, (nb + 15) / 16) : 0u;
+    if (nlate) hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, b);
+    hipLaunchKernelGGL(k_pb_count_late, dim3(nlate + leaf_blocks), dim3(BLOCK), 0, s, b, a, nlate, off, cur, bins, cap, ntx);
 }
 void launch_refit_tail(const BuildArgs& a, hipStream_t s) {
     const uint32_t nb = refit_blocks(a.T);
     if (a.T > RBLOCK) {   // the crossing nodes: climbed (in LDS within a group, then across), then quantized
-        if (a.flat_climb || !a.qlate) {
-            hipLaunchKernelGGL(k_refit_top, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
-            hipLaunchKernelGGL(k_qnodes_cross, dim3((nb + XWAVES - 1) / XWAVES), dim3(BLOCK), 0, s, a);
-        } else {
-            hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, a);
-            hipLaunchKernelGGL(k_qnodes_late, dim3(min(1024u, (nb + 15) / 16)), dim3(BLOCK), 0, s, a);
-        }
+        hipLaunchKernelGGL(k_refit_group, dim3((nb + RGROUP - 1) / RGROUP), dim3(GBLOCK), 0, s, a);
+        hipLaunchKernelGGL(k_qnodes_late, dim3(min(1024u, (nb + 15) / 16)), dim3(BLOCK), 0, s, a);
     }
 }
 // leaf j's pseudo-record from its leaf record's box (the bytes k_refit<true> writes)
@@ -1967,11 +1781,6 @@ void launch_pseudo(const BuildArgs& a, hipStream_t s) {
 void launch_refit(const BuildArgs& a, hipStream_t s) {
     launch_refit_leaves(a, s);
     launch_refit_tail(a, s);
-}
-void launch_w6(const BuildArgs& a, uint4* w6s, uint4* w6, hipStream_t s) {
-    if (a.T <= 1) return;
-    hipLaunchKernelGGL(k_w6_stage, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a, w6s);
-    hipLaunchKernelGGL(k_w6_fill, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a, (const uint4*)w6s, w6);
 }
 void launch_records(const BuildArgs& a, hipStream_t s) {
     if (a.T > 1) hipLaunchKernelGGL(k_records, dim3(blocks_for(a.T - 1)), dim3(BLOCK), 0, s, a);

@@ -1,7 +1,7 @@
 #pragma once
 // pb_bin.h -- the binned primary pass's two bin passes (trace.hip k_pb_bin), as a block function
 // over a block index, so that build.hip can run them in one launch beside the build's crossing
-// nodes (rtbvh_compute_bvh: k_pb_count_top, k_pb_fill_cross).  Included inside each file's
+// nodes' QNodes (rtbvh_compute_bvh: k_pb_count_late).  Included inside each file's
 // anonymous namespace, after its BLOCK constant.
 // k of band b in this rank's deal (its compact rows k*8 .. k*8+7), or -1 when another rank has it
 __device__ __forceinline__ int pb_band_pos(const TraceArgs& a, uint32_t b) {

@@ -76,8 +76,6 @@ struct BuildArgs {
     uint32_t pseudo;          // write the leaves' pseudo-records (rec at pleaf[j]; only the packet walks read them)
     uint32_t rec_on;          // write the node records (rec; a certified-only context's build writes none: api.hip)
     uint32_t* qlate;          // [T] or null: k_refit_group's crossing nodes whose QNodes k_qnodes_late builds (count at 0)
-    uint32_t qall;            // k_refit writes every in-block QNode (the six-wide tree's build reads their margin codes)
-    uint32_t flat_climb;      // launch_refit_tail: k_refit_top's one global climb instead of k_refit_group's (A/B)
     float* nbox;              // [6 (T-1)] or null: internal node k's box (min xyz, max xyz) -- what the certified
                               //   walks' reference-order re-traces and the crossing nodes' QNodes read without records
 };
@@ -91,8 +89,6 @@ void launch_refit(const BuildArgs& a, hipStream_t s);
 // leaves' depth range rootbox[6..7]) -- all the binned primary pass reads -- and the crossing nodes
 void launch_refit_leaves(const BuildArgs& a, hipStream_t s);
 void launch_refit_tail(const BuildArgs& a, hipStream_t s);
-// the six-wide walk-only tree (build.hip; RTBVH_W6 contexts): staging w6s [T-1] x 64 B, items w6 [6T-5] x 64 B
-void launch_w6(const BuildArgs& a, uint4* w6s, uint4* w6, hipStream_t s);
 // the leaves' pseudo-records alone, for a tree built without them (a.pseudo = 0)
 void launch_pseudo(const BuildArgs& a, hipStream_t s);
 // size of BuildArgs::xcnt for T leaves
@@ -158,7 +154,6 @@ struct TraceArgs {
     float* refl_rec;          // optional 14-float RayPresent records (reference reflectRay)
     float* refr_rec;          // optional refractRay records
     const QNode* qnode;       // [2T-1] quantized 4-wide nodes in slots (bounce walk mode 4)
-    const uint4* w6;          // or null: the six-wide walk-only tree (build.hip launch_w6), walked by the certified bounce walk
     // N > 1, the binned pass's bins: the leaves whose footprint meets the rank's rows, in PB_LISTS lists (the
     // count pass appends them, the fill pass reads only them; null at N = 1, where every leaf is read):
     // counters PB_LIST_STRIDE words apart, then the lists, pb_list_cap(T) entries each (pb_bin.h)

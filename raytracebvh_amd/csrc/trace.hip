@@ -1658,7 +1658,7 @@ __device__ __forceinline__ void defer_walk_all(uint32_t* __restrict__ next, uint
 #endif
 constexpr uint32_t DEFER_WORKERS = RTBVH_DEFER_WORKERS;
 
-template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false, bool W6 = false>
+template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
@@ -1672,7 +1672,6 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           const float* __restrict__ nbox) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
-    static_assert(!W6 || CERT, "the six-wide tree is walked by the certified walk (qn: its items, build.hip launch_w6)");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
     const uint32_t n = *qin_count;
     if (n == 0) return;
@@ -1859,7 +1858,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     key = NO_HIT;
                     sp = 0;
                     top = INVALID;
-                    node = W6 ? 6 * (T - 1) : root_slot(T);
+                    node = root_slot(T);
                     guard = 2 * T + 2;
                     if (CERT) {   // a ray the margin does not cover is deferred (DEFER_* below)
                         flg = !(qfast && dot(d, d) <= MT_DD);
@@ -1902,75 +1901,6 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                     L = node;
                     node = INVALID;
                 } else {
-                    // W6: a six-wide node (build.hip launch_w6: q0 = origin, exponents; q1 = margin codes, k, x bytes
-                    // of entries 0-3; q2 = y, z bytes; q3 = entries 4-5 per axis {lo4, lo5, hi4, hi5}, leaf mask | n << 8);
-                    // entry m is item 6k + m
-                    if (W6) {
-                        const v4f* rr = reinterpret_cast<const v4f*>(qn + node);
-                        v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
-                        pin(q0); pin(q1); pin(q2); pin(q3);
-                        if (COUNT) c.internal++;
-                        const uint32_t hdr = __float_as_uint(q0.w);
-                        if (hdr == 0u) {   // no finite grid: the ray is flagged for the reference-order re-trace
-                            flg = true;
-                            done = true;
-                        } else {
-                            const float sx = __uint_as_float((hdr & 255u) << 23), sy = __uint_as_float(((hdr >> 8) & 255u) << 23),
-                                        sz = __uint_as_float(((hdr >> 16) & 255u) << 23);
-                            const uint32_t cw = __float_as_uint(q1.x), kb = 6 * __float_as_uint(q1.y);
-                            const uint32_t tl = __float_as_uint(q3.w);
-                            const uint32_t lmask = tl & 63u, nent = (tl >> 8) & 7u;
-                            const float kbb = key_t(key);
-                            const MtNodeRho nr = mt_node_prep(nk, mt_code_val(cw));
-                            const float tcn = mt_code_val(cw >> 16);
-                            const float rr2 = kbb < __builtin_inff() ? mt_node_eval(nr, kbb) : 0.f;
-                            const QAxis X = qaxis<true>(q0.x, sx, __float_as_uint(q1.z), __float_as_uint(q1.w), o.x, inv.x, rr2),
-                                        Y = qaxis<true>(q0.y, sy, __float_as_uint(q2.x), __float_as_uint(q2.y), o.y, inv.y, rr2),
-                                        Z = qaxis<true>(q0.z, sz, __float_as_uint(q2.z), __float_as_uint(q2.w), o.z, inv.z, rr2);
-                            const auto swp = [](uint32_t w, bool sw) { return sw ? (w >> 16 | w << 16) : w; };
-                            const uint32_t p4x = __float_as_uint(q3.x), p4y = __float_as_uint(q3.y), p4z = __float_as_uint(q3.z);
-                            const QAxis X2 = {swp(p4x, inv.x < 0.f), swp(p4x, !(inv.x < 0.f)), X.b, X.an, X.af};
-                            const QAxis Y2 = {swp(p4y, inv.y < 0.f), swp(p4y, !(inv.y < 0.f)), Y.b, Y.an, Y.af};
-                            const QAxis Z2 = {swp(p4z, inv.z < 0.f), swp(p4z, !(inv.z < 0.f)), Z.b, Z.an, Z.af};
-                            const f3 ai = mk(fabsf(inv.x), fabsf(inv.y), fabsf(inv.z));
-                            float kk[6];
-                            uint32_t ii[6];
-                            bool hh[6];
-                            hh[0] = qbox_fast_cert(X, Y, Z, 0, kbb, nk, nr, ai, tcn, kk[0]);
-                            hh[1] = qbox_fast_cert(X, Y, Z, 1, kbb, nk, nr, ai, tcn, kk[1]);
-                            hh[2] = qbox_fast_cert(X, Y, Z, 2, kbb, nk, nr, ai, tcn, kk[2]);
-                            hh[3] = qbox_fast_cert(X, Y, Z, 3, kbb, nk, nr, ai, tcn, kk[3]);
-                            hh[4] = qbox_fast_cert(X2, Y2, Z2, 0, kbb, nk, nr, ai, tcn, kk[4]);
-                            hh[5] = qbox_fast_cert(X2, Y2, Z2, 1, kbb, nk, nr, ai, tcn, kk[5]);
-#pragma unroll
-                            for (int m = 0; m < 6; m++) {
-                                const bool h = hh[m] && (uint32_t)m < nent;
-                                kk[m] = h ? kk[m] : __builtin_inff();
-                                ii[m] = h ? (kb + (uint32_t)m) | (((lmask >> m) & 1u) ? LEAF_BIT : 0u) : INVALID;
-                            }
-                            // a 12-comparator sorting network on six (missing entries last)
-                            sort2(kk[0], ii[0], kk[5], ii[5]); sort2(kk[1], ii[1], kk[3], ii[3]); sort2(kk[2], ii[2], kk[4], ii[4]);
-                            sort2(kk[1], ii[1], kk[2], ii[2]); sort2(kk[3], ii[3], kk[4], ii[4]);
-                            sort2(kk[0], ii[0], kk[3], ii[3]); sort2(kk[2], ii[2], kk[5], ii[5]);
-                            sort2(kk[0], ii[0], kk[1], ii[1]); sort2(kk[2], ii[2], kk[3], ii[3]); sort2(kk[4], ii[4], kk[5], ii[5]);
-                            sort2(kk[1], ii[1], kk[2], ii[2]); sort2(kk[3], ii[3], kk[4], ii[4]);
-                            const bool lf0 = ii[0] != INVALID && (ii[0] & LEAF_BIT);
-                            L = lf0 ? ii[0] : INVALID;
-                            node = lf0 ? ii[1] : ii[0];
-                            if (sp + 5 > limit) {
-                                c.overflow++;
-                                done = true;
-                                flg = true;
-                            } else {
-                                if (ii[5] != INVALID) wpush(ii[5], kk[5]);
-                                if (ii[4] != INVALID) wpush(ii[4], kk[4]);
-                                if (ii[3] != INVALID) wpush(ii[3], kk[3]);
-                                if (ii[2] != INVALID) wpush(ii[2], kk[2]);
-                                if (!lf0 && ii[1] != INVALID) wpush(ii[1], kk[1]);
-                            }
-                        }
-                    } else
-                    {
                     const v4f* rr = reinterpret_cast<const v4f*>(qn + node);
                     v4f q0 = rr[0], q1 = rr[1], q2 = rr[2], q3 = rr[3];
                     pin(q0); pin(q1); pin(q2); pin(q3);
@@ -2002,22 +1932,20 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                         if (i2 != INVALID) wpush(i2, k2);
                         if (!lf0 && i1 != INVALID) wpush(i1, k1);
                     }
-                    }
                 }
 #ifdef RTBVH_DEBUG_PIXEL
                 if (COUNT && L != INVALID && qin[r].idx == (uint32_t)RTBVH_DEBUG_PIXEL)
                     printf("DBG %d leaf %x sp %d kb %.6g key %.6g\n", (int)CERT, L, sp, key_t(key), key_t(key));
 #endif
                 if (L != INVALID) {   // branch-free test (the same accept predicate), u64 key minimum
-                    const uint32_t j = L & ~LEAF_BIT;   // (W6: the leaf's item, whose word 10 is its sorted index)
-                    const v4f* lr = W6 ? reinterpret_cast<const v4f*>(qn + j) : reinterpret_cast<const v4f*>(leaf + 4 * (size_t)j);
+                    const uint32_t j = L & ~LEAF_BIT;
+                    const v4f* lr = reinterpret_cast<const v4f*>(leaf + 4 * (size_t)j);
                     v4f la = lr[0], lb = lr[1], lc = lr[2];
                     pin(la); pin(lb); pin(lc);
                     if (COUNT) c.leaf++;
                     const float tw = ray_triangle_flat(o, d, mk(la.x, la.y, la.z), mk(la.w, lb.x, lb.y),
                                                        mk(lb.z, lb.w, lc.x), true);
-                    const uint32_t jk = W6 ? __float_as_uint(lc.z) : j;
-                    const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | jk;
+                    const uint64_t k = tw == -1.f ? ~0ull : (uint64_t)__float_as_uint(tw) << 32 | j;
                     btri = k < key ? __float_as_uint(lc.y) & ~LEAF_BIT : btri;
                     key = k < key ? k : key;
                 }
@@ -2378,23 +2306,18 @@ template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                           float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, uint32_t* defer, hipStream_t s) {
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
-#define RTBVH_BTW(L, G, C, W)                                                                                           \
-    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C, W>), dim3(blocks), dim3(BLOCK), 0, s, a.inner,               \
-                       W ? reinterpret_cast<const QNode*>(a.w6) : a.qnode, a.leaf, a.T, qin, qin_count, perm, hitrec, next, \
-                       a.counters, a.overflow, lim, defer, a.topo, a.nb ? a.nbox : nullptr)
-#define RTBVH_BT(L, G, C) RTBVH_BTW(L, G, C, false)
+#define RTBVH_BT(L, G, C)                                                                                              \
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
+                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, defer, a.topo,            \
+                       a.nb ? a.nbox : nullptr)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
-    if (MODE == 2 && cert && a.w6) {   // (the six-wide tree: RTBVH_W6 contexts)
-        if (guard) RTBVH_BTW(false, true, MODE == 2, MODE == 2);
-        else RTBVH_BTW(false, false, MODE == 2, MODE == 2);
-    } else if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
+    if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
         if (guard) RTBVH_BT(false, true, MODE == 2);
         else RTBVH_BT(false, false, MODE == 2);
     } else if (a.limited) { if (guard) RTBVH_BT(true, true, false); else RTBVH_BT(true, false, false); }
     else { if (guard) RTBVH_BT(false, true, false); else RTBVH_BT(false, false, false); }
 #undef RTBVH_BT
-#undef RTBVH_BTW
 }
 
 }  // namespace

@@ -1,4 +1,5 @@
 # Round 6: rebuilt-frame timelines (AUTO_WALK | GRAPH, scripts/frame_rebuild.py under rocprofv3 --kernel-trace) for
+# (RTBVH_FLAT_CLIMB existed until round 6's r06_o measurement: deleted after it)
 # the env settings in VARIANTS (';'-separated, e.g. "RTBVH_FLAT_CLIMB=0;RTBVH_FLAT_CLIMB=1"), interleaved ROUNDS times
 set -o pipefail
 R=$GRAFT_REPO_ROOT

@@ -1,4 +1,5 @@
 # Round 6: the six-wide walk-only tree (RTBVH_W6=1) against the 4-wide one: certified GPU tests under the knob,
+# (RTBVH_W6 existed at commit 2b9ee26 only: deleted after this measurement)
 # then ROUNDS interleaved ab_trace.py runs (AB_SET=certbase) with the knob off / on
 set -o pipefail
 cd $GRAFT_REPO_ROOT

@@ -1,4 +1,5 @@
 # Round 6: PMC of the certified bounce walk on the six-wide tree (RTBVH_W6=1) against the 4-wide one
+# (RTBVH_W6 existed at commit 2b9ee26 only: deleted after this measurement)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
