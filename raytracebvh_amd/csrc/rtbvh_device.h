@@ -38,7 +38,7 @@
 // libraries built with -DRTBVH_AB_BUILD, which the Makefile refuses for librtbvh.so itself
 #if (defined(RTBVH_BOUNCE_PROBE) || defined(RTBVH_SMALL_PROBE) || defined(RTBVH_DEBUG_PIXEL) || \
      (defined(RTBVH_PROBE_NOREC) && RTBVH_PROBE_NOREC != 0) || \
-     (defined(RTBVH_REFIT_PROBE) && RTBVH_REFIT_PROBE != 0) || \
+     (defined(RTBVH_REFIT_PROBE) && RTBVH_REFIT_PROBE != 0) || defined(RTBVH_TAIL_PROBE) || \
      (defined(RTBVH_PB_PROBE) && RTBVH_PB_PROBE != 0)) && !defined(RTBVH_AB_BUILD)
 #error "probe builds render wrong frames: A/B libraries only (-DRTBVH_AB_BUILD, OUT=<another library>)"
 #endif

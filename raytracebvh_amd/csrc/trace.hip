@@ -1677,6 +1677,9 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     if (n == 0) return;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0, 0, 0};
+#ifdef RTBVH_TAIL_PROBE   // (A/B probe builds: each wave's end of walk, 100-us buckets from its start, into counters[32..63])
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     if (CERT && DEFER_WORKERS && blockIdx.x < DEFER_WORKERS && gridDim.x > 2 * DEFER_WORKERS && threadIdx.x < 64) {
         for (;;) {
             defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c);
@@ -2035,6 +2038,12 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             }
         }
     }
+#ifdef RTBVH_TAIL_PROBE
+    if (lane == 0 && !COUNT) {
+        const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t_start;   // 100 MHz: 10000 ticks = 100 us
+        atomicAdd(&counters[32 + min(31u, (uint32_t)(dt / 10000u))], 1ull);
+    }
+#endif
     if (CERT && RTBVH_DEFER_INWALK) {
         // The deferred rays (the slack test cannot take them) the workers above have not taken yet: once its part
         // of the queue is drained, the wave walks them in the reference order; the hit record says "exact" (t
