@@ -178,7 +178,7 @@ struct rtbvh_ctx {
     // tuning knobs of A/B runs, read once by rtbvh_create (RTBVH_BOUNCE_BLOCKS, RTBVH_OVERLAP,
     // RTBVH_SIDE_PRIORITY): a shipped context does not change its launches per frame
     uint32_t knob_bounce_blocks = 0;
-    bool knob_overlap = false, knob_side_priority = true, knob_keep_records = false;
+    bool knob_overlap = false, knob_side_priority = true, knob_keep_records = false, knob_no_early_shade = false;
     // the band deal of band traces (rtbvh_set_band_deal): rank 0's weight in 1/16 of another rank's
     uint32_t root_share = 16;
     struct DealTab {   // a weighted deal's device table: every rank's bands, then slots[b] = r << 24 | pos
@@ -924,8 +924,12 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             if (refill) {
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[3], sg));
                 uint32_t* nxb = nx + (size_t)NEXT_SEGS * NEXT_STRIDE * b;
+                // a frame one at a time shades its rays in the walk's tail (trace.hip RTBVH_EARLY_SHADE: one C5 frame
+                // 3.44-3.46 -> 3.37-3.40 ms); with frames in flight other frames' kernels fill that tail, and the
+                // shading workgroups cost the in-flight rate 1-3% (r06_x): not then
+                const BounceShade es{q[(b + 1) & 1], &qc[b + 1], b + 1 < bounces, c->d_redo[slot], &qc[17 + b], Pg};
                 launch_bounce_traverse(ag, q[b & 1], &qc[b], perm, count, wk.bounce, hit, nxb, tblocks, sg, cert,
-                                       c->d_defer[slot]);
+                                       c->d_defer[slot], cert && !inflight && !c->knob_no_early_shade ? &es : nullptr);
                 if (tg && b == 0) HIPC(c, hipEventRecord(ev[4], sg));
                 const Redo rd{c->d_redo[slot], &qc[17 + b], c->d_defer[slot], nxb};
                 launch_bounce_shade(ag, q[b & 1], &qc[b], hit, q[(b + 1) & 1], &qc[b + 1], count, b + 1 < bounces,
@@ -1120,6 +1124,7 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
     if (const char* e = getenv("RTBVH_OVERLAP")) c->knob_overlap = atoi(e) != 0;
     if (const char* e = getenv("RTBVH_SIDE_PRIORITY")) c->knob_side_priority = atoi(e) != 0;
     if (const char* e = getenv("RTBVH_KEEP_RECORDS")) c->knob_keep_records = atoi(e) != 0;
+    if (const char* e = getenv("RTBVH_EARLY_SHADE")) c->knob_no_early_shade = atoi(e) == 0;   // (A/B: 0 = off)
     *out = c;
     return RTBVH_OK;
 }

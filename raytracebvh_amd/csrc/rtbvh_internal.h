@@ -241,9 +241,19 @@ constexpr uint32_t DEFER_VALID = 0x80000000u;
 // cert: the certified 4-wide walk (WIDE_QUANTIZED, no stack limit, a clz64 tree), whose hit records flag
 // the rays it cannot vouch for; the shading with a Redo checks each hit's certificate and re-traces
 // the flagged rays in the reference order
+// a certified pass's early shading (trace.hip RTBVH_EARLY_SHADE): the outputs k_bounce_shade writes, and the pass's
+// largest ray count (the shading workgroups of the walk's launch cover it)
+struct BounceShade {
+    RayQ* qout;
+    uint32_t* qout_count;
+    bool emit;
+    uint32_t* redo;
+    uint32_t* redo_count;
+    uint32_t P;
+};
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
-                            hipStream_t s, bool cert = false, uint32_t* defer = nullptr);
+                            hipStream_t s, bool cert = false, uint32_t* defer = nullptr, const BounceShade* es = nullptr);
 void launch_bounce_shade(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const float2* hitrec,
                          RayQ* qout, uint32_t* qout_count, bool count, bool emit, uint32_t P, hipStream_t s,
                          const Redo* redo = nullptr);

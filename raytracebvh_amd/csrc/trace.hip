@@ -735,6 +735,14 @@ __device__ __forceinline__ HitInfo shade_hit(const TraceArgs& a, uint32_t best_l
     return shade_hit_tri(a, __float_as_uint(a.leaf[4 * (size_t)best_leaf + 2].y) & ~LEAF_BIT, o, d, t);
 }
 
+// A hit record written through to memory (agent scope, 8 B): the certified walk's early shading reads and claims
+// records from other XCDs while the walk runs, and a record left dirty in the writer's L2 would be written back over
+// the claim (trace.hip RTBVH_EARLY_SHADE)
+__device__ __forceinline__ void st_hitrec(float2* p, float2 v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                       (unsigned long long)__float_as_uint(v.x) | (unsigned long long)__float_as_uint(v.y) << 32,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // the set lanes of mask below this lane (v_mbcnt: no 64-bit lane mask held in VGPRs)
@@ -1618,7 +1626,7 @@ __device__ __forceinline__ void defer_walk_all(uint32_t* __restrict__ next, uint
                                                const Inner* __restrict__ inner, const uint4* __restrict__ topo,
                                                const float* __restrict__ nbox, const float4* __restrict__ leaf,
                                                uint32_t T, const RayQ* __restrict__ qin, float2* __restrict__ hitrec,
-                                               Counts& c) {
+                                               Counts& c, bool wt) {
     const uint32_t lane = threadIdx.x & 63u;
     for (;;) {
         uint32_t base = 0, m = 0;
@@ -1646,7 +1654,9 @@ __device__ __forceinline__ void defer_walk_all(uint32_t* __restrict__ next, uint
                 e = __hip_atomic_load(defer + base + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             } while (!(e & DEFER_VALID));
             defer[base + lane] = 0u;   // (the list is clean for the next pass)
-            hitrec[e & ~DEFER_VALID] = defer_walk<COUNT>(inner, topo, nbox, leaf, T, qin + (e & ~DEFER_VALID), c);
+            const float2 hv = defer_walk<COUNT>(inner, topo, nbox, leaf, T, qin + (e & ~DEFER_VALID), c);
+            if (wt) st_hitrec(hitrec + (e & ~DEFER_VALID), hv);
+            else hitrec[e & ~DEFER_VALID] = hv;
         }
     }
 }
@@ -1658,6 +1668,21 @@ __device__ __forceinline__ void defer_walk_all(uint32_t* __restrict__ next, uint
 #endif
 constexpr uint32_t DEFER_WORKERS = RTBVH_DEFER_WORKERS;
 
+// Early shading (RTBVH_EARLY_SHADE, certified passes): the walk's launch carries shading workgroups after its
+// persistent ones.  They are dispatched as the walk's workgroups retire -- in the walk's tail -- and each takes 1024
+// queue positions in order: a ray whose hit record is final (the pass's records start "not written yet", k_hit_init)
+// is claimed by a compare-and-swap to "shaded" and shaded there (bounce_shade_ray, k_bounce_shade's work); the
+// pass's k_bounce_shade shades the rest.  So the shading of most rays runs beside the walk's last rays.
+#ifndef RTBVH_EARLY_SHADE
+#define RTBVH_EARLY_SHADE 1
+#endif
+constexpr uint32_t ESHADE_RAYS = 1024;   // queue positions per shading workgroup
+// hit-record words of a certified pass with early shading (RTBVH_EARLY_SHADE): not written yet, and shaded already
+constexpr uint32_t HIT_NOT_READY = 0xFFFFFFFFu, HIT_SHADED = 0xFFFFFFFEu;   // (x words: NaN patterns no walk writes)
+template <bool CERT>
+__device__ __forceinline__ void bounce_shade_ray(const TraceArgs& a, const RayQ* __restrict__ qin, uint32_t i, float2 h2,
+                                                 bool valid, RayQ& e, bool& live, bool& flagged, uint32_t& hits,
+                                                 uint32_t& tex);
 template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
@@ -1669,7 +1694,10 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
                                                           unsigned long long* __restrict__ counters,
                                                           unsigned long long* __restrict__ overflow, int stack_limit,
                                                           uint32_t* __restrict__ defer, const uint4* __restrict__ topo,
-                                                          const float* __restrict__ nbox) {
+                                                          const float* __restrict__ nbox, uint32_t nwalk, TraceArgs ta,
+                                                          RayQ* __restrict__ qout, uint32_t* __restrict__ qout_count,
+                                                          int emit, uint32_t* __restrict__ redo,
+                                                          uint32_t* __restrict__ redo_count) {
     constexpr bool NEAREST = MODE >= 1, WIDE = MODE == 2;
     static_assert(!CERT || (WIDE && !LIM), "the certified walk is the 4-wide one, without a stack limit");
     const int limit = LIM ? stack_limit : WIDE ? STACK4B : STACK_SIZE;
@@ -1677,12 +1705,50 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     if (n == 0) return;
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0, 0, 0};
+    // (early shading on: the hit records are written through to memory, st_hitrec)
+    const bool wt = CERT && RTBVH_EARLY_SHADE && gridDim.x > nwalk;
+    if (CERT && RTBVH_EARLY_SHADE && blockIdx.x >= nwalk) {   // a shading workgroup (early shading, above)
+        const uint32_t b0 = (blockIdx.x - nwalk) * ESHADE_RAYS;
+        uint32_t hits = 0, tex = 0;
+        for (uint32_t base = b0; base < b0 + ESHADE_RAYS && base < n; base += BLOCK) {   // (uniform)
+            const uint32_t i = base + threadIdx.x;
+            bool valid = false;
+            float2 h2 = make_float2(0.f, 0.f);
+            if (i < n) {
+                unsigned long long* hp = reinterpret_cast<unsigned long long*>(hitrec + i);
+                const unsigned long long v = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t xb = (uint32_t)v, yb = (uint32_t)(v >> 32);
+                // final: written, not taken, and not a deferred ray's "deferred" record (its walk writes it again)
+                const bool ready = xb != HIT_NOT_READY && xb != HIT_SHADED &&
+                                   !(xb == 0xFF800000u && yb == (INVALID ^ HIT_FLAG));
+                if (ready) {
+                    unsigned long long exp = v;
+                    valid = __hip_atomic_compare_exchange_strong(
+                        hp, &exp, (unsigned long long)HIT_SHADED | (unsigned long long)yb << 32, __ATOMIC_RELAXED,
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                h2 = make_float2(__uint_as_float(xb), __uint_as_float(yb));
+            }
+            RayQ e;
+            bool live, flagged;
+            uint32_t h1 = 0, t1 = 0;   // (bounce_apply sets them: one ray's)
+            bounce_shade_ray<true>(ta, qin, i, h2, valid, e, live, flagged, h1, t1);
+            hits += h1;
+            tex += t1;
+            const uint32_t rs = wave_append(flagged, redo_count);
+            if (flagged) redo[rs] = i;
+            const uint32_t qs = wave_append(emit && live, qout_count);
+            if (emit && live) qout[qs] = e;
+        }
+        if (COUNT) flush_counts<COUNT>(ta, c, hits, tex, 5);
+        return;
+    }
 #ifdef RTBVH_TAIL_PROBE   // (A/B probe builds: each wave's end of walk, 100-us buckets from its start, into counters[32..63])
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     if (CERT && DEFER_WORKERS && blockIdx.x < DEFER_WORKERS && gridDim.x > 2 * DEFER_WORKERS && threadIdx.x < 64) {
         for (;;) {
-            defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c);
+            defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c, wt);
             // every segment claimed (lane k: segment k's counter past its length): no ray left to defer but
             // those being claimed right now
             bool used = true;
@@ -1694,7 +1760,7 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
             if (__ballot(!used) == 0) break;
             __builtin_amdgcn_s_sleep(64);
         }
-        defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c);
+        defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c, wt);
         if (COUNT) {
             unsigned long long v[2] = {c.internal, c.leaf};
 #pragma unroll
@@ -1868,7 +1934,9 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
                         if (flg) {
                             // the "deferred" record first, then the entry with release order: a wave that takes
                             // the entry (acquire) writes the walk's record after this one, never under it
-                            hitrec[r] = make_float2(-__builtin_inff(), __uint_as_float(INVALID ^ HIT_FLAG));
+                            const float2 mk_def = make_float2(-__builtin_inff(), __uint_as_float(INVALID ^ HIT_FLAG));
+                            if (wt) st_hitrec(hitrec + r, mk_def);
+                            else hitrec[r] = mk_def;
                             const uint32_t k = atomicAdd(next + DEFER_COUNT, 1u);
                             __hip_atomic_store(defer + k, r | DEFER_VALID, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                             has = false;
@@ -2026,7 +2094,8 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
             if (WIDE) {
                 uint32_t w = key != NO_HIT ? btri : INVALID;
                 if (CERT && flg) w ^= HIT_FLAG;   // (a hit: bit 30 set; a miss: bit 30 cleared)
-                hitrec[r] = make_float2(key_t(key), __uint_as_float(w));
+                if (CERT && wt) st_hitrec(hitrec + r, make_float2(key_t(key), __uint_as_float(w)));
+                else hitrec[r] = make_float2(key_t(key), __uint_as_float(w));
             }
             else hitrec[r] = make_float2(best, __uint_as_float(hit ? btri : INVALID));
             has = false;
@@ -2049,7 +2118,7 @@ ray_box(o, inv, qdecode(ox, sx, lx, c), qdecode(oy, sy, ly, c), qdecode(oz, sz, 
         // of the queue is drained, the wave walks them in the reference order; the hit record says "exact" (t
         // negated), so k_bounce_shade shades it without a certificate.  A deferred ray no wave takes here
         // (appended after the waves looked) is re-traced by k_bounce_redo.
-        defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c);
+        defer_walk_all<COUNT>(next, defer, inner, topo, nbox, leaf, T, qin, hitrec, c, wt);
     }
     if (COUNT || __ballot(c.overflow != 0)) {
         unsigned long long v[3] = {c.internal, c.leaf, c.overflow};
@@ -2125,8 +2194,32 @@ __device__ __forceinline__ bool leaf_certified(const TraceArgs& a, uint32_t tri,
     return ray_box(o, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, true, t, tm);
 }
 
-// RayTraceReflection.hlsl:19-60 for every queued ray, from its hit record.  CERT: a ray whose walk
-// flagged it or whose hit fails the certificate goes to the re-trace list (redo) instead
+// RayTraceReflection.hlsl:19-60 for queued ray i from its hit record h2 (valid: i is a ray to shade now).  CERT: a ray
+// whose walk flagged it or whose hit fails the certificate is flagged (the caller lists it for the re-trace) instead
+template <bool CERT>
+__device__ __forceinline__ void bounce_shade_ray(const TraceArgs& a, const RayQ* __restrict__ qin, uint32_t i, float2 h2,
+                                                 bool valid, RayQ& e, bool& live, bool& flagged, uint32_t& hits,
+                                                 uint32_t& tex) {
+    live = false;
+    flagged = false;
+    if (!valid) return;
+    e = qin[i];
+    uint32_t tri = __float_as_uint(h2.y);
+    bool skip = false;
+    if (CERT) {
+        flagged = hit_flagged(tri);
+        tri = (tri & LEAF_BIT) ? INVALID : tri & ~HIT_FLAG;
+        if (signbit(h2.x)) {   // the walk's deferred rays (trace.hip DEFER_*): walked in the reference order
+            skip = flagged;    //   by the walk's drained waves (exact: shaded as is), or by k_bounce_redo
+            flagged = false;
+            h2.x = -h2.x;
+        } else if (!flagged && tri != INVALID) {
+            const f3 d = mk(e.dx, e.dy, e.dz);
+            flagged = !leaf_certified(a, tri, mk(e.ox, e.oy, e.oz), mk(1.f / d.x, 1.f / d.y, 1.f / d.z), h2.x);
+        }
+    }
+    if (!flagged && !skip) live = bounce_apply(a, e, tri, h2.x, hits, tex);
+}
 template <bool COUNT, bool CERT>
 __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ* __restrict__ qin,
                                                         const uint32_t* __restrict__ qin_count,
@@ -2139,25 +2232,11 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
     bool live = false, flagged = false;
     uint32_t hits = 0, tex = 0;
     RayQ e;
-    if (i < n) {
-        e = qin[i];
-        float2 h2 = hitrec[i];
-        uint32_t tri = __float_as_uint(h2.y);
-        bool skip = false;
-        if (CERT) {
-            flagged = hit_flagged(tri);
-            tri = (tri & LEAF_BIT) ? INVALID : tri & ~HIT_FLAG;
-            if (signbit(h2.x)) {   // the walk's deferred rays (trace.hip DEFER_*): walked in the reference order
-                skip = flagged;    //   by the walk's drained waves (exact: shaded as is), or by k_bounce_redo
-                flagged = false;
-                h2.x = -h2.x;
-            } else if (!flagged && tri != INVALID) {
-                const f3 d = mk(e.dx, e.dy, e.dz);
-                flagged = !leaf_certified(a, tri, mk(e.ox, e.oy, e.oz), mk(1.f / d.x, 1.f / d.y, 1.f / d.z), h2.x);
-            }
-        }
-        if (!flagged && !skip) live = bounce_apply(a, e, tri, h2.x, hits, tex);
-    }
+    float2 h2 = make_float2(0.f, 0.f);
+    if (i < n) h2 = hitrec[i];
+    // (a ray the walk's early shading took is done: RTBVH_EARLY_SHADE)
+    bounce_shade_ray<CERT>(a, qin, i, h2, i < n && !(CERT && __float_as_uint(h2.x) == HIT_SHADED), e, live, flagged, hits,
+                           tex);
     if (CERT) {
         const uint32_t slot = wave_append(flagged, redo_count);
         if (flagged) redo[slot] = i;
@@ -2168,6 +2247,12 @@ __global__ __launch_bounds__(BLOCK) void k_bounce_shade(TraceArgs a, const RayQ*
         Counts c = {0, 0, 0, 0, 0};
         flush_counts<COUNT>(a, c, hits, tex, 5);
     }
+}
+// (early shading: every hit record of the pass "not written yet" before the walk)
+__global__ __launch_bounds__(BLOCK) void k_hit_init(float2* __restrict__ hitrec, const uint32_t* __restrict__ qin_count) {
+    const uint32_t n = *qin_count;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK)
+        hitrec[i] = make_float2(__uint_as_float(HIT_NOT_READY), __uint_as_float(HIT_NOT_READY));
 }
 
 // The reference-order re-trace of the rays a certified bounce pass flagged (redo: queue indices): the
@@ -2313,12 +2398,18 @@ void launch_primary_c(const TraceArgs& a, RayQ* q, uint32_t* qcount, bool count,
 
 template <bool COUNT, int MODE>
 void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
-                          float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, uint32_t* defer, hipStream_t s) {
+                          float2* hitrec, uint32_t* next, uint32_t blocks, bool cert, uint32_t* defer, hipStream_t s,
+                          const BounceShade* es) {
     const int lim = MODE == 2 ? a.stack_limit4b : a.stack_limit;
+    // early shading (certified passes, es): the hit records start "not written yet", shading workgroups follow the walk's
+    const bool early = RTBVH_EARLY_SHADE && MODE == 2 && cert && es;
+    const uint32_t nshade = early ? (es->P + ESHADE_RAYS - 1) / ESHADE_RAYS : 0u;
+    if (early) hipLaunchKernelGGL(k_hit_init, dim3(1024), dim3(BLOCK), 0, s, hitrec, qin_count);
 #define RTBVH_BT(L, G, C)                                                                                              \
-    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks), dim3(BLOCK), 0, s, a.inner, a.qnode, a.leaf, \
-                       a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, defer, a.topo,            \
-                       a.nb ? a.nbox : nullptr)
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks + nshade), dim3(BLOCK), 0, s, a.inner, a.qnode,   \
+                       a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, defer, a.topo,    \
+                       a.nb ? a.nbox : nullptr, blocks, a, early ? es->qout : nullptr, early ? es->qout_count : nullptr, \
+                       early ? (int)es->emit : 0, early ? es->redo : nullptr, early ? es->redo_count : nullptr)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
     if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
@@ -2451,9 +2542,9 @@ void launch_bounce_keys(const RayQ* q, const uint32_t* count, const float* box, 
 
 void launch_bounce_traverse(const TraceArgs& a, const RayQ* qin, const uint32_t* qin_count, const uint32_t* perm,
                             bool count, BounceWalk walk, float2* hitrec, uint32_t* next, uint32_t blocks,
-                            hipStream_t s, bool cert, uint32_t* defer) {
+                            hipStream_t s, bool cert, uint32_t* defer, const BounceShade* es) {
     if (blocks == 0) blocks = 2048;
-#define RTBVH_TRAV(C, M) launch_bounce_trav_t<C, M>(a, qin, qin_count, perm, hitrec, next, blocks, cert, defer, s)
+#define RTBVH_TRAV(C, M) launch_bounce_trav_t<C, M>(a, qin, qin_count, perm, hitrec, next, blocks, cert, defer, s, es)
     switch (walk) {
         case BounceWalk::NEAREST: if (count) RTBVH_TRAV(true, 1); else RTBVH_TRAV(false, 1); break;
         case BounceWalk::WIDE_QUANTIZED: if (count) RTBVH_TRAV(true, 2); else RTBVH_TRAV(false, 2); break;
