@@ -747,7 +747,9 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     // < 4M pixels -- with frames in flight the next frame's primary blocks then share the CUs
     // (C5, rank of N=8, three frames in flight: 0.85 -> 0.78 ms per frame) -- and 512 below 3M pixels once
     // frames are in flight on caller streams (round 5, four in flight, `r05_hh`: the N = 8 rank 0.62 -> 0.60
-    // ms per frame, N = 4 1.03 -> 1.00; one frame at a time 512 is slower, 1.13 -> 1.37 ms at N = 8)
+    // ms per frame, N = 4 1.03 -> 1.00; one frame at a time 512 is slower, 1.13 -> 1.37 ms at N = 8); one frame at
+    // a time, 1536 (round 6, with early shading, `r06_bb`: the N = 8 rank 1.198 -> 1.169 ms, N = 4 1.602 -> 1.535;
+    // 768 / 2048 / 3072: 1.29 / 1.23 / 1.36 at N = 8)
 #ifndef RTBVH_BOUNCE_GRID
 #define RTBVH_BOUNCE_GRID (256 * BOUNCE_WAVES)
 #endif
@@ -756,7 +758,7 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
     bool inflight = slot != 0;
     for (uint32_t k = 1; k < rtbvh_ctx::MAXSPLIT && !inflight && !c->capturing; k++)
         inflight = c->slot_busy[k] && hipEventQuery(c->ev_slot[k]) == hipErrorNotReady;
-    uint32_t tblocks = P < (1u << 22) ? (inflight && P < (3u << 20) ? 512 : 1024) : RTBVH_BOUNCE_GRID;
+    uint32_t tblocks = P < (1u << 22) ? (!inflight ? 1536 : P < (3u << 20) ? 512 : 1024) : RTBVH_BOUNCE_GRID;
     if (c->knob_bounce_blocks) tblocks = c->knob_bounce_blocks;   // tuning override (A/B runs)
     if (records) {
         if (c->cap_rec < P) {

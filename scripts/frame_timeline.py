@@ -4,7 +4,9 @@ scripts/frame_rebuild.py: frames split at k_morton (the build's first kernel), a
 kernel of the median frame its start / end relative to the frame start and the idle gap before
 it (the GPU idle between launches; with two streams, idle while neither runs).  Writes JSON.
 
-usage: python scripts/frame_timeline.py run_kernel_trace.csv out.json"""
+A trace frame (scripts/rank_prof.py) splits at k_zero, its first kernel: pass it as the third argument.
+
+usage: python scripts/frame_timeline.py run_kernel_trace.csv out.json [first kernel, default k_morton]"""
 import csv
 import json
 import statistics
@@ -16,7 +18,7 @@ def short(name):
     return name.split("(")[0]
 
 
-def main(src, dst):
+def main(src, dst, first="k_morton"):
     rows = []
     with open(src) as f:
         for r in csv.DictReader(f):
@@ -24,7 +26,7 @@ def main(src, dst):
     rows.sort()
     frames, cur = [], None
     for s, e, n in rows:
-        if n.startswith("k_morton"):
+        if n == first or n.startswith(first + "<"):
             cur = []
             frames.append(cur)
         if cur is not None:
@@ -57,4 +59,4 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
