@@ -11,19 +11,21 @@ __device__ __forceinline__ int pb_band_pos(const TraceArgs& a, uint32_t b) {
     }
     return b % a.nranks == a.rank ? (int)(b / a.nranks) : -1;
 }
-// the rank's compact rows among image rows [y0, y1] (an order-preserving map, so a range [c0, c1])
-__device__ __forceinline__ void pb_rows(const TraceArgs& a, int y0, int y1, int& c0, int& c1) {
+// the rank's compact rows among image rows [y0, y1] (an order-preserving map, so a range [c0, c1]); pos(b) is
+// pb_band_pos(a, b), from the block's LDS copy of the deal (pb_bin_block)
+template <class Pos>
+__device__ __forceinline__ void pb_rows(const TraceArgs& a, int y0, int y1, int& c0, int& c1, const Pos& pos) {
     if (a.nranks == 1 || y0 > y1) { c0 = y0; c1 = y1; return; }
     c0 = 1; c1 = 0;
     const int b0 = y0 >> 3, b1 = y1 >> 3;
     int b = b0;
     for (; b <= b1; b++) {
-        const int k = pb_band_pos(a, (uint32_t)b);
+        const int k = pos((uint32_t)b);
         if (k >= 0) { c0 = b == b0 ? k * 8 + (y0 & 7) : k * 8; break; }
     }
     if (b > b1) return;   // none of the bands is the rank's
     for (b = b1; b >= b0; b--) {
-        const int k = pb_band_pos(a, (uint32_t)b);
+        const int k = pos((uint32_t)b);
         if (k >= 0) { c1 = b == b1 ? k * 8 + (y1 & 7) : k * 8 + 7; break; }
     }
 }
@@ -38,6 +40,10 @@ __device__ __forceinline__ void pb_rows(const TraceArgs& a, int y0, int y1, int&
 // a global atomic of its own (correct either way).
 // (PB_LEAVES, rtbvh_internal.h: leaves per workgroup, 4 per thread)
 constexpr uint32_t PB_HASH = 1024;        // LDS table slots
+// N > 1: the deal's band positions copied to LDS per block (frames of up to 8 * PB_LDS_BANDS rows; taller ones
+// read the deal from memory): pb_rows walks a footprint's bands one by one, and from memory each step was a
+// dependent L2 load (the count pass of an N = 8 rank took longer than N = 1's, which bins 8x the entries)
+constexpr uint32_t PB_LDS_BANDS = 2048;
 constexpr uint32_t PB_EMPTY = 0xFFFFFFFFu;
 __device__ __forceinline__ int pb_slot_of(uint32_t* h_key, uint32_t key, bool insert) {
     uint32_t h = (key * 2654435761u) >> 22;   // 10 bits
@@ -56,6 +62,7 @@ __device__ __forceinline__ void pb_bin_block(const TraceArgs& a, uint32_t bid, u
                                              uint32_t* __restrict__ cur, uint4* __restrict__ bins, uint32_t cap,
                                              uint32_t ntx) {
     __shared__ uint32_t h_key[PB_HASH], h_cnt[PB_HASH], h_base[FILL ? PB_HASH : 1];
+    __shared__ uint16_t s_band[PB_LDS_BANDS];   // N > 1: pb_band_pos of every band, 0xFFFF for another rank's
     // N > 1 (a.pb_list): the count pass appends the rank's leaves to one of PB_LISTS lists (count block bid to
     // list bid % PB_LISTS: one atomic per block on its list's counter), and fill block bid takes the 1024
     // entries at (bid / PB_LISTS) * 1024 of list bid % PB_LISTS -- blocks past a list's end return at once
@@ -68,6 +75,13 @@ __device__ __forceinline__ void pb_bin_block(const TraceArgs& a, uint32_t bid, u
     const uint32_t lbase = (bid / PB_LISTS) * PB_LEAVES;
     if (FILL && list && lbase >= nlist) return;   // (uniform over the block)
     for (uint32_t i = threadIdx.x; i < PB_HASH; i += BLOCK) { h_key[i] = PB_EMPTY; h_cnt[i] = 0; }
+    const uint32_t nbands = (a.H + 7) >> 3;
+    const bool lds_bands = a.nranks > 1 && nbands <= PB_LDS_BANDS;
+    if (lds_bands)
+        for (uint32_t b = threadIdx.x; b < nbands; b += BLOCK) {
+            const int k = pb_band_pos(a, b);
+            s_band[b] = k < 0 ? (uint16_t)0xFFFFu : (uint16_t)k;
+        }
     __syncthreads();
     constexpr uint32_t LPT = PB_LEAVES / BLOCK;
     uint4 f[LPT];
@@ -89,7 +103,15 @@ __device__ __forceinline__ void pb_bin_block(const TraceArgs& a, uint32_t bid, u
                 const int x0 = max((int)(int16_t)(l.x & 0xFFFFu) + hw, 0), x1 = min((int)(int16_t)(l.x >> 16) + hw, (int)a.W - 1);
                 const int y0 = max((int)(int16_t)(l.y & 0xFFFFu) + hh, 0), y1 = min((int)(int16_t)(l.y >> 16) + hh, (int)a.H - 1);
                 int c0 = 1, c1 = 0;
-                if (x0 <= x1) pb_rows(a, y0, y1, c0, c1);
+                if (x0 <= x1) {
+                    if (lds_bands)
+                        pb_rows(a, y0, y1, c0, c1, [&](uint32_t b) {
+                            const uint32_t v = s_band[b];
+                            return v == 0xFFFFu ? -1 : (int)v;
+                        });
+                    else
+                        pb_rows(a, y0, y1, c0, c1, [&](uint32_t b) { return pb_band_pos(a, b); });
+                }
                 if (x0 <= x1 && c0 <= c1)
                     f[i] = make_uint4((uint32_t)x0 | (uint32_t)x1 << 16, (uint32_t)c0 | (uint32_t)c1 << 16, l.z, l.w);
             }
