@@ -1683,7 +1683,11 @@ template <bool CERT>
 __device__ __forceinline__ void bounce_shade_ray(const TraceArgs& a, const RayQ* __restrict__ qin, uint32_t i, float2 h2,
                                                  bool valid, RayQ& e, bool& live, bool& flagged, uint32_t& hits,
                                                  uint32_t& tex);
-template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false>
+// ES: the instance with early shading (a frame traced one at a time); the walk without it (frames in flight) is its
+// own instance, so that the shading role's registers cost its walk nothing: with the role inlined the walk's loop
+// spills 13 VGPRs (the ES instance still does: its frame is net faster), without it none.  The role as
+// an out-of-line call (1 spill) made the one-frame walk 2.70 -> 3.16 ms (r06_hab3)
+template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false, bool ES = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
                                                           const float4* __restrict__ leaf, uint32_t T,
@@ -1706,8 +1710,8 @@ __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner
     const uint32_t lane = lane_id();
     Counts c = {0, 0, 0, 0, 0};
     // (early shading on: the hit records are written through to memory, st_hitrec)
-    const bool wt = CERT && RTBVH_EARLY_SHADE && gridDim.x > nwalk;
-    if (CERT && RTBVH_EARLY_SHADE && blockIdx.x >= nwalk) {   // a shading workgroup (early shading, above)
+    constexpr bool wt = CERT && ES && RTBVH_EARLY_SHADE;   // (the ES instance is launched with shading workgroups)
+    if (CERT && ES && RTBVH_EARLY_SHADE && blockIdx.x >= nwalk) {   // a shading workgroup (early shading, above)
         const uint32_t b0 = (blockIdx.x - nwalk) * ESHADE_RAYS;
         uint32_t hits = 0, tex = 0;
         for (uint32_t base = b0; base < b0 + ESHADE_RAYS && base < n; base += BLOCK) {   // (uniform)
@@ -2405,19 +2409,25 @@ void launch_bounce_trav_t(const TraceArgs& a, const RayQ* qin, const uint32_t* q
     const bool early = RTBVH_EARLY_SHADE && MODE == 2 && cert && es;
     const uint32_t nshade = early ? (es->P + ESHADE_RAYS - 1) / ESHADE_RAYS : 0u;
     if (early) hipLaunchKernelGGL(k_hit_init, dim3(1024), dim3(BLOCK), 0, s, hitrec, qin_count);
-#define RTBVH_BT(L, G, C)                                                                                              \
-    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C>), dim3(blocks + nshade), dim3(BLOCK), 0, s, a.inner, a.qnode,   \
+#define RTBVH_BTE(L, G, C, E)                                                                                          \
+    hipLaunchKernelGGL((k_bounce_trav<COUNT, MODE, L, G, C, E>), dim3(blocks + nshade), dim3(BLOCK), 0, s, a.inner,         \
+                       a.qnode,                                                                                        \
                        a.leaf, a.T, qin, qin_count, perm, hitrec, next, a.counters, a.overflow, lim, defer, a.topo,    \
                        a.nb ? a.nbox : nullptr, blocks, a, early ? es->qout : nullptr, early ? es->qout_count : nullptr, \
                        early ? (int)es->emit : 0, early ? es->redo : nullptr, early ? es->redo_count : nullptr)
+#define RTBVH_BT(L, G, C) RTBVH_BTE(L, G, C, false)
     // the guard only for a tree that may have cycles (CPUTests delta), or for COUNT's census
     const bool guard = COUNT || !a.acyclic;
-    if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
+    if (MODE == 2 && cert && early) {
+        if (guard) RTBVH_BTE(false, true, MODE == 2, MODE == 2);
+        else RTBVH_BTE(false, false, MODE == 2, MODE == 2);
+    } else if (MODE == 2 && cert) {   // (the certified walk: no stack limit, a clz64 tree -- api.hip enqueue_trace)
         if (guard) RTBVH_BT(false, true, MODE == 2);
         else RTBVH_BT(false, false, MODE == 2);
     } else if (a.limited) { if (guard) RTBVH_BT(true, true, false); else RTBVH_BT(true, false, false); }
     else { if (guard) RTBVH_BT(false, true, false); else RTBVH_BT(false, false, false); }
 #undef RTBVH_BT
+#undef RTBVH_BTE
 }
 
 }  // namespace
