@@ -1684,9 +1684,9 @@ __device__ __forceinline__ void bounce_shade_ray(const TraceArgs& a, const RayQ*
                                                  bool valid, RayQ& e, bool& live, bool& flagged, uint32_t& hits,
                                                  uint32_t& tex);
 // ES: the instance with early shading (a frame traced one at a time); the walk without it (frames in flight) is its
-// own instance, so that the shading role's registers cost its walk nothing: with the role inlined the walk's loop
-// spills 13 VGPRs (the ES instance still does: its frame is net faster), without it none.  The role as
-// an out-of-line call (1 spill) made the one-frame walk 2.70 -> 3.16 ms (r06_hab3)
+// own instance without the shading role's code.  The role's shading spills 13 VGPRs in its own blocks (the walk's
+// loop has none: its scratch accesses are the deep stack's, as in the plain instance); as an out-of-line call it
+// made the one-frame walk 2.70 -> 3.16 ms (r06_hab3)
 template <bool COUNT, int MODE, bool LIM, bool GUARD, bool CERT = false, bool ES = false>
 __global__ __launch_bounds__(BLOCK, BOUNCE_WAVES) void k_bounce_trav(const Inner* __restrict__ inner,
                                                           const QNode* __restrict__ qn,
