@@ -281,6 +281,8 @@ def main():
                     help="nccl = RCCL over xGMI (the bench); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--inflight", type=int, default=4, choices=[1, 2, 3, 4],
                     help="frames in flight per rank (one context + stream each)")
+    ap.add_argument("--timing-in-flight", action="store_true",
+                    help="keep the per-stage HIP events (RTBVH_FLAG_TIMING) in the frames-in-flight loops too (A/B)")
     ap.add_argument("--traversal", default="auto", choices=["auto", "reference"],
                     help="auto: report nearest-first when its frame is identical to the reference order's")
     ap.add_argument("--root-share", type=int, default=None,
@@ -385,8 +387,11 @@ def main():
 
     def timed(flags, inflight=args.inflight):
         """Warm up, then time exactly args.steps steps between barrier + synchronize."""
+        # the per-stage HIP events only one frame at a time (the kernels' durations below); in the frames-in-flight
+        # loops they are host-clock timed and the events' barriers would only add gaps to the stream they land on
+        timing = rt.FLAG_TIMING if inflight == 1 or args.timing_in_flight else 0
         for c in ctxs:
-            c.set_flags(rt.FLAG_TIMING | flags)
+            c.set_flags(timing | flags)
         run(args.warmup, inflight)
         torch.cuda.synchronize()
         st = ctx.stats()
