@@ -1441,6 +1441,33 @@ def test_binned_band_traces_match_oracle(nranks, share):
     np.testing.assert_array_equal(frame, ofb)
 
 
+def test_binned_band_traces_tall_frame():
+    """A frame of more than 16,384 rows (2,048 bands): the bin passes read the deal from memory instead of
+    their per-block LDS copy (pb_bin.h PB_LDS_BANDS); every rank's bands put back give the whole frame."""
+    import torch
+
+    from raytracebvh_amd.tiles import band_row_ids
+    s = rt.synthetic(20_000, seed=0x5EED0004, half_extent=(50.0, 50.0, 50.0))
+    W, H, nranks, share = 24, 16_411, 3, 11
+    wvp, wv = rt.camera_reference(W, H)
+    with rt.Context(device=0, flags=BINNED_FAST) as c:
+        c.set_scene(s)
+        c.set_camera(wvp, wv)
+        c.compute_bvh(W, H, 1)
+        full = c.read_framebuffer()
+        assert (full[..., :3] != 0).any()
+        c.set_band_deal(share)
+        frame = np.zeros_like(full)
+        for r in range(nranks):
+            rows = rt.lib().rtbvh_deal_rows(H, r, nranks, share)
+            buf = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda:0")
+            torch.cuda.synchronize()
+            c.trace_band_async(W, H, 1, r, nranks, buf.data_ptr())
+            c.synchronize()
+            frame[band_row_ids(H, r, nranks, share)] = buf.cpu().numpy()
+    np.testing.assert_array_equal(frame, full)
+
+
 @pytest.mark.parametrize("overlap", ["0", "1"])
 @pytest.mark.parametrize("tris", [3000, 300_000])
 def test_rebuilt_frame_overlap_matches_build_then_trace(tris, overlap, monkeypatch):
