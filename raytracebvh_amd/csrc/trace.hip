@@ -1676,7 +1676,10 @@ constexpr uint32_t DEFER_WORKERS = RTBVH_DEFER_WORKERS;
 #ifndef RTBVH_EARLY_SHADE
 #define RTBVH_EARLY_SHADE 1
 #endif
-constexpr uint32_t ESHADE_RAYS = 1024;   // queue positions per shading workgroup
+#ifndef RTBVH_ESHADE_RAYS
+#define RTBVH_ESHADE_RAYS 1024
+#endif
+constexpr uint32_t ESHADE_RAYS = RTBVH_ESHADE_RAYS;   // queue positions per shading workgroup
 // hit-record words of a certified pass with early shading (RTBVH_EARLY_SHADE): not written yet, and shaded already
 constexpr uint32_t HIT_NOT_READY = 0xFFFFFFFFu, HIT_SHADED = 0xFFFFFFFEu;   // (x words: NaN patterns no walk writes)
 template <bool CERT>
