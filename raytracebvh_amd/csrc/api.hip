@@ -178,7 +178,8 @@ struct rtbvh_ctx {
     // tuning knobs of A/B runs, read once by rtbvh_create (RTBVH_BOUNCE_BLOCKS, RTBVH_OVERLAP,
     // RTBVH_SIDE_PRIORITY): a shipped context does not change its launches per frame
     uint32_t knob_bounce_blocks = 0;
-    bool knob_overlap = false, knob_side_priority = true, knob_keep_records = false, knob_no_early_shade = false;
+    bool knob_overlap = false, knob_side_priority = true, knob_keep_records = false, knob_no_early_shade = false,
+         knob_no_small_tiles = false;
     // the band deal of band traces (rtbvh_set_band_deal): rank 0's weight in 1/16 of another rank's
     uint32_t root_share = 16;
     struct DealTab {   // a weighted deal's device table: every rank's bands, then slots[b] = r << 24 | pos
@@ -901,8 +902,12 @@ rtbvh_status enqueue_walks(rtbvh_ctx* c, uint32_t W, uint32_t H, uint32_t bounce
             if (rows) {
                 const BuildArgs ba = build_args(c);
                 const Redo rd{c->d_redo[b], &qc[16]};
+                // a rank's small pass one frame at a time: 512 threads a tile (its ~1,000 tiles all run at once;
+                // with frames in flight 256 is faster, round 5 r05_jj). Round 6 (r06_stl): the N = 8 rank's frame
+                // 1.13-1.15 -> 1.11 ms; N = 4 (2.1M pixels) the same, N = 2 (4.1M) +0.05 ms: below 1.5M pixels only
+                const bool small_tiles = !inflight && !c->knob_no_small_tiles && (size_t)W * rows < (3u << 19);
                 launch_pb_pass(ag, pb, rows, q[0], &qc[0], count, bounces > 0, true, overlap ? sp : sg,
-                               fuse_tail ? &ba : nullptr, cert ? &rd : nullptr);
+                               fuse_tail ? &ba : nullptr, cert ? &rd : nullptr, small_tiles);
                 if (fuse_tail) tail.pending = false;
                 if (overlap) {
                     HIPC(c, hipEventRecord(c->ev_prim, sp));
@@ -1127,6 +1132,7 @@ rtbvh_status rtbvh_create(const rtbvh_config* cfg, rtbvh_ctx** out) {
     if (const char* e = getenv("RTBVH_SIDE_PRIORITY")) c->knob_side_priority = atoi(e) != 0;
     if (const char* e = getenv("RTBVH_KEEP_RECORDS")) c->knob_keep_records = atoi(e) != 0;
     if (const char* e = getenv("RTBVH_EARLY_SHADE")) c->knob_no_early_shade = atoi(e) == 0;   // (A/B: 0 = off)
+    if (const char* e = getenv("RTBVH_PB_SMALL_TILES")) c->knob_no_small_tiles = atoi(e) == 0;   // (A/B: 0 = off)
     *out = c;
     return RTBVH_OK;
 }

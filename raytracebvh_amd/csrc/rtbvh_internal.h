@@ -208,7 +208,8 @@ void launch_primary_binned(const TraceArgs& a, const PrimBins& pb, uint32_t rows
 // the overflowed tiles (the whole BVH)
 // redo: a certified pass (the shading checks each hit's certificate; the flagged pixels are re-traced)
 void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
-                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail = nullptr, const Redo* redo = nullptr);
+                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail = nullptr, const Redo* redo = nullptr,
+                    bool small_tiles = false);   // (512 threads a tile: a small pass one frame at a time)
 // the count pass of launch_pb_pass with the climb of the build's crossing nodes in the same launch,
 // then their QNodes (build.hip: the build's launch_refit_tail, moved into the frame)
 void launch_pb_count_top(const BuildArgs& b, const TraceArgs& a, uint32_t* off, uint32_t* cur, uint4* bins, uint32_t cap,

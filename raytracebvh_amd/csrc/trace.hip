@@ -1009,6 +1009,7 @@ static_assert(PB_TILE == 32, "k_primary_binned: 10-bit pixel indices, 4 x 4 bloc
 #define RTBVH_PB_RASTER_BLOCK 256
 #endif
 constexpr uint32_t PB_RASTER_BLOCK = RTBVH_PB_RASTER_BLOCK;   // threads per tile of k_primary_binned
+constexpr uint32_t PB_RASTER_BLOCK_SMALL = 512;   // ... for a small pass one frame at a time (launch_pb_pass)
 // cost probes (A/B builds only, wrong frames): 1 = no fine phase, 2 = the fine phase's tests skipped
 #ifndef RTBVH_PB_PROBE
 #define RTBVH_PB_PROBE 0
@@ -1027,8 +1028,10 @@ __device__ void pb_shade_tile(const TraceArgs& a, uint32_t rows, KeyAt&& key_at,
 #define RTBVH_PB_WAVES 8   // k_primary_binned's launch bounds: 8 waves per SIMD with 37 VGPRs spilled beat
                                    // 6 (16 spilled) and 5 (none) -- primary pass 0.87-0.89 / 0.91-0.93 / 0.98 ms
 #endif
-template <bool COUNT, bool CERT = false, bool FUSE = false, bool REC = true>
-__global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
+// RB: threads per tile -- PB_RASTER_BLOCK, or PB_RASTER_BLOCK_SMALL for a small pass traced one frame at a time
+// (api.hip: a rank's ~1,000 tiles then all run at once, and more waves per tile shorten the longest tile)
+template <bool COUNT, bool CERT = false, bool FUSE = false, bool REC = true, uint32_t RB = PB_RASTER_BLOCK>
+__global__ __launch_bounds__(RB, RTBVH_PB_WAVES) void k_primary_binned(TraceArgs a, const uint32_t* __restrict__ off,
                                                              const uint4* __restrict__ bins, uint32_t cap,
                                                              uint32_t ntx, uint32_t rows,
                                                              unsigned long long* __restrict__ keys, RayQ* __restrict__ q,
@@ -1037,7 +1040,7 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_bin
                                                              uint32_t* __restrict__ redo_count) {
     __shared__ unsigned long long s_key[PB_TILE * PB_KS];
     __shared__ float s_bmax[(PB_TILE / 8) * (PB_TILE / 8)];
-    __shared__ uint32_t s_q[PB_RASTER_BLOCK / 64][PB_QCAP];
+    __shared__ uint32_t s_q[RB / 64][PB_QCAP];
     __shared__ uint32_t s_next;
     const uint32_t* s_t = reinterpret_cast<const uint32_t*>(s_key);   // [2 slot + 1]: a pixel's bound (t bits)
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -1050,7 +1053,7 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_bin
 #endif
     // keys of the pixels outside the frame (or the rank's rows) start at t = 0: no entry covers them,
     // and they never raise a block's largest bound
-    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_KS; i += PB_RASTER_BLOCK)
+    for (uint32_t i = threadIdx.x; i < PB_TILE * PB_KS; i += RB)
         s_key[i] = X0 + i % PB_KS < a.W && C0 + i / PB_KS < rows ? NO_HIT : 0ull;
     if (threadIdx.x < (PB_TILE / 8) * (PB_TILE / 8)) s_bmax[threadIdx.x] = INFINITY;
     if (threadIdx.x == 0) s_next = 0;
@@ -1190,12 +1193,12 @@ __global__ __launch_bounds__(PB_RASTER_BLOCK, RTBVH_PB_WAVES) void k_primary_bin
         __shared__ uint32_t s_cnt[(PB_TILE / 8) * (PB_TILE / 8)];
         __shared__ uint64_t s_mask[2 * (PB_TILE / 8) * (PB_TILE / 8)];
         __shared__ uint32_t s_base;
-        pb_shade_tile<COUNT, CERT, PB_RASTER_BLOCK, REC>(
+        pb_shade_tile<COUNT, CERT, RB, REC>(
             a, rows, [&](uint32_t crow, uint32_t x) { return s_key[(crow - C0) * PB_KS + (x - X0)]; }, q, qcount, emit,
             redo, redo_count, s_cnt, s_mask, s_base);
     } else {
         // the tile's keys, row segments of 32 pixels
-        for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += PB_RASTER_BLOCK) {
+        for (uint32_t i = threadIdx.x; i < PB_TILE * PB_TILE; i += RB) {
             const uint32_t px = i % PB_TILE, py = i / PB_TILE;
             if (X0 + px < a.W && C0 + py < rows) keys[(size_t)(C0 + py) * a.W + X0 + px] = s_key[py * PB_KS + px];
         }
@@ -2466,7 +2469,7 @@ void launch_zero(const ZeroList& z, hipStream_t s) {
 }
 
 void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ* q, uint32_t* qcount, bool count,
-                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail, const Redo* redo) {
+                    bool emit, bool zeroed, hipStream_t s, const BuildArgs* tail, const Redo* redo, bool small_tiles) {
     if (rows == 0 || a.W == 0 || a.T == 0) return;
     const uint32_t keys = pb.ntx * pb.nty * PB_NZ;
     if (!zeroed) (void)hipMemsetAsync(pb.off, 0, ((size_t)keys + 1) * sizeof(uint32_t), s);
@@ -2487,6 +2490,10 @@ void launch_pb_pass(const TraceArgs& a, const PrimBins& pb, uint32_t rows, RayQ*
         if (rec || !(F))                                                                                            \
             hipLaunchKernelGGL((k_primary_binned<C, R, F, true>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off,     \
                                pb.bins, pb.cap, pb.ntx, rows, pb.keys, q, qcount, (int)emit, rl, rc);               \
+        else if (small_tiles)                                                                                       \
+            hipLaunchKernelGGL((k_primary_binned<C, R, F, false, PB_RASTER_BLOCK_SMALL>), grid,                      \
+                               dim3(PB_RASTER_BLOCK_SMALL), 0, s, a, pb.off, pb.bins, pb.cap, pb.ntx, rows, pb.keys, q, \
+                               qcount, (int)emit, rl, rc);                                                          \
         else                                                                                                        \
             hipLaunchKernelGGL((k_primary_binned<C, R, F, false>), grid, dim3(PB_RASTER_BLOCK), 0, s, a, pb.off,    \
                                pb.bins, pb.cap, pb.ntx, rows, pb.keys, q, qcount, (int)emit, rl, rc);               \
